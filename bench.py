@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident batched Frame parse + checksum verify.
+
+BASELINE.json metric "Mpkt/s + GiB/s device-resident parse+cksum, 64B & IMIX,
+1/2/4/8 MI355X". A step is one pass of the hot path (one nexg_parse_batch
+launch) over one batch of synthetic frames already resident in HBM. Default
+workload = BASELINE configs[1]: 16M x 64-B Eth/IPv4/UDP frames per GPU.
+
+Multi-GPU (torchrun, one process per GPU): each rank regenerates its own
+16M-frame shard from the global index range [rank*F, (rank+1)*F) — weak
+scaling, no data-path collective; only a barrier and a MAX over ranks of the
+elapsed time. value = frames processed by all ranks / max elapsed.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "Mpkt/s + GiB/s device-resident parse+cksum, 64B & IMIX, 1/2/4/8 MI355X"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(batch, workload, count, seconds):
+    """Oracle (C restatement of nex-packet's Frame path + reference-semantic
+    checksums) on the host, 1 thread, over the first `count` frames of the
+    same workload, repeated until ~`seconds` of CPU work."""
+    import numpy as np
+    from nex_amd import abi
+    from oracle import oracle
+    n = min(count, batch.count)
+    if batch.offsets is None:
+        data = batch.data[: n * batch.stride].cpu().numpy()
+        offs, lens, stride = None, None, batch.stride
+        nbytes = n * batch.stride
+    else:
+        offs = batch.offsets[: n + 1].cpu().numpy().astype(np.uint64)
+        data = batch.data[: int(offs[n])].cpu().numpy()
+        lens, stride = None, 0
+        nbytes = int(offs[n] - offs[0])
+    reps, t = 0, 0.0
+    while t < seconds and reps < 1000:
+        t0 = time.perf_counter()
+        oracle.parse_packed(data, offs, lens, stride=stride, nthreads=1)
+        t += time.perf_counter() - t0
+        reps += 1
+    mpps = n * reps / t / 1e6
+    return {"value": round(mpps, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+            "gib_s": round(nbytes * reps / t / 2**30, 3),
+            "sample": f"first {n} frames of the same {workload} workload, {reps} passes "
+                      f"({t:.1f} s), oracle/nex_oracle.c (literal restatement of "
+                      "Frame::try_from_buf + ipv4/udp/tcp/icmp checksum; Rust reference "
+                      "not buildable here)"}
+
+
+def load_traffic(workload, out_kind):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (FETCH_SIZE
+    doubled per the gfx950 correction + WRITE_SIZE), if one exists."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t.get(f"{workload}:{out_kind}")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=["udp64", "imix", "ser"], default="udp64")
+    ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
+    ap.add_argument("--out", choices=["desc", "record"], default="desc")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    from nex_amd import abi, dist
+    from nex_amd.engine import Engine
+
+    rank, world, local = dist.env_rank_world()
+    if world != args.gpus and rank == 0:
+        log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dist.init("nccl")
+    eng = Engine(local)
+    F = args.frames
+    first = rank * F
+    stream = torch.cuda.current_stream(device)
+    out_kind = abi.OUT_DESC if args.out == "desc" else abi.OUT_RECORD
+
+    if args.workload in ("udp64", "imix"):
+        wl = abi.WL_UDP64 if args.workload == "udp64" else abi.WL_IMIX
+        batch = eng.gen_batch(wl, F, first_index=first)
+        torch.cuda.synchronize(device)
+        alg_bytes = batch.total_bytes  # Σ frame_len: every byte is read (L4 checksum)
+        out = torch.empty(F * (8 if out_kind == abi.OUT_DESC else 64), dtype=torch.uint8, device=device)
+
+        def step():
+            eng.parse(batch, out_kind=out_kind, out=out, stream=stream)
+        if args.workload == "udp64":
+            cfg = {"workload": "configs[1]: 16M x 64-B Eth/IPv4/UDP frames per GPU, fixed 64-B "
+                               "stride, device-resident; Frame parse (L2/L3/L4) + IPv4 header and "
+                               "UDP checksum verify -> 8-B descriptor per frame" if F == 16 << 20
+                               else f"{F} x 64-B Eth/IPv4/UDP frames per GPU"}
+        else:
+            cfg = {"workload": f"configs[2]: {F} IMIX frames per GPU (64/576/1500 at 7:4:1, "
+                               "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table"}
+    else:
+        p = eng.gen_udp4_params(F, first_index=first)
+        out = torch.empty(F * 42, dtype=torch.uint8, device=device)
+        alg_bytes = F * 42
+        batch = None
+
+        def step():
+            eng.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=b"\x02\0\0\0\0\1",
+                           dst_mac=b"\x02\0\0\0\0\2", ip_flags=2, out=out, stream=stream)
+        cfg = {"workload": f"configs[3]: build+checksum {F} udp_ping-shape Eth/IPv4/UDP frames "
+                           "(42 B) per GPU from device-resident parameter tuples"}
+
+    cfg.update({"frames_per_gpu": F, "bytes_per_gpu": alg_bytes, "output": args.out,
+                "parallelism": f"{world} ranks x index-range shards, no collective",
+                "seed": hex(abi.DEFAULT_SEED)})
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    dist.barrier(device)
+    torch.cuda.synchronize(device)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    dist.barrier(device)
+    elapsed = dist.max_over_ranks(t1 - t0, device)
+    kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # per launch, on the launch stream
+    total_frames = dist.sum_over_ranks(F, device) * args.steps
+    total_bytes = dist.sum_over_ranks(alg_bytes, device) * args.steps
+
+    if rank != 0:
+        return
+    achieved = alg_bytes / kernel_s / 1e9
+    traffic = load_traffic(args.workload, args.out)
+    res = {
+        "metric": METRIC if args.workload != "ser" else "Mpkt/s build+checksum udp_ping-shape frames",
+        "value": round(total_frames / elapsed / 1e6, 2),
+        "unit": "Mpkt/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: SURVEY.md App. C generator (splitmix64, seed 0x6E6578), generated on device",
+        "config": cfg,
+        "gib_s": round(total_bytes / elapsed / 2**30, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
+                     "kernel_ms": round(kernel_s * 1e3, 4),
+                     "algorithmic_bytes_per_launch": alg_bytes},
+    }
+    if world == 1 and not args.no_cpu_baseline and batch is not None:
+        try:
+            res["cpu_baseline"] = cpu_baseline(batch, args.workload, 1 << 20, args.cpu_seconds)
+        except Exception as e:  # reported, never fatal to the GPU measurement
+            res["cpu_baseline"] = {"value": None, "error": repr(e)}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

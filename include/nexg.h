@@ -1,0 +1,252 @@
+/*
+ * nexg.h — C ABI of the MI355X-native batched packet-dissect + checksum engine.
+ *
+ * This is the drop-in boundary for nex-packet's per-frame hot path
+ * (shellrow/nex, reference mounted at /root/reference). The reference exposes
+ * only a Rust API; each entry point below replaces a family of Rust calls that
+ * the callers (examples/parse_frame.rs, examples/dump.rs, examples/udp_ping.rs)
+ * make one frame at a time:
+ *
+ *   nexg_parse_batch      <- frame::Frame::try_from_buf / try_from_buf_with_mode
+ *                            (nex-packet/src/frame.rs:299, :309) evaluated on N
+ *                            frames, fused with the verification checksums
+ *                            ipv4::checksum (ipv4.rs:932), udp::checksum
+ *                            (udp.rs:443), tcp::checksum (tcp.rs:1207),
+ *                            icmp::checksum (icmp.rs:429), icmpv6::checksum
+ *                            (icmpv6.rs:589).
+ *   nexg_checksum_batch   <- util::checksum (nex-packet/src/util.rs:65) on N
+ *                            independent buffers.
+ *   nexg_build_udp4_batch <- UdpPacketBuilder::build (builder/udp.rs:67) +
+ *                            Ipv4PacketBuilder::to_bytes (builder/ipv4.rs:94,168)
+ *                            + EthernetPacketBuilder::to_bytes
+ *                            (builder/ethernet.rs:68), the udp_ping.rs:68-109
+ *                            composition, on N parameter tuples.
+ *   nexg_gen_frames       <- synthetic workload synthesis;
+ *                            no reference counterpart (bench/test inputs).
+ *
+ * Conventions:
+ *   - Plain C: no exceptions cross the ABI; every call returns an int status
+ *     (NEXG_OK = 0, negative on error) and never aborts.
+ *   - All frame / output buffers are DEVICE pointers owned by the caller;
+ *     work is enqueued on `stream` (a hipStream_t, NULL = default stream) and
+ *     is stream-ordered: the call returns before the kernels finish.
+ *   - One context per device; a context is not thread-safe (the reference's
+ *     RawReceiver is likewise single-consumer, nex-datalink/src/lib.rs:363).
+ *   - Frame-level parse failures are data, not call errors: they are reported
+ *     per frame in the status field (ParseError kinds, parse.rs:51-97).
+ */
+#ifndef NEXG_H
+#define NEXG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NEXG_ABI_VERSION 1
+
+/* ---- call status ------------------------------------------------------ */
+enum {
+    NEXG_OK = 0,
+    NEXG_EINVAL = -1,  /* bad argument (NULL pointer, unsupported layout) */
+    NEXG_ENOMEM = -2,  /* host allocation failed                          */
+    NEXG_EDEVICE = -3, /* HIP device error / not a gfx950 device          */
+    NEXG_ELAUNCH = -4, /* kernel launch failed                            */
+    NEXG_ERANGE = -5   /* BuildError::LengthOverflow (builder/error.rs:8)  */
+};
+
+/* ---- per-frame status: ParseError kind (parse.rs:51-97) --------------- */
+enum {
+    NEXG_FRAME_OK = 0,
+    NEXG_ERR_BUFFER_TOO_SHORT = 1, /* ParseError::BufferTooShort */
+    NEXG_ERR_INVALID_LENGTH = 2,   /* ParseError::InvalidLength  */
+    NEXG_ERR_MALFORMED = 3,        /* ParseError::Malformed      */
+    NEXG_ERR_TRUNCATED = 4,        /* ParseError::Truncated      */
+    NEXG_ERR_BAD_EXTENT = 7        /* caller error: frame extent past data_bytes
+                                      or longer than 65535 bytes (no Frame)   */
+};
+
+/* ---- ParseOption / ParseMode (frame.rs:47-50, parse.rs:34-46) ---------- */
+#define NEXG_PARSE_STRICT 0x1u  /* ParseMode::Strict (default Lenient)        */
+#define NEXG_PARSE_FROM_IP 0x2u /* ParseOption.from_ip_packet (ip_offset used) */
+
+typedef struct nexg_parse_option {
+    uint32_t flags;     /* NEXG_PARSE_* */
+    uint32_t ip_offset; /* ParseOption.offset, used with NEXG_PARSE_FROM_IP */
+} nexg_parse_option;
+
+/* ---- per-frame flags word (shared by nexg_desc and nexg_record) --------
+ * Layer bits mirror the Option<> structure of frame::Frame (frame.rs:21-60).
+ * Checksum bits record the verify semantics DESIGN.md §3 states:
+ *   ip ok  := ipv4::checksum(&Ipv4Packet) == header.checksum
+ *   l4 ok  := {tcp,udp}::checksum(&pkt,&src,&dst) == header.checksum,
+ *             icmp::checksum(&pkt) / icmpv6::checksum(&pkt,&src,&dst) likewise.
+ * Bits 24..26 hold the frame status (NEXG_FRAME_OK / NEXG_ERR_*). */
+#define NEXG_L_ETHERNET (1u << 0)  /* datalink.ethernet is Some            */
+#define NEXG_L_ARP (1u << 1)       /* datalink.arp is Some                 */
+#define NEXG_L_IP (1u << 2)        /* frame.ip is Some (maybe all-None)    */
+#define NEXG_L_IPV4 (1u << 3)      /* ip.ipv4 is Some                      */
+#define NEXG_L_IPV6 (1u << 4)      /* ip.ipv6 is Some                      */
+#define NEXG_L_ICMP (1u << 5)      /* ip.icmp is Some                      */
+#define NEXG_L_ICMPV6 (1u << 6)    /* ip.icmpv6 is Some                    */
+#define NEXG_L_TRANSPORT (1u << 7) /* frame.transport is Some              */
+#define NEXG_L_TCP (1u << 8)       /* transport.tcp is Some                */
+#define NEXG_L_UDP (1u << 9)       /* transport.udp is Some                */
+#define NEXG_C_IP_CHECKED (1u << 10) /* IPv4 header checksum evaluated     */
+#define NEXG_C_IP_OK (1u << 11)      /* ... and equals the stored field    */
+#define NEXG_C_IP_PANIC (1u << 12)   /* ipv4::checksum would panic (Q17)   */
+#define NEXG_C_L4_CHECKED (1u << 13) /* L4 checksum evaluated              */
+#define NEXG_C_L4_OK (1u << 14)      /* ... and equals the stored field    */
+#define NEXG_STATUS_SHIFT 24
+#define NEXG_STATUS(flags) (((flags) >> NEXG_STATUS_SHIFT) & 0x7u)
+
+/* Compact 8-byte result per frame (out_kind NEXG_OUT_DESC). Together with the
+ * frame bytes it determines the whole frame::Frame (nex_amd/frame.py
+ * materialises it): header fields sit at fixed offsets of their layer.
+ * payload_off/len locate Frame.payload inside the frame; an empty payload is
+ * reported as (0, 0). */
+typedef struct nexg_desc {
+    uint32_t flags;
+    uint16_t payload_off;
+    uint16_t payload_len;
+} nexg_desc;
+
+/* Full decoded record per frame (out_kind NEXG_OUT_RECORD), 64 bytes.
+ * Field values are the reference's parsed values (ipv4.rs:510-528,
+ * ipv6.rs:259-268, tcp.rs:820-835, udp.rs:227-235, icmp.rs:188-204,
+ * arp.rs:340-371). Fields of absent layers are 0. */
+typedef struct nexg_record {
+    uint32_t flags;          /* as nexg_desc.flags                              */
+    uint16_t payload_off;    /* Frame.payload offset in the frame               */
+    uint16_t payload_len;    /* Frame.payload length                            */
+    uint16_t packet_len;     /* Frame.packet_len (frame.rs:575)                 */
+    uint16_t ethertype;      /* EtherType value (dummy value when FROM_IP)      */
+    uint16_t l3_off;         /* offset of the IP / ARP header                   */
+    uint16_t l4_off;         /* offset of the TCP/UDP/ICMP header (0 if none)   */
+    uint8_t ip_ver_ihl;      /* v4: version<<4|ihl  v6: version<<4  arp: hlen    */
+    uint8_t ip_tos;          /* v4: dscp<<2|ecn     v6: traffic_class arp: plen  */
+    uint16_t ip_length;      /* v4: total_length (effective, Q5) v6: payload_length */
+    uint32_t ip_word;        /* v4: identification<<16 | flags<<13 | frag_off    */
+                             /* v6: flow_label                                   */
+    uint8_t ip_ttl;          /* v4: ttl   v6: hop_limit                          */
+    uint8_t ip_proto;        /* IpNextProtocol::value() of v4 proto / v6 nh (Q8) */
+    uint8_t ip_nopt;         /* v4: options.len()  v6: extensions.len()          */
+    uint8_t l4_nopt;         /* tcp: options.len()                               */
+    uint32_t ip_src;         /* v4 / arp sender proto addr, as a BE u32 value   */
+    uint32_t ip_dst;         /* v4 / arp target proto addr                       */
+    uint16_t ip_csum;        /* v4 header checksum field                         */
+    uint16_t ip_csum_calc;   /* ipv4::checksum(&pkt) (0 if not evaluated)        */
+    uint16_t l4_csum;        /* tcp/udp/icmp/icmpv6 checksum field               */
+    uint16_t l4_csum_calc;   /* reference checksum of the L4 packet              */
+    uint16_t src_port;       /* tcp/udp source      arp: hardware_type           */
+    uint16_t dst_port;       /* tcp/udp destination arp: protocol_type           */
+    uint16_t l4_length;      /* udp: length  tcp: data_offset*4  arp: operation  */
+    uint8_t l4_type;         /* icmp(v6) type   tcp: flags                       */
+    uint8_t l4_code;         /* icmp(v6) code   tcp: data_offset<<4|reserved     */
+    uint32_t tcp_seq;
+    uint32_t tcp_ack;
+    uint16_t tcp_window;
+    uint16_t tcp_urg;
+} nexg_record;
+
+#define NEXG_OUT_DESC 1
+#define NEXG_OUT_RECORD 2
+
+/* ---- frame batch layout ------------------------------------------------
+ * Frame i occupies data[off(i), off(i)+len(i)):
+ *   offsets == NULL : off(i) = i*stride
+ *   offsets != NULL : off(i) = offsets[i]
+ *   lengths != NULL : len(i) = lengths[i]
+ *   lengths == NULL : len(i) = stride (offsets == NULL)
+ *                     or offsets[i+1]-offsets[i] (offsets has count+1 entries)
+ * Every len(i) must be <= 65535 (frames are at most one IPv4 datagram; the
+ * reference's default read buffer is 4096, nex-datalink/src/lib.rs:229).
+ * data_bytes bounds every device load: no byte at or past data+data_bytes is
+ * read. All pointers are device pointers. */
+typedef struct nexg_frames {
+    const uint8_t* data;
+    uint64_t data_bytes;
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    uint32_t stride;
+    uint32_t reserved;
+    uint64_t count;
+} nexg_frames;
+
+/* ---- context ----------------------------------------------------------- */
+typedef struct nexg_ctx nexg_ctx;
+
+int nexg_abi_version(void);
+const char* nexg_strerror(int status);
+/* Binds `device` (HIP ordinal); fails with NEXG_EDEVICE unless it is gfx950. */
+int nexg_ctx_create(int device, nexg_ctx** out);
+int nexg_ctx_destroy(nexg_ctx* ctx);
+/* Message of the last failing call on ctx ("" if none). */
+const char* nexg_ctx_last_error(const nexg_ctx* ctx);
+/* Number of compute units of the bound device (for grid sizing by callers). */
+int nexg_ctx_cu_count(const nexg_ctx* ctx);
+
+/* ---- hot path ----------------------------------------------------------
+ * Frame::try_from_buf_with_mode on every frame + checksum verification.
+ * out_kind NEXG_OUT_DESC   -> out is nexg_desc[count]
+ * out_kind NEXG_OUT_RECORD -> out is nexg_record[count] */
+int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames,
+                     const nexg_parse_option* option, int out_kind, void* out,
+                     void* stream);
+
+/* util::checksum(buf_i, skipword) for every buffer (util.rs:65-78). */
+int nexg_checksum_batch(nexg_ctx* ctx, const nexg_frames* bufs,
+                        uint32_t skipword, uint16_t* out, void* stream);
+
+/* ---- serialize path (udp_ping.rs:68-109 shape) -------------------------- */
+typedef struct nexg_udp4_build {
+    const uint32_t* src_ip;   /* per frame, IPv4 address as BE u32 value     */
+    const uint32_t* dst_ip;   /* per frame                                    */
+    const uint16_t* src_port; /* per frame, or NULL -> def_src_port           */
+    const uint16_t* dst_port; /* per frame, or NULL -> def_dst_port           */
+    const uint16_t* ip_id;    /* per frame, or NULL -> def_ip_id              */
+    const uint8_t* src_mac;   /* 6 bytes per frame, or NULL -> def_src_mac    */
+    const uint8_t* dst_mac;   /* 6 bytes per frame, or NULL -> def_dst_mac    */
+    const uint8_t* payload;   /* UDP payload shared by all frames (may be NULL) */
+    uint32_t payload_len;
+    uint16_t def_src_port, def_dst_port, def_ip_id;
+    uint8_t def_src_mac[6], def_dst_mac[6];
+    uint8_t ttl;      /* Ipv4PacketBuilder default 64 (builder/ipv4.rs:37)   */
+    uint8_t ip_flags; /* 3-bit flags; udp_ping uses DontFragment = 0b010     */
+    uint8_t dscp_ecn; /* dscp<<2|ecn, builder default 0                      */
+    uint8_t reserved;
+    uint64_t count;
+} nexg_udp4_build;
+
+/* Writes frame i (42 + payload_len bytes) at out + i*out_stride.
+ * NEXG_ERANGE if 28 + payload_len > 65535 (builder/udp.rs:83, ipv4.rs:153). */
+int nexg_build_udp4_batch(nexg_ctx* ctx, const nexg_udp4_build* params,
+                          uint8_t* out, uint32_t out_stride, void* stream);
+
+/* ---- synthetic workloads --------------------------
+ * Frame i of a workload depends only on (seed, first_index + i), so shards
+ * regenerate identically on any GPU count. */
+#define NEXG_WL_UDP64 1 /* 64-B Eth/IPv4/UDP, 1/16 with a flipped checksum bit */
+#define NEXG_WL_IMIX 2  /* 64/576/1500 at 7:4:1 over {v4,v6}x{TCP,UDP,ICMP}   */
+
+/* Frame length of each frame of the workload (device lengths[count]). */
+int nexg_gen_lengths(nexg_ctx* ctx, int workload, uint64_t seed,
+                     uint64_t first_index, uint64_t count, uint32_t* lengths,
+                     void* stream);
+/* Writes frame i at data + offsets[i] (offsets NULL -> i*stride). */
+int nexg_gen_frames(nexg_ctx* ctx, int workload, uint64_t seed,
+                    uint64_t first_index, uint64_t count, uint8_t* data,
+                    const uint64_t* offsets, uint32_t stride, void* stream);
+/* SER parameter tuples: src_ip, dst_ip, src_port, dst_port, ip_id. */
+int nexg_gen_udp4_params(nexg_ctx* ctx, uint64_t seed, uint64_t first_index,
+                         uint64_t count, uint32_t* src_ip, uint32_t* dst_ip,
+                         uint16_t* src_port, uint16_t* dst_port,
+                         uint16_t* ip_id, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NEXG_H */

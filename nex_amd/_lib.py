@@ -1,0 +1,56 @@
+"""Loader for the in-tree HIP library nex_amd/libnexg.so.
+
+The library is the product: there is no CPU fallback. If it is missing the
+import of the engine fails loudly with instructions to build it.
+"""
+import ctypes
+import os
+
+from . import abi
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnexg.so")
+
+_lib = None
+
+
+class NexgLibraryMissing(RuntimeError):
+    pass
+
+
+def load():
+    """Load libnexg.so (after torch, so both share torch's HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NexgLibraryMissing(
+            f"{LIB_PATH} not found: build it with `make -C nex_amd/csrc` "
+            "(or __graft_entry__.build()); nex_amd has no CPU fallback")
+    try:
+        import torch  # noqa: F401  (load torch's libamdhip64 first: one HIP runtime)
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(LIB_PATH)
+    P, I, U32, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
+    sig = {
+        "nexg_abi_version": (I, []),
+        "nexg_strerror": (ctypes.c_char_p, [I]),
+        "nexg_ctx_create": (I, [I, ctypes.POINTER(P)]),
+        "nexg_ctx_destroy": (I, [P]),
+        "nexg_ctx_last_error": (ctypes.c_char_p, [P]),
+        "nexg_ctx_cu_count": (I, [P]),
+        "nexg_parse_batch": (I, [P, ctypes.POINTER(abi.Frames), ctypes.POINTER(abi.ParseOptionC), I, P, P]),
+        "nexg_checksum_batch": (I, [P, ctypes.POINTER(abi.Frames), U32, P, P]),
+        "nexg_build_udp4_batch": (I, [P, ctypes.POINTER(abi.Udp4Build), P, U32, P]),
+        "nexg_gen_lengths": (I, [P, I, U64, U64, U64, P, P]),
+        "nexg_gen_frames": (I, [P, I, U64, U64, U64, P, P, U32, P]),
+        "nexg_gen_udp4_params": (I, [P, U64, U64, U64, P, P, P, P, P, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.nexg_abi_version() != abi.ABI_VERSION:
+        raise RuntimeError("libnexg.so ABI version mismatch; rebuild nex_amd/csrc")
+    _lib = lib
+    return lib

@@ -1,0 +1,123 @@
+"""Python mirror of include/nexg.h: constants, ctypes structs, numpy dtypes.
+
+Layouts here must match include/nexg.h byte for byte; tests/test_abi.py checks
+the sizes against the C compiler's view.
+"""
+import ctypes
+
+import numpy as np
+
+ABI_VERSION = 1
+
+# call status
+OK, EINVAL, ENOMEM, EDEVICE, ELAUNCH, ERANGE = 0, -1, -2, -3, -4, -5
+
+# per-frame status: ParseError kind (nex-packet/src/parse.rs:51-97)
+FRAME_OK = 0
+ERR_BUFFER_TOO_SHORT = 1
+ERR_INVALID_LENGTH = 2
+ERR_MALFORMED = 3
+ERR_TRUNCATED = 4
+ERR_BAD_EXTENT = 7
+
+PARSE_STRICT = 0x1
+PARSE_FROM_IP = 0x2
+
+L_ETHERNET = 1 << 0
+L_ARP = 1 << 1
+L_IP = 1 << 2
+L_IPV4 = 1 << 3
+L_IPV6 = 1 << 4
+L_ICMP = 1 << 5
+L_ICMPV6 = 1 << 6
+L_TRANSPORT = 1 << 7
+L_TCP = 1 << 8
+L_UDP = 1 << 9
+C_IP_CHECKED = 1 << 10
+C_IP_OK = 1 << 11
+C_IP_PANIC = 1 << 12
+C_L4_CHECKED = 1 << 13
+C_L4_OK = 1 << 14
+STATUS_SHIFT = 24
+
+OUT_DESC = 1
+OUT_RECORD = 2
+
+WL_UDP64 = 1
+WL_IMIX = 2
+
+#: seed of the synthetic workloads ("nex")
+DEFAULT_SEED = 0x6E6578
+
+
+def status_of(flags):
+    return (np.asarray(flags) >> STATUS_SHIFT) & 0x7
+
+
+DESC_DTYPE = np.dtype([("flags", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2")])
+assert DESC_DTYPE.itemsize == 8
+
+RECORD_DTYPE = np.dtype([
+    ("flags", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"),
+    ("packet_len", "<u2"), ("ethertype", "<u2"), ("l3_off", "<u2"), ("l4_off", "<u2"),
+    ("ip_ver_ihl", "u1"), ("ip_tos", "u1"), ("ip_length", "<u2"),
+    ("ip_word", "<u4"),
+    ("ip_ttl", "u1"), ("ip_proto", "u1"), ("ip_nopt", "u1"), ("l4_nopt", "u1"),
+    ("ip_src", "<u4"), ("ip_dst", "<u4"),
+    ("ip_csum", "<u2"), ("ip_csum_calc", "<u2"), ("l4_csum", "<u2"), ("l4_csum_calc", "<u2"),
+    ("src_port", "<u2"), ("dst_port", "<u2"), ("l4_length", "<u2"),
+    ("l4_type", "u1"), ("l4_code", "u1"),
+    ("tcp_seq", "<u4"), ("tcp_ack", "<u4"), ("tcp_window", "<u2"), ("tcp_urg", "<u2"),
+])
+assert RECORD_DTYPE.itemsize == 64
+
+
+class Frames(ctypes.Structure):
+    """struct nexg_frames"""
+    _fields_ = [
+        ("data", ctypes.c_void_p),
+        ("data_bytes", ctypes.c_uint64),
+        ("offsets", ctypes.c_void_p),
+        ("lengths", ctypes.c_void_p),
+        ("stride", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("count", ctypes.c_uint64),
+    ]
+
+
+class ParseOptionC(ctypes.Structure):
+    """struct nexg_parse_option"""
+    _fields_ = [("flags", ctypes.c_uint32), ("ip_offset", ctypes.c_uint32)]
+
+
+class Udp4Build(ctypes.Structure):
+    """struct nexg_udp4_build"""
+    _fields_ = [
+        ("src_ip", ctypes.c_void_p),
+        ("dst_ip", ctypes.c_void_p),
+        ("src_port", ctypes.c_void_p),
+        ("dst_port", ctypes.c_void_p),
+        ("ip_id", ctypes.c_void_p),
+        ("src_mac", ctypes.c_void_p),
+        ("dst_mac", ctypes.c_void_p),
+        ("payload", ctypes.c_void_p),
+        ("payload_len", ctypes.c_uint32),
+        ("def_src_port", ctypes.c_uint16),
+        ("def_dst_port", ctypes.c_uint16),
+        ("def_ip_id", ctypes.c_uint16),
+        ("def_src_mac", ctypes.c_uint8 * 6),
+        ("def_dst_mac", ctypes.c_uint8 * 6),
+        ("ttl", ctypes.c_uint8),
+        ("ip_flags", ctypes.c_uint8),
+        ("dscp_ecn", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8),
+        ("count", ctypes.c_uint64),
+    ]
+
+
+#: every symbol include/nexg.h declares (tests check the .so exports them)
+EXPORTED_SYMBOLS = (
+    "nexg_abi_version", "nexg_strerror", "nexg_ctx_create", "nexg_ctx_destroy",
+    "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch",
+    "nexg_build_udp4_batch", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
+)

@@ -1,0 +1,470 @@
+// frame_core.hpp — device-side restatement of nex-packet's Frame semantics
+// (shellrow/nex, nex-packet/src/frame.rs:570-658) fused with the packet-API
+// verification checksums, written for one lane per frame.
+//
+// The reference checksums re-serialised packets (ipv4.rs:231-286 to_bytes,
+// tcp.rs:521-575, udp.rs:52-60) with a u32 word sum (util.rs:65-183). Here no
+// bytes are re-serialised: each checksum is assembled in closed form from
+//   * header words read in place, with the fields to_bytes() rewrites
+//     substituted (IPv4 IHL/total_length/proto value, TCP data offset, UDP
+//     length),
+//   * congruent word sums (mod 0xFFFF) of raw byte ranges (`wsum`), and
+//   * zero padding where to_bytes() pads.
+// A sum T is kept congruent to the reference's u32 sum S modulo 0xFFFF and
+// T == 0 iff S == 0 (every weight is positive), which fixes the fold exactly:
+// finalize(S) == fold16(T) (util.rs:73-78).
+//
+// Accessor F (a frame held partly in LDS, partly in HBM) provides:
+//   u8(i)      byte i of the frame
+//   le_sum(a,b) sum over bytes i in [a,b) of byte * (absolute address of i is
+//              odd ? 256 : 1)   (little-endian halfword sum of the range)
+// From le_sum the big-endian word sum of [a,b) with words starting at a is
+//   a odd  : le_sum(a,b)                 (exactly equal)
+//   a even : le_sum(a,b) * 256           (congruent mod 0xFFFF)
+// since 65536 == 1 (mod 0xFFFF).  `frame_parity` is the absolute-address
+// parity of byte 0, so the parity of byte i is frame_parity ^ (i & 1).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nexg.h"
+
+// Every function is __host__ __device__: the kernels run it on gfx950 and the
+// test-only host harness (tests/native/core_harness.hip) runs the very same
+// code on the CPU for differential testing against the oracle.
+#define NEXG_HD __host__ __device__ __forceinline__
+
+namespace nexg {
+
+// ip.rs:308-456  IpNextProtocol::new(n).value(): 143..=252 and 255 -> 255.
+NEXG_HD uint32_t ip_next_protocol_value(uint32_t n) {
+    return (n <= 142u || n == 253u || n == 254u) ? n : 255u;
+}
+
+// util.rs:73-78 finalize_checksum on a congruent sum (see header comment).
+NEXG_HD uint32_t fold_complement(uint64_t t) {
+    t = (t & 0xFFFFFFFFull) + (t >> 32);
+    t = (t & 0xFFFFFFFFull) + (t >> 32);
+    uint32_t s = (uint32_t)t;
+    s = (s & 0xFFFFu) + (s >> 16);
+    s = (s & 0xFFFFu) + (s >> 16);
+    return (~s) & 0xFFFFu;
+}
+
+template <class F>
+struct FrameOps {
+    const F& f;
+    uint32_t parity;  // absolute-address parity of frame byte 0
+
+    NEXG_HD uint32_t be16(uint32_t i) const {
+        return (f.u8(i) << 8) | f.u8(i + 1);
+    }
+    NEXG_HD uint32_t be32(uint32_t i) const {
+        return (be16(i) << 16) | be16(i + 2);
+    }
+    // big-endian word sum of [a,b) with words aligned at a (congruent form)
+    NEXG_HD uint64_t wsum(uint32_t a, uint32_t b) const {
+        if (a >= b) return 0;
+        uint64_t s = f.le_sum(a, b);
+        return ((parity ^ a) & 1u) ? s : (s << 8);
+    }
+};
+
+NEXG_HD void set_payload(nexg_record& r, uint32_t off, uint32_t len) {
+    r.payload_off = (uint16_t)(len ? off : 0u);
+    r.payload_len = (uint16_t)len;
+}
+
+// ---- frame accessors -----------------------------------------------------
+
+// byte mask of dword at slot/abs position j for the byte range [A,B), j < B
+NEXG_HD uint32_t range_mask(uint64_t j, uint64_t A, uint64_t B) {
+    uint32_t lo = A > j ? (uint32_t)(A - j) : 0u;
+    uint32_t hi = (B - j) < 4u ? (uint32_t)(B - j) : 4u;
+    uint32_t m = hi >= 4u ? 0xFFFFFFFFu : ((1u << (8u * hi)) - 1u);
+    return lo >= 4u ? 0u : (m & (0xFFFFFFFFu << (8u * lo)));
+}
+
+NEXG_HD uint32_t halves(uint32_t w) { return (w & 0xFFFFu) + (w >> 16); }
+
+// little-endian halfword sum of global bytes [A, B) (absolute addresses)
+NEXG_HD uint64_t global_le_sum(uint64_t A, uint64_t B) {
+    uint64_t acc = 0;
+    for (uint64_t d = A & ~15ull; d < B; d += 16) {
+        const uint4 v = *reinterpret_cast<const uint4*>(d);
+        uint32_t s = 0;
+        if (d >= A && d + 16 <= B) {
+            s = halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);
+        } else {
+            if (d + 0 < B) s += halves(v.x & range_mask(d + 0, A, B));
+            if (d + 4 < B) s += halves(v.y & range_mask(d + 4, A, B));
+            if (d + 8 < B) s += halves(v.z & range_mask(d + 8, A, B));
+            if (d + 12 < B) s += halves(v.w & range_mask(d + 12, A, B));
+        }
+        acc += s;
+    }
+    return acc;
+}
+
+// Frame whose bytes [0, wlen) are staged in an LDS slot (byte i at
+// slot[o + i], slot 16-B aligned, o == frame address mod 16) and whose
+// remaining bytes are read from HBM.
+struct WinFrame {
+    const uint8_t* slot;
+    const uint8_t* g;
+    uint32_t o;
+    uint32_t wlen;
+
+    NEXG_HD uint32_t u8(uint32_t i) const {
+        return i < wlen ? (uint32_t)slot[o + i] : (uint32_t)g[i];
+    }
+    NEXG_HD uint64_t le_sum(uint32_t a, uint32_t b) const {
+        uint64_t acc = 0;
+        const uint32_t lb = b < wlen ? b : wlen;
+        if (a < lb) {
+            const uint32_t A = o + a, B = o + lb;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(slot);
+            uint32_t s = 0;
+            for (uint32_t j = A & ~3u; j < B; j += 4) s += halves(w[j >> 2] & range_mask(j, A, B));
+            acc = s;
+        }
+        const uint32_t ga = a > wlen ? a : wlen;
+        if (ga < b) {
+            const uint64_t base = reinterpret_cast<uint64_t>(g);
+            acc += global_le_sum(base + ga, base + b);
+        }
+        return acc;
+    }
+};
+
+// ---- L4 ------------------------------------------------------------------
+
+// frame.rs:550-568 + udp.rs:197-236 (try_from_bytes) + udp.rs:443-505.
+template <class O>
+NEXG_HD void parse_udp(const O& o, uint32_t base, uint32_t n,
+                                          uint64_t pseudo, nexg_record& r) {
+    r.flags |= NEXG_L_TRANSPORT;
+    uint32_t ulen = n >= 8 ? o.be16(base + 4) : 0u;
+    if (n < 8 || ulen < 8u || n < ulen) {  // Q14
+        set_payload(r, base, n);
+        return;
+    }
+    uint32_t sp = o.be16(base), dp = o.be16(base + 2), cs = o.be16(base + 6);
+    r.flags |= NEXG_L_UDP;
+    r.l4_off = (uint16_t)base;
+    r.src_port = (uint16_t)sp;
+    r.dst_port = (uint16_t)dp;
+    r.l4_length = (uint16_t)ulen;
+    r.l4_csum = (uint16_t)cs;
+    // to_bytes(): length word rewritten as 8 + payload.len() == ulen; skipword 3
+    uint64_t t = pseudo + 17u + ulen + sp + dp + ulen + o.wsum(base + 8, base + ulen);
+    uint32_t calc = fold_complement(t);
+    r.l4_csum_calc = (uint16_t)calc;
+    r.flags |= NEXG_C_L4_CHECKED | (calc == cs ? NEXG_C_L4_OK : 0u);
+    set_payload(r, base + 8, ulen - 8);
+}
+
+// frame.rs:530-548 + tcp.rs:731-836 (try_from_bytes) + tcp.rs:1207-1269 over
+// to_bytes() (tcp.rs:521-575): options re-encoded up to the first EOL, zero
+// padded to 4, data offset recomputed; pseudo length = serialised length.
+template <class O>
+NEXG_HD void parse_tcp(const O& o, uint32_t base, uint32_t n,
+                                          uint64_t pseudo, nexg_record& r) {
+    r.flags |= NEXG_L_TRANSPORT;
+    bool ok = n >= 20;
+    uint32_t off_res = ok ? o.f.u8(base + 12) : 0u;
+    uint32_t hl = (off_res >> 4) * 4u;
+    ok = ok && hl >= 20u && n >= hl;
+    uint32_t stop = hl, nopt = 0;
+    if (ok) {
+        uint32_t off = 20;
+        while (off < hl) {
+            uint32_t kind = o.f.u8(base + off);
+            off += 1;
+            if (kind == 0u) {  // EOL: push and stop
+                nopt++;
+                stop = off;
+                break;
+            }
+            if (kind == 1u) {  // NOP
+                nopt++;
+                continue;
+            }
+            if (off >= hl) { ok = false; break; }  // Malformed
+            uint32_t l = o.f.u8(base + off);
+            off += 1;
+            if (l < 2u) { ok = false; break; }  // InvalidLength
+            if (off + (l - 2u) > hl) { ok = false; break; }  // Truncated
+            nopt++;
+            off += l - 2u;
+        }
+    }
+    if (!ok) {  // Q13: transport = Some{None, None}, payload = IP payload
+        set_payload(r, base, n);
+        return;
+    }
+    uint32_t sp = o.be16(base), dp = o.be16(base + 2);
+    uint32_t seq_hi = o.be16(base + 4), seq_lo = o.be16(base + 6);
+    uint32_t ack_hi = o.be16(base + 8), ack_lo = o.be16(base + 10);
+    uint32_t flags = o.f.u8(base + 13);
+    uint32_t win = o.be16(base + 14), cs = o.be16(base + 16), urg = o.be16(base + 18);
+    r.flags |= NEXG_L_TCP;
+    r.l4_off = (uint16_t)base;
+    r.src_port = (uint16_t)sp;
+    r.dst_port = (uint16_t)dp;
+    r.tcp_seq = (seq_hi << 16) | seq_lo;
+    r.tcp_ack = (ack_hi << 16) | ack_lo;
+    r.l4_length = (uint16_t)hl;
+    r.l4_type = (uint8_t)flags;
+    r.l4_code = (uint8_t)off_res;
+    r.tcp_window = (uint16_t)win;
+    r.tcp_urg = (uint16_t)urg;
+    r.l4_nopt = (uint8_t)nopt;
+    r.l4_csum = (uint16_t)cs;
+    uint32_t hl_ser = 20u + ((stop - 20u + 3u) & ~3u);
+    uint32_t len_ser = hl_ser + (n - hl);
+    uint64_t t = pseudo + 6u + len_ser + sp + dp + seq_hi + seq_lo + ack_hi + ack_lo +
+                 ((((hl_ser >> 2) << 4) | (off_res & 0xFu)) << 8 | flags) + win + urg +
+                 o.wsum(base + 20, base + stop) + o.wsum(base + hl, base + n);
+    uint32_t calc = fold_complement(t);
+    r.l4_csum_calc = (uint16_t)calc;
+    r.flags |= NEXG_C_L4_CHECKED | (calc == cs ? NEXG_C_L4_OK : 0u);
+    set_payload(r, base + hl, n - hl);
+}
+
+// frame.rs:624-658 + icmp.rs:188-214 / icmpv6.rs:248-272 (>= 8 bytes,
+// payload = [4..)); icmp.rs:429 checksum(to_bytes, 1) / icmpv6.rs:589.
+template <class O>
+NEXG_HD void parse_icmp(const O& o, uint32_t base, uint32_t n,
+                                           bool v6, uint64_t pseudo, nexg_record& r) {
+    if (n < 8) {  // Q15: icmp = None, payload = IP payload
+        set_payload(r, base, n);
+        return;
+    }
+    uint32_t tc = o.be16(base), cs = o.be16(base + 2);
+    r.flags |= v6 ? NEXG_L_ICMPV6 : NEXG_L_ICMP;
+    r.l4_off = (uint16_t)base;
+    r.l4_type = (uint8_t)(tc >> 8);
+    r.l4_code = (uint8_t)tc;
+    r.l4_csum = (uint16_t)cs;
+    uint64_t t = (v6 ? pseudo + 58u + n : 0ull) + tc + o.wsum(base + 4, base + n);
+    uint32_t calc = fold_complement(t);
+    r.l4_csum_calc = (uint16_t)calc;
+    r.flags |= NEXG_C_L4_CHECKED | (calc == cs ? NEXG_C_L4_OK : 0u);
+    set_payload(r, base + 4, n - 4);
+}
+
+// ---- L3 ------------------------------------------------------------------
+
+// frame.rs:440-483 + ipv4.rs:372-529; ipv4::checksum (ipv4.rs:932-938) over
+// to_bytes()[..ihl*4] with the options canonicalised and total_length
+// rewritten (Q16/Q17).  Returns the strict-mode ParseError kind or 0.
+template <class O>
+NEXG_HD uint32_t parse_ipv4(const O& o, uint32_t l3, uint32_t len,
+                                               bool strict, nexg_record& r) {
+    const uint32_t n = len - l3;
+    r.flags |= NEXG_L_IP;
+    uint32_t err = 0, hl = 0, total = 0;
+    uint32_t b0 = n >= 20u ? o.f.u8(l3) : 0u;
+    if (n < 20u) err = NEXG_ERR_BUFFER_TOO_SHORT;
+    else if ((b0 >> 4) != 4u) err = NEXG_ERR_MALFORMED;
+    else if ((b0 & 15u) < 5u) err = NEXG_ERR_INVALID_LENGTH;
+    else {
+        hl = (b0 & 15u) * 4u;
+        if (hl > n) err = NEXG_ERR_TRUNCATED;
+        else {
+            uint32_t declared = o.be16(l3 + 2);
+            uint32_t eff = declared ? declared : n;
+            if (eff < hl) err = NEXG_ERR_INVALID_LENGTH;
+            else if (strict && eff > n) err = NEXG_ERR_TRUNCATED;
+            else total = eff < n ? eff : n;
+        }
+    }
+    // options walk (ipv4.rs:442-508): stop = end of the re-serialisable prefix
+    uint32_t stop = hl, nopt = 0;
+    if (!err) {
+        uint32_t i = 20;
+        while (i < hl) {
+            uint32_t num = o.f.u8(l3 + i) & 0x1Fu;
+            if (num == 0u) { nopt++; stop = i + 1; break; }  // EOL
+            if (num == 1u) { nopt++; i++; continue; }        // NOP
+            if (i + 2u > hl) {
+                if (strict) err = NEXG_ERR_MALFORMED;
+                stop = i;
+                break;
+            }
+            uint32_t l = o.f.u8(l3 + i + 1);
+            if (l < 2u || i + l > hl) {
+                if (strict) err = NEXG_ERR_INVALID_LENGTH;
+                stop = i;
+                break;
+            }
+            nopt++;
+            i += l;
+        }
+    }
+    if (err) return strict ? err : 0u;  // Q4: ip = Some(all None), payload empty
+
+    uint32_t tos = o.f.u8(l3 + 1);
+    uint32_t id = o.be16(l3 + 4), ff = o.be16(l3 + 6);
+    uint32_t ttl = o.f.u8(l3 + 8), proto = ip_next_protocol_value(o.f.u8(l3 + 9));
+    uint32_t cs = o.be16(l3 + 10);
+    uint32_t s_hi = o.be16(l3 + 12), s_lo = o.be16(l3 + 14);
+    uint32_t d_hi = o.be16(l3 + 16), d_lo = o.be16(l3 + 18);
+    r.flags |= NEXG_L_IPV4;
+    r.ip_ver_ihl = (uint8_t)b0;
+    r.ip_tos = (uint8_t)tos;
+    r.ip_length = (uint16_t)total;
+    r.ip_word = (id << 16) | ff;
+    r.ip_ttl = (uint8_t)ttl;
+    r.ip_proto = (uint8_t)proto;
+    r.ip_nopt = (uint8_t)nopt;
+    r.ip_src = (s_hi << 16) | s_lo;
+    r.ip_dst = (d_hi << 16) | d_lo;
+    r.ip_csum = (uint16_t)cs;
+
+    const uint32_t pay = total - hl;
+    const uint32_t hl_ser = 20u + ((stop - 20u + 3u) & ~3u);
+    if (hl_ser + pay < hl) {
+        r.flags |= NEXG_C_IP_PANIC;  // Q17: bytes[..header_len()] out of range
+    } else {
+        uint32_t tot_ser = hl_ser + pay;
+        tot_ser = tot_ser < 65535u ? tot_ser : 65535u;
+        uint64_t t = (((0x40u | (hl_ser >> 2)) << 8) | tos) + tot_ser + id + ff +
+                     ((ttl << 8) | proto) + s_hi + s_lo + d_hi + d_lo +
+                     o.wsum(l3 + 20, l3 + stop) +
+                     o.wsum(l3 + hl, l3 + hl + (hl - hl_ser));
+        uint32_t calc = fold_complement(t);
+        r.ip_csum_calc = (uint16_t)calc;
+        r.flags |= NEXG_C_IP_CHECKED | (calc == cs ? NEXG_C_IP_OK : 0u);
+    }
+    const uint64_t pseudo = (uint64_t)s_hi + s_lo + d_hi + d_lo;  // util.rs:91-93
+    const uint32_t pb = l3 + hl;
+    if (proto == 6u) parse_tcp(o, pb, pay, pseudo, r);
+    else if (proto == 17u) parse_udp(o, pb, pay, pseudo, r);
+    else if (proto == 1u) parse_icmp(o, pb, pay, false, pseudo, r);
+    else set_payload(r, pb, pay);  // Q9
+    return 0;
+}
+
+// frame.rs:485-528 + ipv6.rs:217-384. Extension chain walked for the payload
+// offset; the Frame dispatches on the raw first next-header (Q10).
+template <class O>
+NEXG_HD uint32_t parse_ipv6(const O& o, uint32_t l3, uint32_t len,
+                                               bool strict, nexg_record& r) {
+    const uint32_t n = len - l3;
+    r.flags |= NEXG_L_IP;
+    if (n < 40u) return strict ? NEXG_ERR_BUFFER_TOO_SHORT : 0u;
+    uint32_t w0 = o.be32(l3);
+    if ((w0 >> 28) != 6u) return strict ? NEXG_ERR_MALFORMED : 0u;
+    uint32_t pl = o.be16(l3 + 4);
+    uint32_t declared = 40u + pl;
+    if (strict && declared > n) return NEXG_ERR_TRUNCATED;
+    uint32_t avail = declared < n ? declared : n;
+    uint32_t first = ip_next_protocol_value(o.f.u8(l3 + 6));
+    uint32_t nh = first, off = 40, next = 0, err = 0;
+    while (nh == 0u || nh == 43u || nh == 44u || nh == 60u) {
+        if (off + 2u > avail) { err = NEXG_ERR_TRUNCATED; break; }
+        uint32_t nh2 = ip_next_protocol_value(o.f.u8(l3 + off));
+        uint32_t el = o.f.u8(l3 + off + 1);
+        if (nh == 44u) {
+            if (off + 8u > avail) { err = NEXG_ERR_TRUNCATED; break; }
+            off += 8u;
+        } else {
+            if (nh == 43u && off + 4u > avail) { err = NEXG_ERR_TRUNCATED; break; }
+            uint32_t tl = 8u + el * 8u;
+            if (off + tl > avail) { err = NEXG_ERR_TRUNCATED; break; }
+            off += tl;
+        }
+        next++;
+        nh = nh2;
+    }
+    if (err) return strict ? err : 0u;  // Q12
+    r.flags |= NEXG_L_IPV6;
+    r.ip_ver_ihl = (uint8_t)((w0 >> 28) << 4);
+    r.ip_tos = (uint8_t)(w0 >> 20);
+    r.ip_length = (uint16_t)pl;
+    r.ip_word = w0 & 0xFFFFFu;
+    r.ip_ttl = (uint8_t)o.f.u8(l3 + 7);
+    r.ip_proto = (uint8_t)first;
+    r.ip_nopt = (uint8_t)(next < 255u ? next : 255u);
+    const uint32_t pb = l3 + off, pay = avail - off;
+    if (first == 6u || first == 17u || first == 58u) {
+        uint64_t pseudo = 0;  // util.rs:135-137 (16 address words)
+#pragma unroll
+        for (uint32_t k = 0; k < 32; k += 2) pseudo += o.be16(l3 + 8 + k);
+        if (first == 6u) parse_tcp(o, pb, pay, pseudo, r);
+        else if (first == 17u) parse_udp(o, pb, pay, pseudo, r);
+        else parse_icmp(o, pb, pay, true, pseudo, r);
+    } else {
+        set_payload(r, pb, pay);
+    }
+    return 0;
+}
+
+// frame.rs:424-438 + arp.rs:340-371 (>= 28 bytes; success keeps payload empty)
+template <class O>
+NEXG_HD void parse_arp(const O& o, uint32_t l3, uint32_t len,
+                                          nexg_record& r) {
+    const uint32_t n = len - l3;
+    if (n < 28u) {
+        set_payload(r, l3, n);
+        return;
+    }
+    r.flags |= NEXG_L_ARP;
+    r.src_port = (uint16_t)o.be16(l3);
+    r.dst_port = (uint16_t)o.be16(l3 + 2);
+    r.ip_ver_ihl = (uint8_t)o.f.u8(l3 + 4);
+    r.ip_tos = (uint8_t)o.f.u8(l3 + 5);
+    r.l4_length = (uint16_t)o.be16(l3 + 6);
+    r.ip_src = o.be32(l3 + 14);
+    r.ip_dst = o.be32(l3 + 24);
+}
+
+// frame.rs:570-607 parse_frame_from_bytes (+ 381-422 dummy Ethernet).
+template <class F>
+NEXG_HD void parse_frame(const F& f, uint32_t parity, uint32_t len,
+                                            uint32_t opt_flags, uint32_t ip_offset,
+                                            nexg_record& r) {
+    r = nexg_record{};
+    FrameOps<F> o{f, parity};
+    const bool strict = (opt_flags & NEXG_PARSE_STRICT) != 0u;
+    uint32_t ethertype, l3;
+    if (opt_flags & NEXG_PARSE_FROM_IP) {
+        if (ip_offset >= len) {
+            r.flags = (uint32_t)NEXG_ERR_MALFORMED << NEXG_STATUS_SHIFT;
+            return;
+        }
+        uint32_t n = len - ip_offset, v = f.u8(ip_offset);
+        if (n >= 20u && (v >> 4) == 4u && (v & 15u) >= 5u && (v & 15u) * 4u <= n) ethertype = 0x0800u;
+        else if (n >= 40u && (v >> 4) == 6u) ethertype = 0x86DDu;
+        else {
+            r.flags = (uint32_t)NEXG_ERR_MALFORMED << NEXG_STATUS_SHIFT;
+            return;
+        }
+        l3 = ip_offset;
+    } else {
+        if (len < 14u) {  // Q2: ethernet.rs:310-316
+            r.flags = (uint32_t)NEXG_ERR_BUFFER_TOO_SHORT << NEXG_STATUS_SHIFT;
+            return;
+        }
+        ethertype = o.be16(12);
+        l3 = 14;
+    }
+    r.packet_len = (uint16_t)len;
+    r.ethertype = (uint16_t)ethertype;
+    r.l3_off = (uint16_t)l3;
+    r.flags = NEXG_L_ETHERNET;
+    uint32_t err = 0;
+    if (ethertype == 0x0800u) err = parse_ipv4(o, l3, len, strict, r);
+    else if (ethertype == 0x86DDu) err = parse_ipv6(o, l3, len, strict, r);
+    else if (ethertype == 0x0806u) parse_arp(o, l3, len, r);
+    else set_payload(r, l3, len - l3);  // Q3
+    if (err) {
+        r = nexg_record{};
+        r.flags = err << NEXG_STATUS_SHIFT;
+    }
+}
+
+}  // namespace nexg

@@ -1,0 +1,174 @@
+// nexg_api.hip — the C ABI declared in include/nexg.h.
+//
+// Validation, context handling and kernel selection only; every byte of frame
+// data is processed by the gfx950 kernels in nexg_parse.hip / nexg_build.hip.
+// There is deliberately no CPU fallback: a missing or non-gfx950 device makes
+// nexg_ctx_create fail with NEXG_EDEVICE.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "nexg_internal.hpp"
+
+struct nexg_ctx {
+    int device;
+    int cu_count;
+    char arch[64];
+    char last_error[256];
+};
+
+namespace {
+
+int fail(nexg_ctx* ctx, int code, const char* fmt, const char* detail) {
+    if (ctx) snprintf(ctx->last_error, sizeof(ctx->last_error), fmt, detail ? detail : "");
+    return code;
+}
+
+int hip_status(nexg_ctx* ctx, hipError_t e, int code) {
+    if (e == hipSuccess) return NEXG_OK;
+    return fail(ctx, code, "HIP: %s", hipGetErrorString(e));
+}
+
+bool frames_valid(const nexg_frames* f) {
+    if (!f) return false;
+    if (f->count == 0) return true;
+    if (!f->data) return false;
+    if (!f->offsets && f->stride == 0) return false;
+    if ((reinterpret_cast<uint64_t>(f->data) & 3u) != 0) return false;  // 4-B aligned base
+    return true;
+}
+
+nexg::ParseArgs to_args(const nexg_frames* f) {
+    nexg::ParseArgs a{};
+    a.data = f->data;
+    a.data_bytes = f->data_bytes;
+    a.offsets = f->offsets;
+    a.lengths = f->lengths;
+    a.stride = f->stride;
+    a.count = f->count;
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nexg_abi_version(void) { return NEXG_ABI_VERSION; }
+
+const char* nexg_strerror(int status) {
+    switch (status) {
+        case NEXG_OK: return "ok";
+        case NEXG_EINVAL: return "invalid argument";
+        case NEXG_ENOMEM: return "out of memory";
+        case NEXG_EDEVICE: return "device error or device is not gfx950";
+        case NEXG_ELAUNCH: return "kernel launch failed";
+        case NEXG_ERANGE: return "length overflow (BuildError::LengthOverflow)";
+        default: return "unknown status";
+    }
+}
+
+int nexg_ctx_create(int device, nexg_ctx** out) {
+    if (!out) return NEXG_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return NEXG_EDEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return NEXG_EDEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NEXG_EDEVICE;
+    nexg_ctx* c = static_cast<nexg_ctx*>(calloc(1, sizeof(nexg_ctx)));
+    if (!c) return NEXG_ENOMEM;
+    c->device = device;
+    c->cu_count = prop.multiProcessorCount;
+    snprintf(c->arch, sizeof(c->arch), "%s", prop.gcnArchName);
+    *out = c;
+    return NEXG_OK;
+}
+
+int nexg_ctx_destroy(nexg_ctx* ctx) {
+    free(ctx);
+    return NEXG_OK;
+}
+
+const char* nexg_ctx_last_error(const nexg_ctx* ctx) { return ctx ? ctx->last_error : ""; }
+
+int nexg_ctx_cu_count(const nexg_ctx* ctx) { return ctx ? ctx->cu_count : 0; }
+
+int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
+                     int out_kind, void* out, void* stream) {
+    if (!ctx) return NEXG_EINVAL;
+    if (!frames_valid(frames)) return fail(ctx, NEXG_EINVAL, "invalid frame batch%s", nullptr);
+    if (out_kind != NEXG_OUT_DESC && out_kind != NEXG_OUT_RECORD)
+        return fail(ctx, NEXG_EINVAL, "invalid out_kind%s", nullptr);
+    if (frames->count && !out) return fail(ctx, NEXG_EINVAL, "NULL output%s", nullptr);
+    if ((reinterpret_cast<uint64_t>(out) & (out_kind == NEXG_OUT_DESC ? 7u : 15u)) != 0)
+        return fail(ctx, NEXG_EINVAL, "misaligned output%s", nullptr);
+    nexg::ParseArgs a = to_args(frames);
+    a.opt_flags = option ? option->flags : 0u;
+    a.ip_offset = option ? option->ip_offset : 0u;
+    a.out = out;
+    const nexg::ParseVariant v = nexg::choose_parse_variant(a);
+    return hip_status(ctx, nexg::launch_parse(v, a, out_kind, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
+int nexg_checksum_batch(nexg_ctx* ctx, const nexg_frames* bufs, uint32_t skipword, uint16_t* out,
+                        void* stream) {
+    if (!ctx) return NEXG_EINVAL;
+    if (!frames_valid(bufs)) return fail(ctx, NEXG_EINVAL, "invalid buffer batch%s", nullptr);
+    if (bufs->count && !out) return fail(ctx, NEXG_EINVAL, "NULL output%s", nullptr);
+    nexg::ParseArgs a = to_args(bufs);
+    return hip_status(ctx, nexg::launch_checksum(a, skipword, out, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
+int nexg_build_udp4_batch(nexg_ctx* ctx, const nexg_udp4_build* p, uint8_t* out,
+                          uint32_t out_stride, void* stream) {
+    if (!ctx || !p) return NEXG_EINVAL;
+    if (28ull + p->payload_len > 65535ull)
+        return fail(ctx, NEXG_ERANGE, "UDP/IPv4 length overflow%s", nullptr);
+    if (p->count && (!p->src_ip || !p->dst_ip || !out))
+        return fail(ctx, NEXG_EINVAL, "NULL address array or output%s", nullptr);
+    if (p->payload_len && !p->payload) return fail(ctx, NEXG_EINVAL, "NULL payload%s", nullptr);
+    if (out_stride < 42u + p->payload_len)
+        return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    return hip_status(ctx, nexg::launch_build_udp4(*p, out, out_stride, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
+int nexg_gen_lengths(nexg_ctx* ctx, int workload, uint64_t seed, uint64_t first_index,
+                     uint64_t count, uint32_t* lengths, void* stream) {
+    if (!ctx) return NEXG_EINVAL;
+    if (workload != NEXG_WL_UDP64 && workload != NEXG_WL_IMIX) return fail(ctx, NEXG_EINVAL, "workload%s", nullptr);
+    if (count && !lengths) return fail(ctx, NEXG_EINVAL, "NULL lengths%s", nullptr);
+    return hip_status(ctx, nexg::launch_gen_lengths(workload, seed, first_index, count, lengths,
+                                                    static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
+int nexg_gen_frames(nexg_ctx* ctx, int workload, uint64_t seed, uint64_t first_index,
+                    uint64_t count, uint8_t* data, const uint64_t* offsets, uint32_t stride,
+                    void* stream) {
+    if (!ctx) return NEXG_EINVAL;
+    if (workload != NEXG_WL_UDP64 && workload != NEXG_WL_IMIX) return fail(ctx, NEXG_EINVAL, "workload%s", nullptr);
+    if (count && !data) return fail(ctx, NEXG_EINVAL, "NULL data%s", nullptr);
+    if (!offsets && stride < (workload == NEXG_WL_UDP64 ? 64u : 1500u))
+        return fail(ctx, NEXG_EINVAL, "stride shorter than the workload's frames%s", nullptr);
+    return hip_status(ctx, nexg::launch_gen_frames(workload, seed, first_index, count, data, offsets,
+                                                   stride, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
+int nexg_gen_udp4_params(nexg_ctx* ctx, uint64_t seed, uint64_t first_index, uint64_t count,
+                         uint32_t* src_ip, uint32_t* dst_ip, uint16_t* src_port,
+                         uint16_t* dst_port, uint16_t* ip_id, void* stream) {
+    if (!ctx) return NEXG_EINVAL;
+    if (count && (!src_ip || !dst_ip || !src_port || !dst_port || !ip_id))
+        return fail(ctx, NEXG_EINVAL, "NULL output array%s", nullptr);
+    return hip_status(ctx, nexg::launch_gen_udp4_params(seed, first_index, count, src_ip, dst_ip,
+                                                        src_port, dst_port, ip_id,
+                                                        static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
+}  // extern "C"

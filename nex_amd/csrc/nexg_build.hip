@@ -1,0 +1,304 @@
+// nexg_build.hip — serialize path and synthetic workload synthesis.
+//
+// k_build_udp4: the examples/udp_ping.rs:68-109 composition
+//   UdpPacketBuilder::build (builder/udp.rs:67-95: length = 8 + payload,
+//   checksum via udp::checksum over to_bytes with skipword 3, computed 0 kept)
+//   -> Ipv4PacketBuilder::to_bytes (builder/ipv4.rs:94-170: IHL 5, total
+//   length, ipv4::checksum) -> EthernetPacketBuilder::to_bytes
+//   (builder/ethernet.rs:68, ethernet.rs:211-216)
+// on one lane per tuple. Frames are assembled in LDS and leave the CU as
+// coalesced 16-B stores of the tile's contiguous output range.
+//
+// k_gen_*: SURVEY.md Appendix C workloads. splitmix64 is counter based
+// (draw m of frame i is mix(seed ^ i*phi + (m+1)*phi)), so a wave fills one
+// frame cooperatively: lane l produces 8-byte words l, l+64, ...
+#include "frame_core.hpp"
+#include "nexg_internal.hpp"
+
+namespace nexg {
+
+constexpr uint64_t kPhi = 0x9E3779B97F4A7C15ull;
+
+NEXG_HD uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+NEXG_HD uint64_t draw(uint64_t s0, uint64_t m) { return mix64(s0 + (m + 1) * kPhi); }
+
+// IMIX class/protocol draw (App. C): the length class keeps 7:4:1 exactly; a
+// protocol that does not fit the class (v6+TCP in 64 B) is redrawn from the
+// following draws. Returns draws consumed.
+NEXG_HD uint32_t imix_class(uint64_t s0, uint32_t& len, uint32_t& proto) {
+    uint32_t m = 0;
+    const uint64_t c0 = draw(s0, m++);
+    const uint32_t cls = (uint32_t)(c0 % 12u);
+    len = cls < 7u ? 64u : (cls < 11u ? 576u : 1500u);
+    proto = (uint32_t)((c0 >> 32) % 6u);
+    while (proto == 3u && len == 64u) proto = (uint32_t)(draw(s0, m++) % 6u);
+    return m;
+}
+
+// ---------------------------------------------------------------- builder
+
+constexpr uint32_t kBuildTile = 256;
+constexpr uint32_t kBuildMaxStride = 128;
+
+struct BuildArgs {
+    nexg_udp4_build p;
+    uint8_t* out;
+    uint32_t out_stride;
+};
+
+template <bool STAGED>
+__global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * kBuildMaxStride : 16];
+    const nexg_udp4_build& p = a.p;
+    const uint64_t first = (uint64_t)blockIdx.x * kBuildTile;
+    const uint64_t left = p.count - first;
+    const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i = first + tid;
+    const uint32_t flen = 42u + p.payload_len;
+    if (tid < nf) {
+        const uint32_t src = p.src_ip[i], dst = p.dst_ip[i];
+        const uint32_t sp = p.src_port ? p.src_port[i] : p.def_src_port;
+        const uint32_t dp = p.dst_port ? p.dst_port[i] : p.def_dst_port;
+        const uint32_t id = p.ip_id ? p.ip_id[i] : p.def_ip_id;
+        const uint32_t ulen = 8u + p.payload_len, total = 20u + ulen;
+        // BE word sum of the shared payload (even UDP offset 8); L2-resident
+        uint64_t pw = 0;
+        for (uint32_t k = 0; k < p.payload_len; k += 2)
+            pw += ((uint32_t)p.payload[k] << 8) | (k + 1 < p.payload_len ? (uint32_t)p.payload[k + 1] : 0u);
+        const uint64_t addr = (uint64_t)(src >> 16) + (src & 0xFFFFu) + (dst >> 16) + (dst & 0xFFFFu);
+        // udp.rs:443-477 on to_bytes(): pseudo + sport + dport + length (+ payload)
+        const uint32_t ucs = fold_complement(addr + 17u + ulen + sp + dp + ulen + pw);
+        // ipv4.rs:932-938 on to_bytes()[..20]
+        const uint32_t w0 = (0x45u << 8) | p.dscp_ecn, w3 = ((uint32_t)(p.ip_flags & 7u)) << 13;
+        const uint32_t w4 = ((uint32_t)p.ttl << 8) | 17u;
+        const uint32_t ics = fold_complement(addr + w0 + total + id + w3 + w4);
+        uint8_t h[42];
+        for (int k = 0; k < 6; k++) {
+            h[k] = p.dst_mac ? p.dst_mac[i * 6 + k] : p.def_dst_mac[k];
+            h[6 + k] = p.src_mac ? p.src_mac[i * 6 + k] : p.def_src_mac[k];
+        }
+        h[12] = 0x08; h[13] = 0x00;
+        h[14] = (uint8_t)(w0 >> 8); h[15] = (uint8_t)w0;
+        h[16] = (uint8_t)(total >> 8); h[17] = (uint8_t)total;
+        h[18] = (uint8_t)(id >> 8); h[19] = (uint8_t)id;
+        h[20] = (uint8_t)(w3 >> 8); h[21] = 0;
+        h[22] = p.ttl; h[23] = 17;
+        h[24] = (uint8_t)(ics >> 8); h[25] = (uint8_t)ics;
+        h[26] = (uint8_t)(src >> 24); h[27] = (uint8_t)(src >> 16); h[28] = (uint8_t)(src >> 8); h[29] = (uint8_t)src;
+        h[30] = (uint8_t)(dst >> 24); h[31] = (uint8_t)(dst >> 16); h[32] = (uint8_t)(dst >> 8); h[33] = (uint8_t)dst;
+        h[34] = (uint8_t)(sp >> 8); h[35] = (uint8_t)sp;
+        h[36] = (uint8_t)(dp >> 8); h[37] = (uint8_t)dp;
+        h[38] = (uint8_t)(ulen >> 8); h[39] = (uint8_t)ulen;
+        h[40] = (uint8_t)(ucs >> 8); h[41] = (uint8_t)ucs;
+        if (STAGED) {
+            uint8_t* d = smem + tid * a.out_stride;
+#pragma unroll
+            for (int k = 0; k < 42; k++) d[k] = h[k];
+            for (uint32_t k = 0; k < p.payload_len; k++) d[42 + k] = p.payload[k];
+            for (uint32_t k = flen; k < a.out_stride; k++) d[k] = 0;
+        } else {
+            uint8_t* d = a.out + i * (uint64_t)a.out_stride;
+#pragma unroll
+            for (int k = 0; k < 42; k++) d[k] = h[k];
+            for (uint32_t k = 0; k < p.payload_len; k++) d[42 + k] = p.payload[k];
+        }
+    }
+    if (STAGED) {
+        __syncthreads();
+        const uint32_t bytes = nf * a.out_stride;
+        uint8_t* T = a.out + first * a.out_stride;
+        for (uint32_t c = tid; c < bytes / 16u; c += kBuildTile)
+            reinterpret_cast<uint4*>(T)[c] = reinterpret_cast<const uint4*>(smem)[c];
+        // tail of the last, partial tile (caller allocates count * out_stride)
+        const uint32_t tail = bytes & ~15u;
+        if (tid < bytes - tail) T[tail + tid] = smem[tail + tid];
+    }
+}
+
+// ------------------------------------------------------------- generators
+
+__global__ void k_gen_lengths(int workload, uint64_t seed, uint64_t first, uint64_t count,
+                              uint32_t* lengths) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    uint32_t len = 64, proto = 1;
+    if (workload == NEXG_WL_IMIX) imix_class(seed ^ ((first + i) * kPhi), len, proto);
+    lengths[i] = len;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+constexpr uint32_t kGenBuf = 1536;  // >= 1500, multiple of 16
+
+// one wave per frame; four waves per block, grid-stride, block-uniform loop
+__global__ __launch_bounds__(256) void k_gen_frames(int workload, uint64_t seed, uint64_t first,
+                                                    uint64_t count, uint8_t* data,
+                                                    const uint64_t* offsets, uint32_t stride) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[4 * kGenBuf];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint8_t* b = smem + wave * kGenBuf;
+    const uint64_t nblocks = gridDim.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * 4; base < count; base += nblocks * 4) {
+        const uint64_t li = base + wave;
+        const bool active = li < count;
+        const uint64_t s0 = seed ^ ((first + li) * kPhi);
+        uint32_t len = 64, proto = 1, d0 = 0;
+        if (workload == NEXG_WL_IMIX) d0 = imix_class(s0, len, proto);
+        const uint32_t nwords = (len + 7u) / 8u;
+        if (active) {
+            for (uint32_t k = lane; k < nwords; k += 64) {
+                const uint64_t r = draw(s0, d0 + k);
+                reinterpret_cast<uint2*>(b)[k] = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+            }
+        }
+        __syncthreads();
+        const bool v6 = proto >= 3u;
+        const uint32_t l4p = proto % 3u;  // 0 tcp, 1 udp, 2 icmp
+        const uint32_t l4 = v6 ? 54u : 34u, n = len - l4;
+        const uint32_t pr = l4p == 0u ? 6u : (l4p == 1u ? 17u : (v6 ? 58u : 1u));
+        const uint32_t skip = l4p == 0u ? 8u : (l4p == 1u ? 3u : 1u);
+        if (active && lane == 0) {
+            b[0] &= 0xFE;
+            b[6] &= 0xFE;
+            uint8_t* t = b + l4;
+            if (!v6) {
+                b[12] = 0x08; b[13] = 0x00; b[14] = 0x45;
+                b[16] = (uint8_t)((len - 14u) >> 8); b[17] = (uint8_t)(len - 14u);
+                b[20] = 0x40; b[21] = 0x00; b[22] = 64; b[23] = (uint8_t)pr;
+                b[24] = 0; b[25] = 0;
+            } else {
+                b[12] = 0x86; b[13] = 0xDD;
+                b[14] = (uint8_t)(0x60u | (b[14] & 0x0Fu));
+                b[18] = (uint8_t)((len - 54u) >> 8); b[19] = (uint8_t)(len - 54u);
+                b[20] = (uint8_t)pr; b[21] = 64;
+            }
+            if (l4p == 0u) {
+                t[12] = 0x50; t[16] = 0; t[17] = 0; t[18] = 0; t[19] = 0;
+            } else if (l4p == 1u) {
+                t[4] = (uint8_t)(n >> 8); t[5] = (uint8_t)n; t[6] = 0; t[7] = 0;
+            } else {
+                t[0] = v6 ? 128 : 8; t[1] = 0; t[2] = 0; t[3] = 0;
+            }
+        }
+        __syncthreads();
+        // L4 word sum over [l4, len) (checksum field is zero), l4 even
+        uint32_t part = 0;
+        if (active) {
+            const uint32_t A = l4, B = len;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(b);
+            for (uint32_t j = (A & ~3u) + 4u * lane; j < B; j += 256u) {
+                uint32_t v = w[j >> 2];
+                uint32_t lo = A > j ? A - j : 0u, hi = (B - j) < 4u ? B - j : 4u;
+                uint32_t m = (hi >= 4u ? 0xFFFFFFFFu : ((1u << (8u * hi)) - 1u)) & (0xFFFFFFFFu << (8u * lo));
+                v &= m;
+                part += (v & 0xFFFFu) + (v >> 16);
+            }
+        }
+        const uint32_t s_le = wave_sum(part);
+        if (active && lane == 0) {
+            auto be = [&](uint32_t k) { return ((uint32_t)b[k] << 8) | b[k + 1]; };
+            uint64_t addr = 0;
+            if (!v6) {
+                uint64_t ih = 0;
+                for (uint32_t k = 14; k < 34; k += 2) ih += be(k);
+                const uint32_t ics = fold_complement(ih);
+                b[24] = (uint8_t)(ics >> 8); b[25] = (uint8_t)ics;
+                for (uint32_t k = 26; k < 34; k += 2) addr += be(k);
+            } else {
+                for (uint32_t k = 22; k < 54; k += 2) addr += be(k);
+            }
+            uint64_t t = ((uint64_t)s_le) << 8;
+            if (!(l4p == 2u && !v6)) t += addr + pr + n;
+            const uint32_t cs = fold_complement(t);
+            uint8_t* f = b + l4 + 2u * skip;
+            f[0] = (uint8_t)(cs >> 8); f[1] = (uint8_t)cs;
+            const uint64_t c = draw(s0, d0 + nwords);
+            if ((c & 15u) == 0u) {
+                const uint32_t field = (uint32_t)(c >> 4) & 1u, bit = (uint32_t)(c >> 8) & 15u;
+                uint8_t* q = (!v6 && field == 0u) ? b + 24 : f;
+                const uint32_t v = (((uint32_t)q[0] << 8) | q[1]) ^ (1u << bit);
+                q[0] = (uint8_t)(v >> 8); q[1] = (uint8_t)v;
+            }
+        }
+        __syncthreads();
+        if (active) {
+            uint8_t* dst = data + (offsets ? offsets[li] : li * (uint64_t)stride);
+            if ((reinterpret_cast<uint64_t>(dst) & 3u) == 0u) {
+                for (uint32_t k = lane; k < len / 4u; k += 64)
+                    reinterpret_cast<uint32_t*>(dst)[k] = reinterpret_cast<const uint32_t*>(b)[k];
+                for (uint32_t k = (len & ~3u) + lane; k < len; k += 64) dst[k] = b[k];
+            } else {
+                for (uint32_t k = lane; k < len; k += 64) dst[k] = b[k];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_gen_udp4_params(uint64_t seed, uint64_t first, uint64_t count, uint32_t* src_ip,
+                                  uint32_t* dst_ip, uint16_t* sport, uint16_t* dport,
+                                  uint16_t* ip_id) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint64_t s0 = seed ^ ((first + i) * kPhi);
+    const uint64_t r0 = draw(s0, 0), r1 = draw(s0, 1);
+    src_ip[i] = (uint32_t)r0;
+    dst_ip[i] = (uint32_t)(r0 >> 32);
+    sport[i] = (uint16_t)r1;
+    dport[i] = (uint16_t)(r1 >> 16);
+    ip_id[i] = (uint16_t)(r1 >> 32);
+}
+
+// --------------------------------------------------------------- launchers
+
+hipError_t launch_build_udp4(const nexg_udp4_build& p, uint8_t* out, uint32_t out_stride,
+                             hipStream_t s) {
+    if (p.count == 0) return hipSuccess;
+    BuildArgs a{p, out, out_stride};
+    const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
+    const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
+    if (staged)
+        hipLaunchKernelGGL(k_build_udp4<true>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_build_udp4<false>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_lengths(int workload, uint64_t seed, uint64_t first, uint64_t count,
+                              uint32_t* lengths, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_lengths, dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, s,
+                       workload, seed, first, count, lengths);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_frames(int workload, uint64_t seed, uint64_t first, uint64_t count,
+                             uint8_t* data, const uint64_t* offsets, uint32_t stride,
+                             hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    uint64_t blocks = (count + 3) / 4;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_gen_frames, dim3((uint32_t)blocks), dim3(256), 0, s, workload, seed, first,
+                       count, data, offsets, stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_udp4_params(uint64_t seed, uint64_t first, uint64_t count,
+                                  uint32_t* src_ip, uint32_t* dst_ip, uint16_t* sport,
+                                  uint16_t* dport, uint16_t* ip_id, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_udp4_params, dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, s,
+                       seed, first, count, src_ip, dst_ip, sport, dport, ip_id);
+    return hipGetLastError();
+}
+
+}  // namespace nexg

@@ -1,0 +1,48 @@
+// nexg_internal.hpp — host-side launch interfaces shared between the kernel
+// translation units and the C ABI (nexg_api.hip). Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nexg.h"
+
+namespace nexg {
+
+struct ParseArgs {
+    const uint8_t* data;
+    uint64_t data_bytes;
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    uint32_t stride;
+    uint64_t count;
+    uint32_t opt_flags;
+    uint32_t ip_offset;
+    void* out;
+};
+
+// Kernel variants of the parse path.
+enum class ParseVariant {
+    TileStride64,   // fixed 64-B stride: coalesced tile staging into LDS
+    TileStride,     // fixed stride (multiple of 16, <= 128): tile staging
+    LaneWindow,     // any layout: per-lane 128-B header window + HBM bulk
+};
+
+hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStream_t s);
+ParseVariant choose_parse_variant(const ParseArgs& a);
+
+hipError_t launch_checksum(const ParseArgs& a, uint32_t skipword, uint16_t* out, hipStream_t s);
+
+hipError_t launch_build_udp4(const nexg_udp4_build& p, uint8_t* out, uint32_t out_stride,
+                             hipStream_t s);
+
+hipError_t launch_gen_lengths(int workload, uint64_t seed, uint64_t first, uint64_t count,
+                              uint32_t* lengths, hipStream_t s);
+hipError_t launch_gen_frames(int workload, uint64_t seed, uint64_t first, uint64_t count,
+                             uint8_t* data, const uint64_t* offsets, uint32_t stride,
+                             hipStream_t s);
+hipError_t launch_gen_udp4_params(uint64_t seed, uint64_t first, uint64_t count,
+                                  uint32_t* src_ip, uint32_t* dst_ip, uint16_t* sport,
+                                  uint16_t* dport, uint16_t* ip_id, hipStream_t s);
+
+}  // namespace nexg

@@ -1,0 +1,238 @@
+"""Batched device engine over the C ABI (include/nexg.h).
+
+torch is used only as device-memory / stream plumbing: frames, offsets and
+outputs are torch CUDA(HIP) tensors whose data pointers go straight to
+libnexg.so, and work is enqueued on torch's current stream.
+"""
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import abi
+from ._lib import load
+from .frame import ParseMode, ParseOption
+
+
+class NexgError(RuntimeError):
+    def __init__(self, status, message=""):
+        super().__init__(f"nexg error {status}: {message}")
+        self.status = status
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def u32_tensor(values, device="cuda"):
+    """Device tensor holding u32 values (stored as int32 bit patterns)."""
+    a = np.asarray(values, dtype=np.uint64).astype(np.uint32).view(np.int32)
+    return _torch().from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+def u16_tensor(values, device="cuda"):
+    """Device tensor holding u16 values (stored as int16 bit patterns)."""
+    a = np.asarray(values, dtype=np.uint64).astype(np.uint16).view(np.int16)
+    return _torch().from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+@dataclass
+class FrameBatch:
+    """A device-resident batch of raw frames (nexg_frames).
+
+    data     uint8 tensor on the device
+    offsets  int64 tensor (count or count+1 entries) or None (fixed stride)
+    lengths  int32 tensor or None
+    """
+    data: "object"
+    count: int
+    stride: int = 0
+    offsets: Optional[object] = None
+    lengths: Optional[object] = None
+
+    def to_c(self):
+        return abi.Frames(
+            data=self.data.data_ptr() if self.count else None,
+            data_bytes=self.data.numel(),
+            offsets=None if self.offsets is None else self.offsets.data_ptr(),
+            lengths=None if self.lengths is None else self.lengths.data_ptr(),
+            stride=self.stride, reserved=0, count=self.count)
+
+    @property
+    def total_bytes(self):
+        if self.lengths is not None:
+            return int(self.lengths.sum().item())
+        if self.offsets is not None:
+            return int((self.offsets[self.count] - self.offsets[0]).item())
+        return self.count * self.stride
+
+    @classmethod
+    def from_frames(cls, frames: Sequence[bytes], device="cuda", pad_to=4):
+        """Pack host frames back to back (each start aligned to `pad_to`)."""
+        torch = _torch()
+        offs = np.zeros(len(frames) + 1, dtype=np.int64)
+        lens = np.array([len(f) for f in frames], dtype=np.int32)
+        pos = 0
+        for i, f in enumerate(frames):
+            offs[i] = pos
+            pos += (len(f) + pad_to - 1) // pad_to * pad_to
+        offs[len(frames)] = pos
+        buf = np.zeros(max(pos, 16), dtype=np.uint8)
+        for i, f in enumerate(frames):
+            buf[offs[i]:offs[i] + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
+        return cls(data=torch.from_numpy(buf).to(device), count=len(frames),
+                   offsets=torch.from_numpy(offs).to(device),
+                   lengths=torch.from_numpy(lens).to(device))
+
+    @classmethod
+    def from_strided(cls, array: np.ndarray, device="cuda", lengths=None):
+        """count x stride uint8 host array -> fixed-stride device batch."""
+        torch = _torch()
+        count, stride = array.shape
+        data = torch.from_numpy(np.ascontiguousarray(array).reshape(-1)).to(device)
+        lt = None if lengths is None else torch.from_numpy(np.asarray(lengths, np.int32)).to(device)
+        return cls(data=data, count=count, stride=stride, lengths=lt)
+
+
+class Engine:
+    """One nexg context bound to one gfx950 device (nexg_ctx_create)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        torch = _torch()
+        self.device = device
+        self.torch_device = torch.device("cuda", device)
+        h = ctypes.c_void_p()
+        rc = self.lib.nexg_ctx_create(device, ctypes.byref(h))
+        if rc != abi.OK:
+            raise NexgError(rc, self.lib.nexg_strerror(rc).decode())
+        self.ctx = h
+
+    def close(self):
+        if self.ctx:
+            self.lib.nexg_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def cu_count(self):
+        return self.lib.nexg_ctx_cu_count(self.ctx)
+
+    def _stream(self, stream):
+        torch = _torch()
+        s = stream if stream is not None else torch.cuda.current_stream(self.torch_device)
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def _check(self, rc):
+        if rc != abi.OK:
+            raise NexgError(rc, self.lib.nexg_ctx_last_error(self.ctx).decode())
+
+    # --- hot path -------------------------------------------------------
+    def parse(self, batch: FrameBatch, option: ParseOption = ParseOption(),
+              mode: ParseMode = ParseMode.Lenient, out_kind: int = abi.OUT_DESC,
+              out=None, stream=None):
+        """Frame::try_from_buf_with_mode on every frame (frame.rs:309).
+
+        Returns a uint8 device tensor holding nexg_desc[count] (8 B each) or
+        nexg_record[count] (64 B each); see `descs_to_numpy`."""
+        torch = _torch()
+        width = 8 if out_kind == abi.OUT_DESC else 64
+        if out is None:
+            out = torch.empty(max(batch.count, 1) * width, dtype=torch.uint8, device=self.torch_device)
+        fr = batch.to_c()
+        opt = abi.ParseOptionC(option.flags(mode), option.offset)
+        self._check(self.lib.nexg_parse_batch(self.ctx, ctypes.byref(fr), ctypes.byref(opt), out_kind,
+                                              _ptr(out), self._stream(stream)))
+        return out
+
+    def parse_to_numpy(self, batch, option=ParseOption(), mode=ParseMode.Lenient,
+                       out_kind=abi.OUT_RECORD):
+        out = self.parse(batch, option, mode, out_kind)
+        _torch().cuda.synchronize(self.torch_device)
+        dt = abi.RECORD_DTYPE if out_kind == abi.OUT_RECORD else abi.DESC_DTYPE
+        return out.cpu().numpy()[: batch.count * dt.itemsize].view(dt)
+
+    def checksum(self, batch: FrameBatch, skipword: int, stream=None):
+        """util::checksum(buf, skipword) per buffer (util.rs:65)."""
+        torch = _torch()
+        out = torch.empty(max(batch.count, 1), dtype=torch.int16, device=self.torch_device)
+        fr = batch.to_c()
+        skip = min(int(skipword), 0xFFFFFFFF)
+        self._check(self.lib.nexg_checksum_batch(self.ctx, ctypes.byref(fr), skip, _ptr(out),
+                                                 self._stream(stream)))
+        return out[: batch.count]
+
+    # --- serialize path ---------------------------------------------------
+    def build_udp4(self, src_ip, dst_ip, src_port=None, dst_port=None, ip_id=None,
+                   def_src_port=0, def_dst_port=0, def_ip_id=0,
+                   src_mac=b"\0" * 6, dst_mac=b"\0" * 6, ttl=64, ip_flags=0, dscp_ecn=0,
+                   payload=None, out_stride=None, out=None, stream=None):
+        """UdpPacketBuilder -> Ipv4PacketBuilder -> EthernetPacketBuilder
+        (udp_ping.rs:68-109) on every tuple. Tensors are int32/int16 device
+        tensors holding the u32/u16 values."""
+        torch = _torch()
+        count = src_ip.numel()
+        plen = 0 if payload is None else payload.numel()
+        stride = out_stride or (42 + plen)
+        if out is None:
+            out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
+        p = abi.Udp4Build()
+        p.src_ip, p.dst_ip = src_ip.data_ptr(), dst_ip.data_ptr()
+        p.src_port = None if src_port is None else src_port.data_ptr()
+        p.dst_port = None if dst_port is None else dst_port.data_ptr()
+        p.ip_id = None if ip_id is None else ip_id.data_ptr()
+        p.src_mac = p.dst_mac = None
+        p.payload = None if payload is None else payload.data_ptr()
+        p.payload_len = plen
+        p.def_src_port, p.def_dst_port, p.def_ip_id = def_src_port, def_dst_port, def_ip_id
+        p.def_src_mac[:] = list(src_mac)
+        p.def_dst_mac[:] = list(dst_mac)
+        p.ttl, p.ip_flags, p.dscp_ecn, p.count = ttl, ip_flags, dscp_ecn, count
+        self._check(self.lib.nexg_build_udp4_batch(self.ctx, ctypes.byref(p), _ptr(out), stride,
+                                                   self._stream(stream)))
+        return out
+
+    # --- synthetic workloads ----------------------------------------------
+    def gen_batch(self, workload: int, count: int, seed: int = abi.DEFAULT_SEED,
+                  first_index: int = 0, stream=None) -> FrameBatch:
+        """Device-generated SURVEY.md App. C workload (UDP64: fixed 64-B
+        stride; IMIX: packed with an int64 offset table of count+1 entries)."""
+        torch = _torch()
+        dev = self.torch_device
+        s = self._stream(stream)
+        if workload == abi.WL_UDP64:
+            data = torch.empty(max(count, 1) * 64, dtype=torch.uint8, device=dev)
+            self._check(self.lib.nexg_gen_frames(self.ctx, workload, seed, first_index, count,
+                                                 _ptr(data), None, 64, s))
+            return FrameBatch(data=data, count=count, stride=64)
+        lengths = torch.empty(max(count, 1), dtype=torch.int32, device=dev)
+        self._check(self.lib.nexg_gen_lengths(self.ctx, workload, seed, first_index, count,
+                                              _ptr(lengths), s))
+        offsets = torch.zeros(count + 1, dtype=torch.int64, device=dev)
+        if count:
+            torch.cumsum(lengths[:count].to(torch.int64), 0, out=offsets[1:])
+        total = int(offsets[count].item()) if count else 0
+        data = torch.empty(max(total, 16) + 16, dtype=torch.uint8, device=dev)
+        self._check(self.lib.nexg_gen_frames(self.ctx, workload, seed, first_index, count,
+                                             _ptr(data), _ptr(offsets), 0, s))
+        return FrameBatch(data=data, count=count, offsets=offsets)
+
+    def gen_udp4_params(self, count, seed=abi.DEFAULT_SEED, first_index=0, stream=None):
+        torch = _torch()
+        dev = self.torch_device
+        t32 = [torch.empty(max(count, 1), dtype=torch.int32, device=dev) for _ in range(2)]
+        t16 = [torch.empty(max(count, 1), dtype=torch.int16, device=dev) for _ in range(3)]
+        self._check(self.lib.nexg_gen_udp4_params(self.ctx, seed, first_index, count,
+                                                  *[_ptr(t) for t in t32 + t16], self._stream(stream)))
+        return [t[:count] for t in t32 + t16]

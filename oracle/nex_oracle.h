@@ -1,0 +1,82 @@
+/*
+ * nex_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of shellrow/nex nex-packet's per-frame path, used as the
+ * parity checker for the HIP engine (nex_amd). Only tests/, __graft_entry__
+ * smoke() and bench.py's cpu_baseline leg may load it; the product never does.
+ *
+ * Parity pinning: the reference is Rust with no Cargo.lock and no vendored
+ * crates, and cargo/rustc are absent from this image, so the reference cannot
+ * be built or run here. This restatement is pinned by the
+ * reference's own known-answer tests and fixtures, committed as data under
+ * tests/golden/ (util.rs:190-261, icmpv6.rs:606-631, frame.rs:665-784,
+ * ipv4.rs:944-1204, ipv6.rs:706-802, tcp.rs:1276-1314, udp.rs:511-527,
+ * icmp.rs:708-725, the fuzz seed corpus and the bench frames).
+ *
+ * Every function follows the reference literally — including re-serialising
+ * packets before checksumming them (to_bytes), as the Rust does — so that it is
+ * an independent algorithm from the GPU kernels, which fold the same
+ * arithmetic into closed-form word sums.
+ */
+#ifndef NEX_ORACLE_H
+#define NEX_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../include/nexg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* util.rs:65 checksum(data, skipword) */
+uint16_t nexo_checksum(const uint8_t* data, size_t len, size_t skipword);
+/* util.rs:141 sum_be_words (private in the reference; exposed for its KATs) */
+uint32_t nexo_sum_be_words(const uint8_t* data, size_t len, size_t skipword);
+/* util.rs:169 sum_be_words_joined */
+uint32_t nexo_sum_be_words_joined(const uint8_t* data, size_t len,
+                                  size_t skipword, const uint8_t* extra,
+                                  size_t extra_len);
+/* util.rs:81 ipv4_checksum */
+uint16_t nexo_ipv4_checksum(const uint8_t* data, size_t len, size_t skipword,
+                            const uint8_t* extra, size_t extra_len,
+                            const uint8_t src[4], const uint8_t dst[4],
+                            uint8_t proto);
+/* util.rs:111 ipv6_checksum */
+uint16_t nexo_ipv6_checksum(const uint8_t* data, size_t len, size_t skipword,
+                            const uint8_t* extra, size_t extra_len,
+                            const uint8_t src[16], const uint8_t dst[16],
+                            uint8_t proto);
+
+/* frame.rs:309 Frame::try_from_buf_with_mode + verification checksums for one
+ * frame, written as a nexg_record (and its nexg_desc projection). */
+void nexo_parse_frame(const uint8_t* frame, size_t len, uint32_t flags,
+                      uint32_t ip_offset, nexg_record* rec);
+void nexo_record_to_desc(const nexg_record* rec, nexg_desc* desc);
+
+/* Batch form over a host-memory nexg_frames layout (pointers are HOST). */
+int nexo_parse_batch(const nexg_frames* frames, uint32_t flags,
+                     uint32_t ip_offset, nexg_record* recs, nexg_desc* descs,
+                     int nthreads);
+
+/* Builders: udp_ping.rs:68-109 composition for one tuple. Returns bytes
+ * written (42 + payload_len) or -1 on BuildError. */
+int nexo_build_udp4(const uint8_t src_mac[6], const uint8_t dst_mac[6],
+                    uint32_t src_ip, uint32_t dst_ip, uint16_t sport,
+                    uint16_t dport, uint16_t ip_id, uint8_t ttl,
+                    uint8_t ip_flags, uint8_t dscp_ecn, const uint8_t* payload,
+                    uint32_t payload_len, uint8_t* out);
+
+/* Synthetic workloads, independent CPU implementation
+ * of the generator the engine ships (nexg_gen_*). */
+uint32_t nexo_gen_length(int workload, uint64_t seed, uint64_t index);
+void nexo_gen_frame(int workload, uint64_t seed, uint64_t index, uint8_t* out);
+void nexo_gen_udp4_params(uint64_t seed, uint64_t index, uint32_t* src_ip,
+                          uint32_t* dst_ip, uint16_t* sport, uint16_t* dport,
+                          uint16_t* ip_id);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,144 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the CPU restatement
+(oracle/nex_oracle.c, built into oracle/liboracle.so by oracle/Makefile).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module. Parity status: pinned by the reference's own KATs and fixtures
+(tests/golden/); the Rust reference itself cannot be built here.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from nex_amd import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        P, S, U16, U32, U64, I = (ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint16,
+                                  ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int)
+        L.nexo_checksum.restype = U16
+        L.nexo_checksum.argtypes = [P, S, S]
+        L.nexo_sum_be_words.restype = U32
+        L.nexo_sum_be_words.argtypes = [P, S, S]
+        L.nexo_sum_be_words_joined.restype = U32
+        L.nexo_sum_be_words_joined.argtypes = [P, S, S, P, S]
+        L.nexo_ipv4_checksum.restype = U16
+        L.nexo_ipv4_checksum.argtypes = [P, S, S, P, S, P, P, ctypes.c_uint8]
+        L.nexo_ipv6_checksum.restype = U16
+        L.nexo_ipv6_checksum.argtypes = [P, S, S, P, S, P, P, ctypes.c_uint8]
+        L.nexo_parse_frame.restype = None
+        L.nexo_parse_frame.argtypes = [P, S, U32, U32, P]
+        L.nexo_parse_batch.restype = I
+        L.nexo_parse_batch.argtypes = [ctypes.POINTER(abi.Frames), U32, U32, P, P, I]
+        L.nexo_build_udp4.restype = I
+        L.nexo_build_udp4.argtypes = [P, P, U32, U32, U16, U16, U16, ctypes.c_uint8, ctypes.c_uint8,
+                                      ctypes.c_uint8, P, U32, P]
+        L.nexo_gen_length.restype = U32
+        L.nexo_gen_length.argtypes = [I, U64, U64]
+        L.nexo_gen_frame.restype = None
+        L.nexo_gen_frame.argtypes = [I, U64, U64, P]
+        L.nexo_gen_udp4_params.restype = None
+        L.nexo_gen_udp4_params.argtypes = [U64, U64, P, P, P, P, P]
+        _lib = L
+    return _lib
+
+
+def _buf(b):
+    b = bytes(b)
+    return ctypes.create_string_buffer(b, max(len(b), 1)), len(b)
+
+
+def checksum(data, skipword):
+    buf, n = _buf(data)
+    return lib().nexo_checksum(buf, n, min(skipword, 2**63))
+
+
+def sum_be_words(data, skipword):
+    buf, n = _buf(data)
+    return lib().nexo_sum_be_words(buf, n, min(skipword, 2**63))
+
+
+def sum_be_words_joined(data, skipword, extra):
+    b1, n1 = _buf(data)
+    b2, n2 = _buf(extra)
+    return lib().nexo_sum_be_words_joined(b1, n1, min(skipword, 2**63), b2, n2)
+
+
+def ipv6_checksum(data, skipword, src, dst, proto):
+    buf, n = _buf(data)
+    return lib().nexo_ipv6_checksum(buf, n, skipword, None, 0, bytes(src), bytes(dst), proto)
+
+
+def ipv4_checksum(data, skipword, src, dst, proto):
+    buf, n = _buf(data)
+    return lib().nexo_ipv4_checksum(buf, n, skipword, None, 0, bytes(src), bytes(dst), proto)
+
+
+def parse_frame(frame, flags=0, ip_offset=0):
+    rec = np.zeros(1, dtype=abi.RECORD_DTYPE)
+    buf, n = _buf(frame)
+    lib().nexo_parse_frame(buf, n, flags, ip_offset, rec.ctypes.data)
+    return rec[0]
+
+
+def parse_packed(data: np.ndarray, offsets=None, lengths=None, stride=0, flags=0, ip_offset=0,
+                 nthreads=1):
+    """Parse a host-memory batch laid out as nexg_frames; returns records."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    count = (len(lengths) if lengths is not None else
+             (len(offsets) - 1 if offsets is not None else len(data) // stride))
+    offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.uint32)
+    fr = abi.Frames(data=data.ctypes.data, data_bytes=data.nbytes,
+                    offsets=None if offs is None else offs.ctypes.data,
+                    lengths=None if lens is None else lens.ctypes.data,
+                    stride=stride, reserved=0, count=count)
+    recs = np.zeros(count, dtype=abi.RECORD_DTYPE)
+    lib().nexo_parse_batch(ctypes.byref(fr), flags, ip_offset, recs.ctypes.data, None, nthreads)
+    return recs
+
+
+def parse_frames(frames, flags=0, ip_offset=0):
+    return np.array([parse_frame(f, flags, ip_offset) for f in frames], dtype=abi.RECORD_DTYPE)
+
+
+def build_udp4(src_mac, dst_mac, src_ip, dst_ip, sport, dport, ip_id=0, ttl=64, ip_flags=0,
+               dscp_ecn=0, payload=b""):
+    out = ctypes.create_string_buffer(42 + len(payload) + 64)
+    pb, pn = _buf(payload)
+    n = lib().nexo_build_udp4(bytes(src_mac), bytes(dst_mac), src_ip, dst_ip, sport, dport, ip_id,
+                              ttl, ip_flags, dscp_ecn, pb, pn, out)
+    if n < 0:
+        raise ValueError("BuildError::LengthOverflow")
+    return out.raw[:n]
+
+
+def gen_length(workload, index, seed=abi.DEFAULT_SEED):
+    return lib().nexo_gen_length(workload, seed, index)
+
+
+def gen_frame(workload, index, seed=abi.DEFAULT_SEED):
+    n = gen_length(workload, index, seed)
+    out = ctypes.create_string_buffer(max(n, 1504))
+    lib().nexo_gen_frame(workload, seed, index, out)
+    return out.raw[:n]
+
+
+def gen_udp4_params(index, seed=abi.DEFAULT_SEED):
+    v = [ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint16(), ctypes.c_uint16(), ctypes.c_uint16()]
+    lib().nexo_gen_udp4_params(seed, index, *[ctypes.byref(x) for x in v])
+    return tuple(x.value for x in v)

@@ -1,0 +1,246 @@
+"""Writes tests/golden/reference_vectors.json.
+
+Every vector is an input and the outputs the REFERENCE's own tests assert for
+it (shellrow/nex nex-packet unit tests, fuzz seed corpus, bench fixtures),
+transcribed as data with the file:line it comes from. Nothing here is
+computed: the oracle and the GPU engine are checked against these values.
+
+Run: python tests/golden/make_golden.py
+"""
+import json
+import os
+
+
+def h(bs):
+    return bytes(bs).hex()
+
+
+def eth(payload, ethertype=0x0800, dst=bytes(6), src=bytes(6)):
+    return bytes(dst) + bytes(src) + ethertype.to_bytes(2, "big") + bytes(payload)
+
+
+V = []
+
+
+def add(name, cite, frame, expect, flags=0, ip_offset=0, note=""):
+    V.append({"name": name, "cite": cite, "frame": h(frame), "parse_flags": flags,
+              "ip_offset": ip_offset, "expect": expect, "note": note})
+
+
+# ---- util.rs:190-261 (checksum arithmetic) --------------------------------
+UTIL = {
+    "cite": "nex-packet/src/util.rs:190-261",
+    "sum_be_words": [
+        {"data": h(range(11)), "skipword": 1, "sum": 7190},
+        {"data": h(range(11)), "skipword": 2, "sum": 6676},
+        {"data": h(range(11)), "skipword": 99, "sum": 7705},
+        {"data": h(range(11)), "skipword": 101, "sum": 7705},
+        {"data": "", "skipword": 0, "sum": 0},
+        {"data": "", "skipword": 10, "sum": 0},
+        {"data": "01", "skipword": 1, "sum": 256},
+        {"data": "0101", "skipword": 0, "sum": 0},
+        {"data": "0101", "skipword": 1, "sum": 257},
+        {"data": "040404", "skipword": 0, "sum": 1024},
+        {"data": "040404", "skipword": 1, "sum": 1028},
+        {"data": "040404", "skipword": 2, "sum": 2052},
+        {"data": "040404", "skipword": 3, "sum": 2052},
+    ],
+    "joined_equals_contiguous": [
+        {"data": "01", "extra": "020304", "contiguous": "01020304"},
+        {"data": "0102", "extra": "03", "contiguous": "010203"},
+    ],
+    "checksum": [
+        {"data": "ffffffff", "skipword": 2**64 - 1, "checksum": 0},
+        {"data": "01", "skipword": 2**64 - 1, "checksum": 0xFEFF},
+        {"data": "010203", "skipword": 2**64 - 1, "checksum": 0xFBFD},
+    ],
+}
+
+# ---- icmpv6.rs:606-631 (ICMPv6 pseudo-header checksum KAT) ----------------
+ICMPV6_ECHO = bytes([0x80, 0x00, 0xFF, 0xFF, 0x00, 0x00, 0x00, 0x01]) + bytes([
+    0x20, 0x20, 0x75, 0x73, 0x74, 0x20, 0x61, 0x20, 0x66, 0x6c, 0x65, 0x73, 0x68, 0x20,
+    0x77, 0x6f, 0x75, 0x6e, 0x64, 0x20, 0x20, 0x74, 0x69, 0x73, 0x20, 0x62, 0x75, 0x74,
+    0x20, 0x61, 0x20, 0x73, 0x63, 0x72, 0x61, 0x74, 0x63, 0x68, 0x20, 0x20, 0x6b, 0x6e,
+    0x69, 0x67, 0x68, 0x74, 0x73, 0x20, 0x6f, 0x66, 0x20, 0x6e, 0x69, 0x20, 0x20, 0x20])
+LO6 = bytes(15) + b"\x01"
+
+
+def ipv6_hdr(payload, nh, src=LO6, dst=LO6, plen=None, tc_flow=(0x60, 0, 0, 0), hop=64):
+    plen = len(payload) if plen is None else plen
+    return bytes(tc_flow) + plen.to_bytes(2, "big") + bytes([nh, hop]) + src + dst + bytes(payload)
+
+
+ICMPV6 = {
+    "cite": "nex-packet/src/icmpv6.rs:606-631",
+    "packet": h(ICMPV6_ECHO), "src": h(LO6), "dst": h(LO6),
+    "checksum": 0x1D2E, "checksum_type_0x81": 0x1C2E,
+}
+add("icmpv6_echo_request_lo", "icmpv6.rs:606-631 (wrapped in Eth/IPv6 ::1->::1)",
+    eth(ipv6_hdr(ICMPV6_ECHO, 58), 0x86DD),
+    {"layers": ["eth", "ip", "ipv6", "icmpv6"], "l4_type": 0x80, "l4_csum": 0xFFFF,
+     "l4_csum_calc": 0x1D2E})
+add("icmpv6_echo_reply_lo", "icmpv6.rs:626-630 (type changed to 0x81)",
+    eth(ipv6_hdr(b"\x81" + ICMPV6_ECHO[1:], 58), 0x86DD),
+    {"layers": ["eth", "ip", "ipv6", "icmpv6"], "l4_type": 0x81, "l4_csum_calc": 0x1C2E})
+
+# ---- frame.rs:665-784 ----------------------------------------------------
+add("unknown_ethertype_keeps_payload", "frame.rs:665-678",
+    eth(b"\xde\xad\xbe\xef", 0x88B5),
+    {"layers": ["eth"], "payload": "deadbeef"})
+raw = bytearray(14 + 20 + 8 + 4)
+raw[12:14] = b"\x08\x00"
+raw[14:34] = bytes([0x45, 0, 0, 0x20, 0, 1, 0, 0, 64, 17, 0, 0, 192, 0, 2, 1, 198, 51, 100, 2])
+raw[34:42] = bytes([0x04, 0xD2, 0x00, 0x35, 0x00, 0x0C, 0x00, 0x00])
+raw[42:46] = bytes([1, 2, 3, 4])
+add("ipv4_udp_frame", "frame.rs:680-734", raw,
+    {"layers": ["eth", "ip", "ipv4", "transport", "udp"], "ip_version": 4, "dst_port": 53,
+     "payload": "01020304"})
+add("dummy_ethernet_ipv4", "frame.rs:736-745 (ParseOption from_ip_packet, offset 0)",
+    bytes([0x45, 0x00, 0x00, 0x14, 0x00, 0x00, 0x00, 0x00, 64, 17, 0, 0, 127, 0, 0, 1, 127, 0, 0, 1]),
+    {"layers": ["eth", "ip", "ipv4", "transport"], "ethertype": 0x0800}, flags=2,
+    note="UDP over 0 bytes fails -> transport Some(None,None)")
+add("frame_slice_ipv4_tcp", "frame.rs:747-762 (FrameSlice boundaries; same bytes via Frame)",
+    bytes([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 0x08, 0x00, 0x45, 0, 0, 44, 0, 0, 0, 0, 64, 6, 0,
+           0, 192, 0, 2, 1, 198, 51, 100, 2, 0, 80, 0x04, 0xd2, 0, 0, 0, 0, 0, 0, 0, 0, 0x50,
+           0x18, 0, 0, 0, 0, 0, 0]) + b"data",
+    {"layers": ["eth", "ip", "ipv4", "transport", "tcp"], "l3_off": 14, "l4_off": 34,
+     "payload": b"data".hex(), "ip_proto": 6})
+b = bytearray(14 + 40 + 8 + 8 + 3)
+b[12:14] = (0x86DD).to_bytes(2, "big")
+b[14] = 0x60
+b[18:20] = (19).to_bytes(2, "big")
+b[20] = 0
+b[21] = 64
+b[54] = 17
+b[55] = 0
+b[62:64] = (1234).to_bytes(2, "big")
+b[64:66] = (53).to_bytes(2, "big")
+b[66:68] = (11).to_bytes(2, "big")
+b[70:] = b"dns"
+add("frame_slice_ipv6_hbh_udp", "frame.rs:764-784 (Frame path: HBH -> no transport, Q10)", b,
+    {"layers": ["eth", "ip", "ipv6"], "ip_nopt": 1, "payload": bytes(b[62:73]).hex()},
+    note="FrameSlice reports network 48 B / UDP; Frame keeps raw next_header 0 (Q10) and "
+         "exposes the bytes after the extension chain as payload")
+
+# ---- ipv4.rs:944-1204 ------------------------------------------------------
+IPV4_RT = bytes([0x45, 0x00, 0x00, 0x1c, 0x1c, 0x46, 0x40, 0x00, 0x40, 0x06, 0xb1, 0xe6,
+                 0xc0, 0xa8, 0x00, 0x01, 0xc0, 0xa8, 0x00, 0xc7,
+                 0xde, 0xad, 0xbe, 0xef, 0xca, 0xfe, 0xba, 0xbe])
+add("ipv4_round_trip", "ipv4.rs:944-969 (from_ip_packet)", IPV4_RT,
+    {"layers": ["eth", "ip", "ipv4", "transport"], "ip_ihl": 5, "ip_length": 28,
+     "ip_src": "192.168.0.1", "ip_dst": "192.168.0.199", "ip_csum": 0xB1E6,
+     "payload": "deadbeefcafebabe"},
+    flags=2, note="TCP over 8 bytes fails -> transport Some(None,None), payload = IP payload")
+IPV4_OPT = bytes([0x47, 0x00, 0x00, 0x20, 0x12, 0x34, 0x40, 0x00, 0x40, 0x11, 0x00, 0x00,
+                  0xc0, 0xa8, 0x00, 0x01, 0xc0, 0xa8, 0x00, 0x02,
+                  0x01, 0x87, 0x04, 0x12, 0x34, 0x00, 0x00, 0x00,
+                  0xde, 0xad, 0xbe, 0xef])
+add("ipv4_with_options", "ipv4.rs:971-1020 (from_ip_packet)", IPV4_OPT,
+    {"layers": ["eth", "ip", "ipv4", "transport"], "ip_ihl": 7, "ip_length": 32, "ip_nopt": 3,
+     "payload": "deadbeef"}, flags=2)
+IPV4_CS = bytes([0x45, 0x00, 0x00, 0x14, 0x00, 0x00, 0x40, 0x00, 0x40, 0x06, 0x00, 0x00,
+                 0x0a, 0x00, 0x00, 0x01, 0x0a, 0x00, 0x00, 0x02])
+add("ipv4_checksum_zero_field", "ipv4.rs:1073-1095 (checksum(&p) then reparse)", IPV4_CS,
+    {"layers": ["eth", "ip", "ipv4", "transport"], "ip_csum": 0, "ip_csum_consistent": True},
+    flags=2, note="reference asserts checksum(p) round-trips; value pinned by the oracle")
+STRICT = bytes([0x45, 0x00, 0x00, 0x28, 0x00, 0x00, 0x00, 0x00, 64, 17, 0, 0, 127, 0, 0, 1, 127,
+                0, 0, 1, 1, 2, 3, 4])
+add("ipv4_strict_truncation", "ipv4.rs:1176-1187 (strict -> Truncated)", STRICT,
+    {"status": 4}, flags=3)
+add("ipv4_lenient_truncation", "ipv4.rs:1186 (lenient parse succeeds)", STRICT,
+    {"layers": ["eth", "ip", "ipv4", "transport"], "ip_length": 24}, flags=2)
+ZERO = bytes([0x45, 0x00, 0x00, 0x00, 0x68, 0x23, 0x40, 0x00, 0x80, 0x06, 0x00, 0x00, 192, 168,
+              10, 113, 192, 168, 10, 10, 0xde, 0xad, 0xbe, 0xef])
+add("ipv4_zero_total_length", "ipv4.rs:1189-1204 (TSO capture: total = captured)", ZERO,
+    {"layers": ["eth", "ip", "ipv4", "transport"], "ip_length": 24, "payload": "deadbeef"},
+    flags=2)
+
+# ---- ipv6.rs:706-741, :797-802 ---------------------------------------------
+IPV6_P = bytes([0x60, 0xA1, 0x23, 0x45, 0x00, 0x08, 0x06, 0x40,
+                0xfe, 0x80, 0, 0, 0, 0, 0, 0, 0x02, 0x1a, 0x2b, 0xff, 0xfe, 0x1a, 0x2b, 0x3c,
+                0xff, 0x02, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x02]) + b"Hello!!\n"
+add("ipv6_from_bytes", "ipv6.rs:706-741 (from_ip_packet)", IPV6_P,
+    {"layers": ["eth", "ip", "ipv6", "transport"], "ip_tos": 0x0A, "ip_word": 0x12345,
+     "ip_length": 8, "ip_proto": 6, "ip_ttl": 0x40, "payload": b"Hello!!\n".hex()},
+    flags=2, note="traffic_class 0xa, flow label 0x12345; TCP over 8 bytes fails")
+add("ipv6_too_short", "ipv6.rs:797-802 (20 bytes rejected)", eth(bytes(20), 0x86DD),
+    {"layers": ["eth", "ip"]})
+
+# ---- L4 unit fixtures wrapped in IPv4 (tcp.rs, udp.rs, icmp.rs) ------------
+def ipv4_hdr(payload, proto, src=(10, 0, 0, 1), dst=(10, 0, 0, 2), ident=0):
+    tot = 20 + len(payload)
+    return bytes([0x45, 0, tot >> 8, tot & 255, ident >> 8, ident & 255, 0x40, 0, 64, proto, 0, 0,
+                  *src, *dst]) + bytes(payload)
+
+
+TCP_P = bytes([0xc1, 0x67, 0x23, 0x28, 0x90, 0x37, 0xd2, 0xb8, 0x94, 0x4b, 0xb2, 0x76, 0x80, 0x18,
+               0x0f, 0xaf, 0xc0, 0x31, 0x00, 0x00, 0x01, 0x01, 0x08, 0x0a, 0x2c, 0x57, 0xcd, 0xa5,
+               0x02, 0xa0, 0x41, 0x92]) + b"test"
+add("tcp_basic_parse", "tcp.rs:1276-1314 (wrapped in Eth/IPv4)", eth(ipv4_hdr(TCP_P, 6)),
+    {"layers": ["eth", "ip", "ipv4", "transport", "tcp"], "src_port": 0xC167,
+     "dst_port": 0x2328, "tcp_seq": 0x9037D2B8, "tcp_ack": 0x944BB276, "l4_length": 32,
+     "l4_type": 0x18, "tcp_window": 0x0FAF, "l4_csum": 0xC031, "l4_nopt": 3,
+     "payload": b"test".hex()})
+UDP_P = bytes([0x12, 0x34, 0xab, 0xcd, 0x00, 0x0c, 0x55, 0xaa]) + b"data"
+add("udp_basic_parse", "udp.rs:510-527 (wrapped in Eth/IPv4)", eth(ipv4_hdr(UDP_P, 17)),
+    {"layers": ["eth", "ip", "ipv4", "transport", "udp"], "src_port": 0x1234,
+     "dst_port": 0xABCD, "l4_length": 12, "l4_csum": 0x55AA, "payload": b"data".hex()})
+ICMP_P = bytes([8, 0, 0x3a, 0xbc, 0x04, 0xd2, 0x00, 0x2a]) + b"ping"
+add("icmp_echo_request", "icmp.rs:708-725 (wrapped in Eth/IPv4)", eth(ipv4_hdr(ICMP_P, 1)),
+    {"layers": ["eth", "ip", "ipv4", "icmp"], "l4_type": 8, "l4_code": 0, "l4_csum": 0x3ABC,
+     "payload": "04d2002a" + b"ping".hex()})
+
+# ---- bench fixtures (nex-packet/benches) -----------------------------------
+BENCH_V4_TCP = bytes([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 0x08, 0x00, 0x45, 0x00, 0x00, 0x30,
+                      0x12, 0x34, 0x40, 0x00, 64, 0x06, 0, 0, 192, 0, 2, 1, 198, 51, 100, 2, 0x04,
+                      0xd2, 0x00, 0x50, 0, 0, 0, 1, 0, 0, 0, 0, 0x50, 0x18, 0x20, 0x00, 0, 0, 0,
+                      0]) + b"hello!!!"
+add("bench_ipv4_tcp_frame", "benches/packet_parse.rs:9-16", BENCH_V4_TCP,
+    {"layers": ["eth", "ip", "ipv4", "transport", "tcp"], "payload": b"hello!!!".hex()})
+BENCH_V6_UDP = bytes([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 0x86, 0xdd, 0x60, 0, 0, 0, 0, 16, 17,
+                      64, 0xfe, 0x80, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0xfe, 0x80, 0, 0,
+                      0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 0x04, 0xd2, 0x00, 0x35, 0x00, 0x10, 0,
+                      0]) + b"dns!" + bytes([0, 1, 2, 3])
+add("bench_ipv6_udp_frame", "benches/packet_parse.rs:18-24", BENCH_V6_UDP,
+    {"layers": ["eth", "ip", "ipv6", "transport", "udp"], "dst_port": 53,
+     "payload": (b"dns!" + bytes([0, 1, 2, 3])).hex()})
+add("bench_ipv4_udp_packet", "benches/packet_operations.rs:18-21 (ipv4_checksum input)",
+    bytes([0x45, 0, 0, 28, 0x12, 0x34, 0x40, 0, 64, 17, 0, 0, 192, 0, 2, 1, 198, 51, 100, 2,
+           0x04, 0xd2, 0, 53, 0, 8, 0, 0]),
+    {"layers": ["eth", "ip", "ipv4", "transport", "udp"], "payload": ""}, flags=2)
+
+# ---- fuzz seed corpus (fuzz/corpus/*/*.hex) --------------------------------
+add("fuzz_ethernet_vlan_ipv4_frame", "fuzz/corpus/ethernet_vlan/ipv4_frame.hex",
+    bytes.fromhex("00112233445566778899aabb08004500001c1234400040110000c0000201c633640204d2003500080000"),
+    {"layers": ["eth", "ip", "ipv4", "transport", "udp"], "dst_port": 53})
+add("fuzz_ipv4_options", "fuzz/corpus/ipv4_options/options.hex",
+    bytes.fromhex("470000201234400040110000c0a80001c0a800020187041234000000deadbeef"),
+    {"layers": ["eth", "ip", "ipv4", "transport"], "ip_nopt": 3}, flags=2)
+add("fuzz_ipv6_hop_by_hop", "fuzz/corpus/ipv6_extensions/hop_by_hop.hex",
+    bytes.fromhex("6000000000100040fe800000000000000000000000000001fe800000000000000000000000000002"
+                  "110000000000000004d2003500080000"),
+    {"layers": ["eth", "ip", "ipv6"], "ip_nopt": 1}, flags=2)
+add("fuzz_icmpv6_ndp_rs", "fuzz/corpus/icmpv6_ndp/router_solicitation.hex (in Eth/IPv6)",
+    eth(ipv6_hdr(bytes.fromhex("85000000000000000101001122334455"), 58), 0x86DD),
+    {"layers": ["eth", "ip", "ipv6", "icmpv6"], "l4_type": 0x85})
+
+# ---- serialize path: udp_ping.rs:68-109 ------------------------------------
+BUILD = [{
+    "cite": "examples/udp_ping.rs:29-30,68-109; builder/udp.rs:116-130; builder/ipv4.rs:25-47",
+    "src_ip": "192.168.1.100", "dst_ip": "1.1.1.1", "sport": 53443, "dport": 33435,
+    "ip_flags": 2, "ttl": 64, "ip_id": 0, "udp_length": 8, "ip_total_length": 28,
+    "frame_len": 42,
+}]
+
+
+def main():
+    out = {"util": UTIL, "icmpv6": ICMPV6, "frames": V, "build": BUILD,
+           "source": "shellrow/nex reference tests (see each 'cite')"}
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_vectors.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print(f"wrote {len(V)} frame vectors to {path}")
+
+
+if __name__ == "__main__":
+    main()

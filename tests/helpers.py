@@ -1,0 +1,204 @@
+"""Shared test helpers: golden vectors, expectation checks, malformed mixes."""
+import ipaddress
+import json
+import os
+
+import numpy as np
+
+from nex_amd import abi
+from nex_amd.frame import frame_from_record
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_vectors.json")
+
+LAYER_BITS = {
+    "eth": abi.L_ETHERNET, "arp": abi.L_ARP, "ip": abi.L_IP, "ipv4": abi.L_IPV4,
+    "ipv6": abi.L_IPV6, "icmp": abi.L_ICMP, "icmpv6": abi.L_ICMPV6,
+    "transport": abi.L_TRANSPORT, "tcp": abi.L_TCP, "udp": abi.L_UDP,
+}
+LAYER_MASK = 0x3FF
+
+
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def check_expect(rec, frame: bytes, exp: dict, name=""):
+    """Assert a record satisfies a reference-test expectation dict."""
+    flags = int(rec["flags"])
+    if "status" in exp:
+        assert (flags >> abi.STATUS_SHIFT) & 7 == exp["status"], name
+        return
+    assert (flags >> abi.STATUS_SHIFT) & 7 == 0, name
+    if "layers" in exp:
+        want = 0
+        for l in exp["layers"]:
+            want |= LAYER_BITS[l]
+        assert flags & LAYER_MASK == want, (name, hex(flags & LAYER_MASK), hex(want))
+    fr = frame_from_record(rec, frame)
+    for k, v in exp.items():
+        if k in ("layers", "status"):
+            continue
+        if k == "payload":
+            assert fr.payload.hex() == v, (name, fr.payload.hex(), v)
+        elif k == "ip_version":
+            assert (fr.ip.ipv4 or fr.ip.ipv6).version == v, name
+        elif k == "ip_ihl":
+            assert int(rec["ip_ver_ihl"]) & 15 == v, name
+        elif k in ("ip_src", "ip_dst"):
+            assert str(ipaddress.IPv4Address(int(rec[k]))) == v, name
+        elif k == "ip_csum_consistent":
+            assert int(rec["ip_csum_calc"]) != 0 or int(rec["ip_csum"]) == 0, name
+        else:
+            assert int(rec[k]) == v, (name, k, int(rec[k]), v)
+
+
+def records_equal(a: np.ndarray, b: np.ndarray, frames=None, what=""):
+    """Bit-exact comparison of two record (or desc) arrays with a readable diff."""
+    assert a.dtype == b.dtype and a.shape == b.shape, (a.dtype, b.dtype, a.shape, b.shape)
+    ab, bb = a.view(np.uint8).reshape(len(a), -1), b.view(np.uint8).reshape(len(b), -1)
+    bad = np.nonzero((ab != bb).any(axis=1))[0]
+    if len(bad):
+        i = int(bad[0])
+        diffs = [n for n in a.dtype.names if a[i][n] != b[i][n]]
+        detail = {n: (int(a[i][n]), int(b[i][n])) for n in diffs}
+        fr = "" if frames is None else bytes(frames[i]).hex()
+        raise AssertionError(f"{what}: {len(bad)} of {len(a)} records differ; first #{i}: "
+                             f"{detail} frame={fr}")
+
+
+# ---- malformed / edge-case mixes (SURVEY.md App. C "malformed mix") ---------
+
+def _ipv4(payload, proto, ihl=5, opts=b"", total=None, ident=0x1234, flags_frag=0x4000):
+    hl = 20 + len(opts)
+    tot = hl + len(payload) if total is None else total
+    h = bytes([0x40 | ihl, 0, tot >> 8 & 255, tot & 255, ident >> 8, ident & 255,
+               flags_frag >> 8, flags_frag & 255, 64, proto, 0, 0, 10, 1, 2, 3, 10, 4, 5, 6])
+    return h + opts + payload
+
+
+def _eth(p, et=0x0800):
+    return bytes(range(1, 13)) + et.to_bytes(2, "big") + p
+
+
+def _ipv6(payload, nh, plen=None):
+    plen = len(payload) if plen is None else plen
+    return (bytes([0x6a, 0xbc, 0xde, 0xf1]) + plen.to_bytes(2, "big") + bytes([nh, 64]) +
+            bytes(range(16)) + bytes(range(16, 32)) + payload)
+
+
+def _tcp(payload, opts=b"", doff=None):
+    d = (20 + len(opts)) // 4 if doff is None else doff
+    return bytes([0x12, 0x34, 0x00, 0x50, 1, 2, 3, 4, 5, 6, 7, 8, (d << 4) | 0x3, 0x18, 0x20, 0,
+                  0xAB, 0xCD, 0, 7]) + opts + payload
+
+
+def _udp(payload, length=None):
+    ln = 8 + len(payload) if length is None else length
+    return bytes([0x04, 0xd2, 0x00, 0x35, ln >> 8, ln & 255, 0x12, 0x34]) + payload
+
+
+def crafted_frames():
+    """Deterministic edge cases for every quirk in SURVEY.md Appendix A."""
+    P = bytes(range(37))
+    f = []
+    f.append(b"")                                             # Q2 empty
+    f.append(bytes(13))                                       # Q2 < 14
+    f.append(_eth(b"", 0x0800))                               # IPv4 with 0 bytes
+    f.append(_eth(P[:19], 0x0800))                            # Q4 < 20
+    f.append(_eth(bytes([0x55]) + bytes(19), 0x0800))         # Q4 version
+    f.append(_eth(bytes([0x44]) + bytes(19), 0x0800))         # Q4 ihl < 5
+    f.append(_eth(bytes([0x4f]) + bytes(30), 0x0800))         # Q4 ihl*4 > len
+    f.append(_eth(_ipv4(_udp(P), 17, total=10)))              # Q4 total < ihl
+    f.append(_eth(_ipv4(_udp(P), 17, total=0)))               # Q5 zero total
+    f.append(_eth(_ipv4(_udp(P), 17, total=200)))             # Q5 declared > captured
+    f.append(_eth(_ipv4(_udp(P), 17)) + bytes(9))             # Q5 Ethernet padding
+    f.append(_eth(_ipv4(_udp(P, length=7), 17)))              # Q14 UDP length < 8
+    f.append(_eth(_ipv4(_udp(P, length=100), 17)))            # Q14 UDP length > avail
+    f.append(_eth(_ipv4(_udp(P, length=20), 17)))             # Q14 bytes beyond UDP length
+    f.append(_eth(_ipv4(_udp(P[:3]), 17)))                    # odd UDP length
+    f.append(_eth(_ipv4(P[:5], 17)))                          # UDP < 8
+    f.append(_eth(_ipv4(_tcp(P), 6)))
+    f.append(_eth(_ipv4(_tcp(P, doff=4), 6)))                 # Q13 doff < 5
+    f.append(_eth(_ipv4(_tcp(P[:3], doff=15), 6)))            # Q13 doff*4 > len
+    f.append(_eth(_ipv4(_tcp(P, opts=b"\x01\x01\x08\x0a" + bytes(8)), 6)))   # NOP NOP TS
+    f.append(_eth(_ipv4(_tcp(P, opts=b"\x02\x04\x05\xb4\x00\x13\x22\x33"), 6)))  # MSS EOL junk
+    f.append(_eth(_ipv4(_tcp(P, opts=b"\x00\x99\x99\x99\x11\x22\x33\x44"), 6)))  # early EOL
+    f.append(_eth(_ipv4(_tcp(P, opts=b"\x01\x01\x01\x02"), 6)))          # kind w/o length
+    f.append(_eth(_ipv4(_tcp(P, opts=b"\x05\x01\x00\x00"), 6)))          # len < 2
+    f.append(_eth(_ipv4(_tcp(P, opts=b"\x05\x09\x00\x00"), 6)))          # overflow
+    f.append(_eth(_ipv4(_tcp(P[:1], opts=b"\x03\x03\x07\x00"), 6)))      # odd payload
+    f.append(_eth(_ipv4(P, 1)))                                # ICMP
+    f.append(_eth(_ipv4(bytes(7), 1)))                         # Q15 ICMP < 8
+    f.append(_eth(_ipv4(bytes(8), 1)))                         # ICMP all-zero (csum 0xFFFF)
+    f.append(_eth(_ipv4(P, 200)))                              # Q8 proto 200 -> 255
+    f.append(_eth(_ipv4(P, 255)))
+    f.append(_eth(_ipv4(P, 50)))                               # Q9 other proto
+    f.append(_eth(_ipv4(_udp(P), 17, flags_frag=0x2001)))      # Q7 fragment
+    # IPv4 options (Q6, Q16, Q17)
+    f.append(_eth(_ipv4(_udp(P), 17, ihl=7, opts=b"\x01\x87\x04\x12\x34\x00\x00\x00")))
+    f.append(_eth(_ipv4(_udp(P), 17, ihl=7, opts=b"\x00\x11\x22\x33\x44\x55\x66\x77")))  # EOL first
+    f.append(_eth(_ipv4(_udp(P), 17, ihl=8, opts=b"\x01\x00" + bytes(10))))
+    f.append(_eth(_ipv4(_udp(P), 17, ihl=6, opts=b"\x07")))   # no room for length
+    f.append(_eth(_ipv4(_udp(P), 17, ihl=6, opts=b"\x07\x01\x00\x00")))  # len < 2
+    f.append(_eth(_ipv4(_udp(P), 17, ihl=6, opts=b"\x07\x09\x00\x00")))  # overflow
+    f.append(_eth(_ipv4(b"", 17, ihl=15, opts=b"\x00" + bytes(39))))       # Q17 panic case
+    f.append(_eth(_ipv4(P[:6], 17, ihl=15, opts=b"\x00" + bytes(39))))    # Q17 window into payload
+    f.append(_eth(_ipv4(_udp(P), 17, ihl=15, opts=b"\x01" * 40)))
+    # IPv6 (Q10-Q12)
+    f.append(_eth(_ipv6(_udp(P), 17), 0x86DD))
+    f.append(_eth(_ipv6(_tcp(P), 6), 0x86DD))
+    f.append(_eth(_ipv6(_tcp(P, opts=b"\x01\x01\x08\x0a" + bytes(8)), 6), 0x86DD))
+    f.append(_eth(_ipv6(P, 58), 0x86DD))
+    f.append(_eth(_ipv6(P[:7], 58), 0x86DD))
+    f.append(_eth(_ipv6(_udp(P), 17, plen=0), 0x86DD))        # Q11 payload_length 0
+    f.append(_eth(_ipv6(_udp(P), 17, plen=500), 0x86DD))      # Q11 > captured
+    f.append(_eth(_ipv6(bytes([17, 0]) + bytes(6) + _udp(P), 0), 0x86DD))   # HBH
+    f.append(_eth(_ipv6(bytes([44, 1]) + bytes(14) + bytes([17, 0]) + bytes(6) + _udp(P), 60), 0x86DD))
+    f.append(_eth(_ipv6(bytes([6, 0, 0, 1]) + bytes(4) + _tcp(P), 44), 0x86DD))   # Frag
+    f.append(_eth(_ipv6(bytes([17, 0, 0, 0]) + bytes(4) + _udp(P), 43), 0x86DD))  # Route
+    f.append(_eth(_ipv6(bytes([17, 9]), 0), 0x86DD))          # Q12 truncated ext
+    f.append(_eth(_ipv6(bytes([17]), 0), 0x86DD))             # Q12 no room
+    f.append(_eth(_ipv6(bytes([17, 0, 0]), 43), 0x86DD))      # route < 4
+    f.append(_eth(_ipv6(bytes([17, 0, 0, 0, 0]), 44), 0x86DD))  # frag < 8
+    f.append(_eth(_ipv6(_udp(P), 51), 0x86DD))                # AH not walked
+    f.append(_eth(_ipv6(_udp(P), 200), 0x86DD))               # reserved
+    f.append(_eth(bytes([0x50]) + bytes(45), 0x86DD))         # version
+    f.append(_eth(bytes(39), 0x86DD))                         # < 40
+    # ARP / VLAN / misc EtherTypes (Q3)
+    f.append(_eth(bytes(range(28)), 0x0806))
+    f.append(_eth(bytes(range(27)), 0x0806))
+    f.append(_eth(bytes(range(40)), 0x0806))
+    f.append(_eth(b"\x20\x01\x08\x00" + _ipv4(_udp(P), 17), 0x8100))
+    f.append(_eth(P, 0x88CC))
+    f.append(_eth(b"", 0x1234))
+    return f
+
+
+def mutate_frames(rng: np.random.Generator, base, n: int):
+    """Random structural mutations of valid frames (fuzz-corpus style)."""
+    out = []
+    for _ in range(n):
+        fr = bytearray(base[int(rng.integers(len(base)))])
+        k = int(rng.integers(8))
+        if k == 0 and len(fr):                       # truncate
+            fr = fr[: int(rng.integers(len(fr) + 1))]
+        elif k == 1 and len(fr) > 14:                # flip random header bytes
+            for _ in range(int(rng.integers(1, 4))):
+                j = int(rng.integers(14, min(len(fr), 80)))
+                fr[j] = int(rng.integers(256))
+        elif k == 2 and len(fr) > 17:                # random total length / payload length
+            j = 16 if fr[12:14] == b"\x08\x00" else 18
+            fr[j:j + 2] = int(rng.integers(0, 1 << 16)).to_bytes(2, "big")
+        elif k == 3 and len(fr) > 14:                # random IHL / version nibble
+            fr[14] = int(rng.integers(256))
+        elif k == 4:                                 # append padding / junk
+            fr += bytes(rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8))
+        elif k == 5 and len(fr) > 46:                # random L4 length-ish fields
+            for j in (38, 39, 46, 47, 58, 59, 66):
+                if j < len(fr) and rng.random() < 0.4:
+                    fr[j] = int(rng.integers(256))
+        elif k == 6:                                 # random bytes frame
+            fr = bytearray(rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8))
+        out.append(bytes(fr))
+    return out

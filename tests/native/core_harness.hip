@@ -1,0 +1,34 @@
+// TEST INFRASTRUCTURE ONLY: runs the engine's device parse core
+// (nex_amd/csrc/frame_core.hpp, the exact code the gfx950 kernels execute)
+// on the host CPU, reproducing the LaneWindow staging (16-B aligned LDS slot,
+// window of `window` bytes, remainder read from "HBM"), so differential tests
+// against the oracle run without a GPU. Not part of the product library.
+#include <string.h>
+
+#include "../../nex_amd/csrc/frame_core.hpp"
+
+extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uint64_t* offsets,
+                             const uint32_t* lengths, uint32_t stride, uint64_t count,
+                             uint32_t flags, uint32_t ip_offset, uint32_t window,
+                             nexg_record* out) {
+    alignas(16) uint8_t slot[65536 + 32];
+    for (uint64_t i = 0; i < count; i++) {
+        const uint64_t off = offsets ? offsets[i] : i * (uint64_t)stride;
+        const uint64_t len = lengths ? lengths[i] : (offsets ? offsets[i + 1] - off : stride);
+        nexg_record r{};
+        if (len > 65535 || off > data_bytes || len > data_bytes - off) {
+            r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
+        } else {
+            const uint8_t* g = data + off;
+            const uint32_t o = (uint32_t)(reinterpret_cast<uint64_t>(g) & 15u);
+            const uint32_t wlen = len < window ? (uint32_t)len : window;
+            memset(slot, 0xA5, sizeof(slot));  // poison: bytes outside the window must not matter
+            memcpy(slot + o, g, wlen);
+            nexg::WinFrame f{slot, g, o, wlen};
+            nexg::parse_frame(f, (uint32_t)(reinterpret_cast<uint64_t>(g) & 1u), (uint32_t)len, flags,
+                              ip_offset, r);
+        }
+        out[i] = r;
+    }
+    return 0;
+}

@@ -1,0 +1,79 @@
+"""CPU: the C-ABI library loads and exports every symbol include/nexg.h
+declares, and the Python struct mirrors match the C layout. No compute calls
+(there is no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from nex_amd import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "nexg.h")
+LIB = os.path.join(ROOT, "nex_amd", "libnexg.so")
+
+
+def declared_functions():
+    text = open(HDR).read()
+    return sorted(set(re.findall(r"\b(nexg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_exported_list():
+    assert declared_functions() == sorted(abi.EXPORTED_SYMBOLS)
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libnexg.so not built")
+def test_library_exports_every_symbol():
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [s for s in declared_functions() if s not in exported]
+    assert not missing, missing
+    lib = ctypes.CDLL(LIB)
+    for s in declared_functions():
+        assert getattr(lib, s) is not None
+    lib.nexg_abi_version.restype = ctypes.c_int
+    assert lib.nexg_abi_version() == abi.ABI_VERSION
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libnexg.so not built")
+def test_library_has_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-S", LIB], capture_output=True, text=True)
+    assert ".hip_fatbin" in out.stdout
+    blob = open(LIB, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_struct_layouts_match_c(tmp_path):
+    """Compile a probe against include/nexg.h and compare sizes/offsets."""
+    fields = abi.RECORD_DTYPE.names
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', 'int main(void){',
+             'printf("%zu %zu %zu %zu %zu\\n", sizeof(nexg_record), sizeof(nexg_desc), '
+             'sizeof(nexg_frames), sizeof(nexg_parse_option), sizeof(nexg_udp4_build));']
+    for f in fields:
+        lines.append(f'printf("%zu\\n", offsetof(nexg_record, {f}));')
+    for f, _ in abi.Udp4Build._fields_:
+        lines.append(f'printf("%zu\\n", offsetof(nexg_udp4_build, {f}));')
+    lines.append("return 0;}")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-std=c11", "-o", str(exe), str(src)])
+    out = subprocess.check_output([str(exe)], text=True).split()
+    sizes = list(map(int, out[:5]))
+    assert sizes == [64, 8, ctypes.sizeof(abi.Frames), ctypes.sizeof(abi.ParseOptionC),
+                     ctypes.sizeof(abi.Udp4Build)]
+    offs = list(map(int, out[5:5 + len(fields)]))
+    assert offs == [abi.RECORD_DTYPE.fields[f][1] for f in fields]
+    boffs = list(map(int, out[5 + len(fields):]))
+    assert boffs == [getattr(abi.Udp4Build, f).offset for f, _ in abi.Udp4Build._fields_]
+
+
+def test_engine_refuses_without_library(monkeypatch, tmp_path):
+    """The product path fails loudly when the HIP library is missing."""
+    from nex_amd import _lib
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.NexgLibraryMissing):
+        _lib.load()

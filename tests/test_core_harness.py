@@ -1,0 +1,71 @@
+"""CPU: the engine's device parse core (frame_core.hpp, the code the gfx950
+kernels run) executed on the host via tests/native/core_harness.hip, checked
+bit-exactly against the oracle on crafted, mutated and generated frames across
+parse modes, frame alignments and LDS window sizes. This is the pre-GPU gate;
+tests/test_gpu_parity.py repeats the comparison on the device."""
+import numpy as np
+import pytest
+
+from nex_amd import abi
+from tests import helpers
+from tests.native import harness
+
+
+def pack(frames, align=1, base_off=0):
+    offs, pos = [], base_off
+    for f in frames:
+        offs.append(pos)
+        pos += (len(f) + align - 1) // align * align
+    buf = np.zeros(pos + 16, np.uint8)
+    for f, p in zip(frames, offs):
+        buf[p:p + len(f)] = np.frombuffer(f, np.uint8)
+    return buf, np.array(offs, np.uint64), np.array([len(f) for f in frames], np.uint32)
+
+
+@pytest.fixture(scope="module")
+def corpus(oracle):
+    g = helpers.golden()
+    base = ([bytes.fromhex(v["frame"]) for v in g["frames"]] + helpers.crafted_frames() +
+            [oracle.gen_frame(abi.WL_IMIX, i) for i in range(60)] +
+            [oracle.gen_frame(abi.WL_UDP64, i) for i in range(20)])
+    rng = np.random.default_rng(2024)
+    return base + helpers.mutate_frames(rng, base, 12000)
+
+
+@pytest.mark.parametrize("flags", [0, abi.PARSE_STRICT, abi.PARSE_FROM_IP,
+                                   abi.PARSE_FROM_IP | abi.PARSE_STRICT])
+@pytest.mark.parametrize("layout", [(1, 0), (1, 3), (4, 0), (16, 0)], ids=str)
+def test_core_matches_oracle(oracle, corpus, flags, layout):
+    buf, offs, lens = pack(corpus, *layout)
+    ipo = 14 if flags & abi.PARSE_FROM_IP else 0
+    want = oracle.parse_packed(buf, offs, lens, flags=flags, ip_offset=ipo)
+    for window in (128, 64, 0):
+        got = harness.parse_packed(buf, offs, lens, flags=flags, ip_offset=ipo, window=window)
+        helpers.records_equal(got, want, [buf[p:p + l] for p, l in zip(offs, lens)],
+                              f"flags={flags} layout={layout} window={window}")
+
+
+def test_core_bad_extent(oracle):
+    buf = np.zeros(100, np.uint8)
+    got = harness.parse_packed(buf, np.array([0, 90, 200], np.uint64), np.array([64, 20, 4], np.uint32))
+    st = abi.status_of(got["flags"])
+    assert list(st) == [0, abi.ERR_BAD_EXTENT, abi.ERR_BAD_EXTENT]
+
+
+def test_core_max_size_frames(oracle):
+    """65535-byte frames (the ABI maximum): IPv4 zero total length, UDP and
+    TCP spanning the whole frame, IPv6 jumbo-ish payload."""
+    rng = np.random.default_rng(7)
+    body = bytes(rng.integers(0, 256, 65535 - 14 - 20 - 8, dtype=np.uint8))
+    frames = [
+        helpers._eth(helpers._ipv4(helpers._udp(body), 17, total=0)),
+        helpers._eth(helpers._ipv4(helpers._tcp(body[:-12]), 6, total=0)),
+        helpers._eth(helpers._ipv6(helpers._udp(body[:-20]), 17, plen=65535), 0x86DD),
+        helpers._eth(helpers._ipv4(body + bytes(8), 1, total=0)),
+    ]
+    frames = [f[:65535] for f in frames]
+    buf, offs, lens = pack(frames, 1, 1)
+    want = oracle.parse_packed(buf, offs, lens)
+    got = harness.parse_packed(buf, offs, lens)
+    helpers.records_equal(got, want, None, "max-size")
+    assert (want["flags"] & abi.C_L4_CHECKED).all()

@@ -1,0 +1,191 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the oracle.
+
+Bit-exact on every record/descriptor field: this is integer/byte work, there
+is no tolerance. Small cases compare every frame; full-size (16M-frame)
+batches compare a random sample plus size-independent properties."""
+import numpy as np
+import pytest
+
+from nex_amd import abi
+from nex_amd.engine import FrameBatch
+from nex_amd.frame import ParseMode, ParseOption
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+
+FLAGS = [(ParseOption(), ParseMode.Lenient), (ParseOption(), ParseMode.Strict),
+         (ParseOption(True, 14), ParseMode.Lenient), (ParseOption(True, 14), ParseMode.Strict)]
+
+
+def desc_of(recs):
+    d = np.zeros(len(recs), abi.DESC_DTYPE)
+    for n in abi.DESC_DTYPE.names:
+        d[n] = recs[n]
+    return d
+
+
+@pytest.fixture(scope="module")
+def corpus(oracle):
+    g = helpers.golden()
+    base = ([bytes.fromhex(v["frame"]) for v in g["frames"]] + helpers.crafted_frames() +
+            [oracle.gen_frame(abi.WL_IMIX, i) for i in range(60)] +
+            [oracle.gen_frame(abi.WL_UDP64, i) for i in range(20)])
+    rng = np.random.default_rng(99)
+    return base + helpers.mutate_frames(rng, base, 30000)
+
+
+def test_golden_frames_on_gpu(engine, oracle):
+    g = helpers.golden()["frames"]
+    for v in g:
+        fr = bytes.fromhex(v["frame"])
+        opt = ParseOption(bool(v["parse_flags"] & abi.PARSE_FROM_IP), v["ip_offset"])
+        mode = ParseMode.Strict if v["parse_flags"] & abi.PARSE_STRICT else ParseMode.Lenient
+        rec = engine.parse_to_numpy(FrameBatch.from_frames([fr]), opt, mode)[0]
+        helpers.check_expect(rec, fr, v["expect"], v["name"])
+        want = oracle.parse_frame(fr, v["parse_flags"], v["ip_offset"])
+        assert rec.tobytes() == want.tobytes(), v["name"]
+
+
+@pytest.mark.parametrize("pad", [1, 4, 16])
+@pytest.mark.parametrize("opt,mode", FLAGS, ids=lambda x: str(x))
+def test_packed_mix_matches_oracle(engine, oracle, corpus, pad, opt, mode):
+    batch = FrameBatch.from_frames(corpus, pad_to=pad)
+    flags = opt.flags(mode)
+    want = oracle.parse_frames(corpus, flags, opt.offset)
+    got = engine.parse_to_numpy(batch, opt, mode, abi.OUT_RECORD)
+    helpers.records_equal(got, want, corpus, f"packed pad={pad} flags={flags}")
+    got_d = engine.parse_to_numpy(batch, opt, mode, abi.OUT_DESC)
+    helpers.records_equal(got_d, desc_of(want), corpus, "desc")
+
+
+@pytest.mark.parametrize("stride", [64, 128, 96, 80, 200])
+def test_fixed_stride_matches_oracle(engine, oracle, corpus, stride):
+    rng = np.random.default_rng(stride)
+    sel = [f for f in corpus if len(f) <= stride][:20000]
+    arr = np.zeros((len(sel), stride), np.uint8)
+    fill = rng.integers(0, 256, arr.shape, dtype=np.uint8)  # bytes past each frame: junk
+    arr[:] = fill
+    for i, f in enumerate(sel):
+        arr[i, :len(f)] = np.frombuffer(f, np.uint8)
+    lens = np.array([len(f) for f in sel], np.int32)
+    want = oracle.parse_frames(sel)
+    got = engine.parse_to_numpy(FrameBatch.from_strided(arr, lengths=lens))
+    helpers.records_equal(got, want, sel, f"stride={stride} with lengths")
+    full = [bytes(arr[i]) for i in range(len(sel))]
+    want = oracle.parse_frames(full)
+    got = engine.parse_to_numpy(FrameBatch.from_strided(arr))
+    helpers.records_equal(got, want, full, f"stride={stride} full")
+
+
+def test_generators_match_oracle(engine, oracle):
+    import torch
+    n = 3000
+    b = engine.gen_batch(abi.WL_UDP64, n, first_index=12345)
+    torch.cuda.synchronize()
+    data = b.data.cpu().numpy()
+    for i in range(0, n, 7):
+        assert bytes(data[i * 64:(i + 1) * 64]) == oracle.gen_frame(abi.WL_UDP64, 12345 + i), i
+    b = engine.gen_batch(abi.WL_IMIX, n, first_index=777)
+    offs = b.offsets.cpu().numpy()
+    data = b.data.cpu().numpy()
+    for i in range(0, n, 3):
+        assert bytes(data[offs[i]:offs[i + 1]]) == oracle.gen_frame(abi.WL_IMIX, 777 + i), i
+    p = [t.cpu().numpy() for t in engine.gen_udp4_params(100, first_index=5)]
+    for i in range(100):
+        want = oracle.gen_udp4_params(5 + i)
+        got = (int(p[0][i]) & 0xFFFFFFFF, int(p[1][i]) & 0xFFFFFFFF, int(p[2][i]) & 0xFFFF,
+               int(p[3][i]) & 0xFFFF, int(p[4][i]) & 0xFFFF)
+        assert got == want
+
+
+@pytest.mark.parametrize("workload,count", [(abi.WL_UDP64, 16 << 20), (abi.WL_IMIX, 16 << 20)])
+def test_full_size_sampled(engine, oracle, workload, count):
+    """BASELINE.json full sizes: sample 65536 frames bit-exact + properties."""
+    import torch
+    b = engine.gen_batch(workload, count)
+    desc = engine.parse(b, out_kind=abi.OUT_DESC)
+    torch.cuda.synchronize()
+    d = desc.cpu().numpy().view(abi.DESC_DTYPE)
+    f = d["flags"]
+    assert (abi.status_of(f) == 0).all()
+    assert (f & abi.C_L4_CHECKED).all()
+    bad = ((f & abi.C_L4_OK) == 0) | (((f & abi.C_IP_CHECKED) != 0) & ((f & abi.C_IP_OK) == 0))
+    assert abs(bad.mean() - 1 / 16) < 0.002
+    rng = np.random.default_rng(workload)
+    idx = np.sort(rng.choice(count, 65536, replace=False))
+    if workload == abi.WL_UDP64:
+        assert (d["payload_len"] == 22).all() and (d["payload_off"] == 42).all()
+        raw = b.data.cpu().numpy().reshape(count, 64)[idx]
+        frames = [bytes(r) for r in raw]
+    else:
+        offs = b.offsets.cpu().numpy()
+        data = b.data.cpu().numpy()
+        frames = [bytes(data[offs[i]:offs[i + 1]]) for i in idx]
+    want = oracle.parse_frames(frames)
+    helpers.records_equal(d[idx], desc_of(want), frames, "full-size sample")
+    # generated frames are exactly the oracle generator's
+    for k in range(0, 65536, 4096):
+        assert frames[k] == oracle.gen_frame(workload, int(idx[k]))
+
+
+def test_checksum_batch_kats(engine, oracle):
+    util = helpers.golden()["util"]
+    bufs = [bytes.fromhex(v["data"]) for v in util["checksum"]]
+    got = engine.checksum(FrameBatch.from_frames(bufs), 2**32 - 1).cpu().numpy().astype(np.uint16)
+    assert list(got) == [v["checksum"] for v in util["checksum"]]
+    rng = np.random.default_rng(3)
+    bufs = [bytes(rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8)) for _ in range(5000)]
+    for skip in (0, 1, 5, 70, 2**32 - 1):
+        got = engine.checksum(FrameBatch.from_frames(bufs, pad_to=1), skip).cpu().numpy().astype(np.uint16)
+        want = [oracle.checksum(x, skip) for x in bufs]
+        assert list(got) == want, skip
+    # KAT: checksum(0..11, 1) == !sum_be_words == !7190 (util.rs:193)
+    got = engine.checksum(FrameBatch.from_frames([bytes(range(11))]), 1).cpu().numpy().astype(np.uint16)
+    assert int(got[0]) == (~7190) & 0xFFFF
+
+
+@pytest.mark.parametrize("payload_len", [0, 5, 22])
+def test_build_udp4_matches_oracle(engine, oracle, payload_len):
+    import torch
+    n = 20000
+    p = engine.gen_udp4_params(n, first_index=42)
+    payload = bytes(range(7, 7 + payload_len))
+    pt = torch.tensor(list(payload), dtype=torch.uint8, device="cuda") if payload_len else None
+    smac, dmac = bytes([2, 0, 0, 0, 0, 1]), bytes([2, 0, 0, 0, 0, 2])
+    out = engine.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=smac, dst_mac=dmac, ttl=64,
+                            ip_flags=2, payload=pt)
+    torch.cuda.synchronize()
+    L = 42 + payload_len
+    data = out.cpu().numpy()[: n * L].reshape(n, L)
+    host = [t.cpu().numpy() for t in p]
+    for i in range(0, n, 97):
+        want = oracle.build_udp4(smac, dmac, int(host[0][i]) & 0xFFFFFFFF, int(host[1][i]) & 0xFFFFFFFF,
+                                 int(host[2][i]) & 0xFFFF, int(host[3][i]) & 0xFFFF,
+                                 int(host[4][i]) & 0xFFFF, 64, 2, 0, payload)
+        assert bytes(data[i]) == want, i
+    # every built frame verifies through the GPU parse path
+    recs = engine.parse_to_numpy(FrameBatch(data=out, count=n, stride=L), out_kind=abi.OUT_DESC)
+    assert ((recs["flags"] & (abi.C_IP_OK | abi.C_L4_OK)) == (abi.C_IP_OK | abi.C_L4_OK)).all()
+
+
+def test_udp_ping_golden_on_gpu(engine):
+    import torch
+    from nex_amd.engine import u32_tensor
+    b = helpers.golden()["build"][0]
+    ip = lambda s: int.from_bytes(bytes(map(int, s.split("."))), "big")
+    out = engine.build_udp4(u32_tensor([ip(b["src_ip"])]), u32_tensor([ip(b["dst_ip"])]),
+                            def_src_port=b["sport"], def_dst_port=b["dport"], ip_flags=b["ip_flags"])
+    torch.cuda.synchronize()
+    f = bytes(out.cpu().numpy()[:42])
+    assert f.hex() == "00000000000000000000000008004500001c00004000401176c3c0a8016401010101d0c3829b0008e870"
+
+
+def test_bad_extent_and_empty(engine):
+    import torch
+    data = torch.zeros(100, dtype=torch.uint8, device="cuda")
+    offs = torch.tensor([0, 90, 200], dtype=torch.int64, device="cuda")
+    lens = torch.tensor([64, 20, 4], dtype=torch.int32, device="cuda")
+    d = engine.parse_to_numpy(FrameBatch(data=data, count=3, offsets=offs, lengths=lens), out_kind=abi.OUT_DESC)
+    assert list(abi.status_of(d["flags"])) == [0, abi.ERR_BAD_EXTENT, abi.ERR_BAD_EXTENT]
+    d = engine.parse_to_numpy(FrameBatch(data=data, count=0, stride=64), out_kind=abi.OUT_DESC)
+    assert len(d) == 0

@@ -1,0 +1,186 @@
+"""CPU: the oracle (CPU restatement) pinned against the reference's own KATs,
+fixtures and quirks (tests/golden/reference_vectors.json)."""
+import numpy as np
+import pytest
+
+from nex_amd import abi
+from nex_amd.frame import frame_from_record, Truncated, BufferTooShort, Malformed
+from tests import helpers
+
+
+G = helpers.golden()
+
+
+@pytest.mark.parametrize("v", G["util"]["sum_be_words"], ids=lambda v: f"{v['data'][:8]}-{v['skipword']}")
+def test_util_sum_be_words_kat(oracle, v):
+    # util.rs:190-217
+    assert oracle.sum_be_words(bytes.fromhex(v["data"]), v["skipword"]) == v["sum"]
+
+
+def test_util_joined_kat(oracle):
+    # util.rs:244-254
+    for v in G["util"]["joined_equals_contiguous"]:
+        j = oracle.sum_be_words_joined(bytes.fromhex(v["data"]), 2**63, bytes.fromhex(v["extra"]))
+        assert j == oracle.sum_be_words(bytes.fromhex(v["contiguous"]), 2**63)
+
+
+def test_util_checksum_kat(oracle):
+    # util.rs:256-261
+    for v in G["util"]["checksum"]:
+        assert oracle.checksum(bytes.fromhex(v["data"]), v["skipword"]) == v["checksum"]
+
+
+def test_checksum_empty_is_zero(oracle):
+    # Q19: util.rs:66-68
+    assert oracle.checksum(b"", 0) == 0
+    assert oracle.checksum(bytes(4), 99) == 0xFFFF
+
+
+def test_icmpv6_checksum_kat(oracle):
+    # icmpv6.rs:606-631
+    k = G["icmpv6"]
+    pkt = bytes.fromhex(k["packet"])
+    src, dst = bytes.fromhex(k["src"]), bytes.fromhex(k["dst"])
+    assert oracle.ipv6_checksum(pkt, 1, src, dst, 58) == k["checksum"]
+    assert oracle.ipv6_checksum(b"\x81" + pkt[1:], 1, src, dst, 58) == k["checksum_type_0x81"]
+
+
+@pytest.mark.parametrize("v", G["frames"], ids=lambda v: v["name"])
+def test_golden_frames(oracle, v):
+    fr = bytes.fromhex(v["frame"])
+    rec = oracle.parse_frame(fr, v["parse_flags"], v["ip_offset"])
+    helpers.check_expect(rec, fr, v["expect"], v["name"])
+
+
+def test_survey_crosscheck_values(oracle):
+    """Values an independent scratch restatement produced during the survey
+    (SURVEY.md §8(c)); not reference-asserted, but a second implementation."""
+    g = {v["name"]: bytes.fromhex(v["frame"]) for v in G["frames"]}
+    r = oracle.parse_frame(g["ipv4_udp_frame"])
+    assert (int(r["ip_csum_calc"]), int(r["l4_csum_calc"])) == (0x8E95, 0x0A92)
+    r = oracle.parse_frame(g["bench_ipv4_tcp_frame"])
+    assert (int(r["ip_csum_calc"]), int(r["l4_csum_calc"])) == (0x3C5D, 0x3956)
+    r = oracle.parse_frame(g["ipv4_round_trip"], abi.PARSE_FROM_IP)
+    assert int(r["ip_csum_calc"]) == 0x9C7D and not (int(r["flags"]) & abi.C_IP_OK)
+
+
+def test_udp_ping_build_golden(oracle):
+    b = G["build"][0]
+    f = oracle.build_udp4(bytes(6), bytes(6), 0xC0A80164, 0x01010101, b["sport"], b["dport"],
+                          ip_flags=b["ip_flags"])
+    assert len(f) == b["frame_len"]
+    r = oracle.parse_frame(f)
+    assert int(r["flags"]) & abi.C_IP_OK and int(r["flags"]) & abi.C_L4_OK
+    assert int(r["ip_length"]) == b["ip_total_length"] and int(r["l4_length"]) == b["udp_length"]
+    assert (int(r["l4_csum"]), int(r["ip_csum"])) == (0xE870, 0x76C3)  # survey cross-check
+    with pytest.raises(ValueError):
+        oracle.build_udp4(bytes(6), bytes(6), 1, 2, 3, 4, payload=bytes(65535 - 28 + 1))
+
+
+# ---- quirks -------------------------------------------
+
+def _rec(oracle, fr, flags=0, off=0):
+    return oracle.parse_frame(fr, flags, off)
+
+
+def test_q2_short_ethernet_is_error(oracle):
+    with pytest.raises(BufferTooShort):
+        frame_from_record(_rec(oracle, bytes(13)), bytes(13))
+    with pytest.raises(Malformed):
+        frame_from_record(_rec(oracle, bytes(10), abi.PARSE_FROM_IP, 3), bytes(10))
+
+
+def test_q4_lenient_ipv4_failure(oracle):
+    fr = helpers._eth(bytes([0x44]) + bytes(30))
+    f = frame_from_record(_rec(oracle, fr), fr)
+    assert f.ip is not None and f.ip.ipv4 is None and f.transport is None and f.payload == b""
+
+
+def test_q5_effective_total_length(oracle):
+    P = bytes(range(20))
+    fr = helpers._eth(helpers._ipv4(helpers._udp(P), 17, total=0))
+    assert int(_rec(oracle, fr)["ip_length"]) == len(fr) - 14
+    fr = helpers._eth(helpers._ipv4(helpers._udp(P), 17)) + bytes(10)  # padding excluded
+    f = frame_from_record(_rec(oracle, fr), fr)
+    assert f.payload == P
+    fr = helpers._eth(helpers._ipv4(helpers._udp(P), 17, total=400))
+    assert int(_rec(oracle, fr)["ip_length"]) == len(fr) - 14
+    with pytest.raises(Truncated):
+        frame_from_record(_rec(oracle, fr, abi.PARSE_STRICT), fr)
+
+
+def test_q8_reserved_protocol_changes_ip_checksum(oracle):
+    fr = bytearray(helpers._eth(helpers._ipv4(bytes(8), 200)))
+    r = _rec(oracle, bytes(fr))
+    assert int(r["ip_proto"]) == 255
+    # the serialised header carries 255, so checksumming the raw bytes differs
+    raw = oracle.checksum(bytes(fr[14:34]), 5)
+    assert int(r["ip_csum_calc"]) != raw
+
+
+def test_q10_ipv6_extension_keeps_raw_next_header(oracle):
+    P = bytes(range(16))
+    fr = helpers._eth(helpers._ipv6(bytes([17, 0]) + bytes(6) + helpers._udp(P), 0), 0x86DD)
+    r = _rec(oracle, fr)
+    assert int(r["ip_proto"]) == 0 and not (int(r["flags"]) & abi.L_TRANSPORT)
+    assert int(r["payload_off"]) == 14 + 48
+
+
+def test_q13_tcp_failure_keeps_ip_payload(oracle):
+    P = bytes(range(30))
+    seg = helpers._tcp(P, doff=4)
+    fr = helpers._eth(helpers._ipv4(seg, 6))
+    f = frame_from_record(_rec(oracle, fr), fr)
+    assert f.transport.tcp is None and f.transport.udp is None and f.payload == seg
+
+
+def test_q15_icmp_needs_8_bytes(oracle):
+    fr = helpers._eth(helpers._ipv4(bytes(7), 1))
+    f = frame_from_record(_rec(oracle, fr), fr)
+    assert f.ip.icmp is None and f.payload == bytes(7) and f.transport is None
+
+
+def test_q16_tcp_early_eol_reserialises(oracle):
+    P = bytes(range(9))
+    seg = helpers._tcp(P, opts=b"\x00\x99\x99\x99\x11\x22\x33\x44")
+    fr = helpers._eth(helpers._ipv4(seg, 6))
+    r = _rec(oracle, fr)
+    raw = oracle.ipv4_checksum(seg, 8, bytes([10, 1, 2, 3]), bytes([10, 4, 5, 6]), 6)
+    assert int(r["l4_csum_calc"]) != raw  # re-serialised: doff 6, zeroed tail
+
+
+def test_q17_ipv4_checksum_panic_flagged(oracle):
+    fr = helpers._eth(helpers._ipv4(b"", 17, ihl=15, opts=b"\x00" + bytes(39)))
+    r = _rec(oracle, fr)
+    assert int(r["flags"]) & abi.C_IP_PANIC and not int(r["flags"]) & abi.C_IP_CHECKED
+
+
+def test_q18_udp_zero_checksum_literal(oracle):
+    # a stored 0 is compared literally; no "0 means no checksum" rule
+    P = bytes(range(12))
+    fr = bytearray(helpers._eth(helpers._ipv4(helpers._udp(P), 17)))
+    fr[40:42] = b"\x00\x00"
+    r = _rec(oracle, bytes(fr))
+    assert int(r["l4_csum"]) == 0 and not (int(r["flags"]) & abi.C_L4_OK)
+
+
+def test_generator_udp64_properties(oracle):
+    recs = np.array([oracle.parse_frame(oracle.gen_frame(abi.WL_UDP64, i)) for i in range(4096)],
+                    dtype=abi.RECORD_DTYPE)
+    f = recs["flags"]
+    assert ((f & abi.L_UDP) != 0).all() and (recs["payload_len"] == 22).all()
+    bad = ((f & abi.C_IP_OK) == 0) | ((f & abi.C_L4_OK) == 0)
+    assert 0.04 < bad.mean() < 0.09  # 1/16 corrupted
+    assert not (((f & abi.C_IP_OK) == 0) & ((f & abi.C_L4_OK) == 0)).any()
+
+
+def test_generator_imix_properties(oracle):
+    n = 6000
+    lens = np.array([oracle.gen_length(abi.WL_IMIX, i) for i in range(n)])
+    share = [(lens == L).mean() for L in (64, 576, 1500)]
+    assert abs(share[0] - 7 / 12) < 0.03 and abs(share[1] - 4 / 12) < 0.03
+    recs = np.array([oracle.parse_frame(oracle.gen_frame(abi.WL_IMIX, i)) for i in range(800)],
+                    dtype=abi.RECORD_DTYPE)
+    f = recs["flags"]
+    assert (f & abi.C_L4_CHECKED).all()
+    assert ((f & abi.L_IPV6) != 0).mean() > 0.3 and ((f & abi.L_TCP) != 0).mean() > 0.2
