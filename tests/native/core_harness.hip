@@ -5,12 +5,12 @@
 // against the oracle run without a GPU. Not part of the product library.
 #include <string.h>
 
-#include "../../nex_amd/csrc/frame_core.hpp"
+#include "../../nex_amd/csrc/parse_kernels.hpp"
 
 extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uint64_t* offsets,
                              const uint32_t* lengths, uint32_t stride, uint64_t count,
                              uint32_t flags, uint32_t ip_offset, uint32_t window,
-                             nexg_record* out) {
+                             int use_fast, nexg_record* out) {
     alignas(16) uint8_t slot[65536 + 32];
     for (uint64_t i = 0; i < count; i++) {
         const uint64_t off = offsets ? offsets[i] : i * (uint64_t)stride;
@@ -24,9 +24,40 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
             const uint32_t wlen = len < window ? (uint32_t)len : window;
             memset(slot, 0xA5, sizeof(slot));  // poison: bytes outside the window must not matter
             memcpy(slot + o, g, wlen);
-            nexg::WinFrame f{slot, g, o, wlen};
-            nexg::parse_frame(f, (uint32_t)(reinterpret_cast<uint64_t>(g) & 1u), (uint32_t)len, flags,
-                              ip_offset, r);
+            uint32_t w[16];
+            if (use_fast && len == 64) memcpy(w, g, 64);
+            if (use_fast && len == 64 && nexg::fast_udp4_64(w, flags, r)) {
+                out[i] = r;
+                continue;
+            }
+            const uint32_t par = (uint32_t)(reinterpret_cast<uint64_t>(g) & 1u);
+            if (use_fast == 4 && (par == 0)) {  // canonical fast path (k_parse_lane80) or generic
+                uint32_t w80[20] = {0};
+                memcpy(w80, g, len < 80 ? len : 80);
+                const uint64_t base = reinterpret_cast<uint64_t>(g);
+                const uint64_t tail = len > 80 ? nexg::global_le_sum(base + 80, base + len) : 0;
+                if (!nexg::fast_canonical80(w80, (uint32_t)len, flags, tail, r)) {
+                    nexg::WinFrame f{slot, g, o, wlen};
+                    nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
+                }
+            } else if (use_fast == 3) {  // StreamFrame: window = PITCH - o bytes, whole-frame sum given
+                const uint32_t pitch = window + 16;
+                const uint32_t wl = len < pitch - o ? (uint32_t)len : pitch - o;
+                memcpy(slot + o, g, wl);
+                const uint64_t base = reinterpret_cast<uint64_t>(g);
+                nexg::StreamFrame f{slot, g, o, wl, (uint32_t)len, nexg::global_le_sum(base, base + len)};
+                nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
+            } else if (use_fast == 2) {  // TileFrame: deferred tail summed separately (k_parse_coop)
+                nexg::TileFrame f{slot, g, o, wlen};
+                nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
+                if (f.dstate == 3) {
+                    const uint64_t base = reinterpret_cast<uint64_t>(g);
+                    f.complete(nexg::global_le_sum(base + f.ta, base + f.tb), r);
+                }
+            } else {
+                nexg::WinFrame f{slot, g, o, wlen};
+                nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
+            }
         }
         out[i] = r;
     }

@@ -19,12 +19,13 @@ def lib():
         L = ctypes.CDLL(LIB)
         P, U32, U64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
         L.harness_parse.restype = ctypes.c_int
-        L.harness_parse.argtypes = [P, U64, P, P, U32, U64, U32, U32, U32, P]
+        L.harness_parse.argtypes = [P, U64, P, P, U32, U64, U32, U32, U32, ctypes.c_int, P]
         _lib = L
     return _lib
 
 
-def parse_packed(data, offsets=None, lengths=None, stride=0, flags=0, ip_offset=0, window=128):
+def parse_packed(data, offsets=None, lengths=None, stride=0, flags=0, ip_offset=0, window=128,
+                 use_fast=False):
     data = np.ascontiguousarray(data, dtype=np.uint8)
     count = (len(lengths) if lengths is not None else
              (len(offsets) - 1 if offsets is not None else len(data) // stride))
@@ -34,5 +35,5 @@ def parse_packed(data, offsets=None, lengths=None, stride=0, flags=0, ip_offset=
     lib().harness_parse(data.ctypes.data, data.nbytes,
                         None if offs is None else offs.ctypes.data,
                         None if lens is None else lens.ctypes.data, stride, count, flags,
-                        ip_offset, window, recs.ctypes.data)
+                        ip_offset, window, int(use_fast), recs.ctypes.data)
     return recs

@@ -40,9 +40,11 @@ def test_core_matches_oracle(oracle, corpus, flags, layout):
     ipo = 14 if flags & abi.PARSE_FROM_IP else 0
     want = oracle.parse_packed(buf, offs, lens, flags=flags, ip_offset=ipo)
     for window in (128, 64, 0):
-        got = harness.parse_packed(buf, offs, lens, flags=flags, ip_offset=ipo, window=window)
-        helpers.records_equal(got, want, [buf[p:p + l] for p, l in zip(offs, lens)],
-                              f"flags={flags} layout={layout} window={window}")
+        for mode in (0, 2, 3, 4):  # WinFrame / TileFrame / StreamFrame / canonical fast path
+            got = harness.parse_packed(buf, offs, lens, flags=flags, ip_offset=ipo, window=window,
+                                       use_fast=mode)
+            helpers.records_equal(got, want, [buf[p:p + l] for p, l in zip(offs, lens)],
+                                  f"flags={flags} layout={layout} window={window} mode={mode}")
 
 
 def test_core_bad_extent(oracle):
@@ -66,6 +68,47 @@ def test_core_max_size_frames(oracle):
     frames = [f[:65535] for f in frames]
     buf, offs, lens = pack(frames, 1, 1)
     want = oracle.parse_packed(buf, offs, lens)
-    got = harness.parse_packed(buf, offs, lens)
-    helpers.records_equal(got, want, None, "max-size")
+    for mode in (0, 2, 3, 4):
+        got = harness.parse_packed(buf, offs, lens, use_fast=mode)
+        helpers.records_equal(got, want, None, f"max-size mode={mode}")
     assert (want["flags"] & abi.C_L4_CHECKED).all()
+
+
+def test_fast_path_udp64_matches_oracle(oracle):
+    """fast_udp4_64 (register path of the TileStride64 kernel) vs the oracle on
+    64-B frames: generated ones (fast path taken) and single-field mutations of
+    them (fast path taken or declined; the result must not depend on which)."""
+    rng = np.random.default_rng(64)
+    base = [oracle.gen_frame(abi.WL_UDP64, i) for i in range(2000)]
+    frames = list(base)
+    for f in base[:1500]:
+        fr = bytearray(f)
+        j = int(rng.choice([12, 13, 14, 16, 17, 23, 38, 39, int(rng.integers(64))]))
+        fr[j] = int(rng.choice([0, 0x45, 17, 30, 50, int(rng.integers(256))]))
+        frames.append(bytes(fr))
+    buf = np.frombuffer(b"".join(frames), np.uint8).copy()
+    for flags in (0, abi.PARSE_STRICT, abi.PARSE_FROM_IP):
+        ipo = 14 if flags & abi.PARSE_FROM_IP else 0
+        want = oracle.parse_packed(buf, stride=64, flags=flags, ip_offset=ipo)
+        got = harness.parse_packed(buf, stride=64, flags=flags, ip_offset=ipo, use_fast=True)
+        helpers.records_equal(got, want, frames, f"fast path flags={flags}")
+
+
+def test_canonical_fast_path_on_imix(oracle):
+    """fast_canonical80 on generated IMIX frames (all six shapes, every length
+    class) and single-byte mutations of them."""
+    rng = np.random.default_rng(80)
+    base = [oracle.gen_frame(abi.WL_IMIX, i) for i in range(3000)]
+    frames = list(base)
+    for f in base[:2500]:
+        fr = bytearray(f)
+        j = int(rng.choice([12, 13, 14, 16, 17, 18, 19, 20, 23, 38, 39, 46, 58, 59, 66, 67,
+                            int(rng.integers(len(f)))]))
+        fr[min(j, len(fr) - 1)] = int(rng.choice([0, 0x45, 0x60, 6, 17, 58, 1, 0x50, int(rng.integers(256))]))
+        frames.append(bytes(fr))
+        frames.append(f[: int(rng.integers(30, len(f) + 1))])
+    buf, offs, lens = pack(frames, 4)
+    for flags in (0, abi.PARSE_STRICT):
+        want = oracle.parse_packed(buf, offs, lens, flags=flags)
+        got = harness.parse_packed(buf, offs, lens, flags=flags, use_fast=4)
+        helpers.records_equal(got, want, frames, f"canonical flags={flags}")

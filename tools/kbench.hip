@@ -1,0 +1,222 @@
+// kbench.hip — kernel microbenchmarks for the parse hot path (one process,
+// interleaved variants, hipEvent timing). Frames come from the product
+// generator (libnexg.so C ABI); every parse variant's output is compared
+// byte-for-byte with the product kernel's.
+//   build: make -C tools kbench      run: tools/kbench [frames]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../nex_amd/csrc/parse_kernels.hpp"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1); } } while (0)
+
+using namespace nexg;
+
+// 64 B in, 8 B out per frame, coalesced: the traffic ceiling of the layout
+template <bool NT>
+__global__ __launch_bounds__(256) void k_readpeak(const uint8_t* data, uint64_t count, uint2* out) {
+    const uint64_t first = (uint64_t)blockIdx.x * 256;
+    const uint4* T = reinterpret_cast<const uint4*>(data + first * 64);
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint4 v = load16<NT>(T + threadIdx.x + 256 * k);
+        x ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    out[first + threadIdx.x] = make_uint2(x, 0);
+}
+
+// float4 copy: read N, write N (reference point from the microarch guide)
+__global__ __launch_bounds__(256) void k_copy(const uint4* in, uint4* out, uint64_t n16) {
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (; i < n16; i += stride) out[i] = in[i];
+}
+
+// LDS staging exactly as the product kernel, then a trivial per-lane reduce
+__global__ __launch_bounds__(256) void k_stageonly(const uint8_t* data, uint64_t count, uint2* out) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[256 * 80];
+    const uint64_t first = (uint64_t)blockIdx.x * 256;
+    const uint8_t* T = data + first * 64;
+    for (uint32_t c = threadIdx.x; c < 1024; c += 256) {
+        const uint4 v = reinterpret_cast<const uint4*>(T)[c];
+        *reinterpret_cast<uint4*>(smem + (c >> 2) * 80 + (c & 3) * 16) = v;
+    }
+    __syncthreads();
+    uint32_t x = 0;
+    for (int k = 0; k < 4; k++) {
+        uint4 v = *reinterpret_cast<const uint4*>(smem + threadIdx.x * 80 + 16 * k);
+        x ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    out[first + threadIdx.x] = make_uint2(x, 0);
+}
+
+// one lane per frame, 4 strided 16-B loads straight from HBM (no LDS)
+__global__ __launch_bounds__(256) void k_lanedirect(const uint8_t* data, uint64_t count, uint2* out,
+                                                    uint32_t flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint4* p = reinterpret_cast<const uint4*>(data + i * 64);
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint4 v = p[k];
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+    nexg_record r;
+    if (!fast_udp4_64(w, flags, r)) r.flags = 0xdead;
+    out[i] = make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
+}
+
+
+struct Var {
+    std::string name;
+    std::function<void()> run;
+    double bytes;  // algorithmic bytes per launch
+    std::vector<float> ms;
+};
+
+int main(int argc, char** argv) {
+    const uint64_t count = argc > 1 ? strtoull(argv[1], nullptr, 0) : (16ull << 20);
+    const int reps = 20, rounds = 7;
+    nexg_ctx* ctx;
+    if (nexg_ctx_create(0, &ctx) != 0) { printf("ctx failed\n"); return 1; }
+    uint8_t* data;
+    uint2 *out, *ref;
+    uint4* cpy;
+    CK(hipMalloc(&data, count * 64));
+    CK(hipMalloc(&out, count * 8));
+    CK(hipMalloc(&ref, count * 8));
+    CK(hipMalloc(&cpy, count * 64));
+    if (nexg_gen_frames(ctx, 1, 0x6E6578, 0, count, data, nullptr, 64, nullptr) != 0) return 1;
+    CK(hipDeviceSynchronize());
+    ParseArgs a{};
+    a.data = data; a.data_bytes = count * 64; a.stride = 64; a.count = count; a.out = out;
+    const dim3 grid((uint32_t)(count / 256)), blk(256);
+    std::vector<Var> vars;
+    auto parse = [&](auto kern) { return [=]() { hipLaunchKernelGGL(kern, grid, blk, 0, 0, a); }; };
+    vars.push_back({"prod_fast", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, true, false>), count * 64.0});
+    vars.push_back({"prod_fast_nt", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, true, true>), count * 64.0});
+    vars.push_back({"prod_generic", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, false, false>), count * 64.0});
+    vars.push_back({"udp64_stream_w64", parse(k_parse_stream<NEXG_OUT_DESC, 64>), count * 64.0});
+    vars.push_back({"lanewindow_generic", parse(k_parse<1, NEXG_OUT_DESC, 0, 128, false, false>), count * 64.0});
+    vars.push_back({"lane_direct_fast", [=]() { hipLaunchKernelGGL(k_lanedirect, grid, blk, 0, 0, data, count, out, 0u); }, count * 64.0});
+    vars.push_back({"stage_only", [=]() { hipLaunchKernelGGL(k_stageonly, grid, blk, 0, 0, data, count, out); }, count * 64.0});
+    vars.push_back({"readpeak", [=]() { hipLaunchKernelGGL(k_readpeak<false>, grid, blk, 0, 0, data, count, out); }, count * 64.0});
+    vars.push_back({"readpeak_nt", [=]() { hipLaunchKernelGGL(k_readpeak<true>, grid, blk, 0, 0, data, count, out); }, count * 64.0});
+    vars.push_back({"copy_float4", [=]() { hipLaunchKernelGGL(k_copy, dim3(256 * 32), blk, 0, 0, (const uint4*)data, cpy, count * 4); }, count * 128.0});
+
+    // correctness of parse variants vs the product kernel (full descriptors)
+    hipLaunchKernelGGL((k_parse<0, NEXG_OUT_DESC, 64, 64, false, false>), grid, blk, 0, 0, ParseArgs{data, count * 64, nullptr, nullptr, 64, count, 0, 0, ref});
+    CK(hipDeviceSynchronize());
+    std::vector<uint2> h_ref(count), h_out(count);
+    CK(hipMemcpy(h_ref.data(), ref, count * 8, hipMemcpyDeviceToHost));
+    for (auto& v : vars) {
+        if (v.name.rfind("prod", 0) != 0 && v.name.rfind("lane", 0) != 0) continue;
+        CK(hipMemset(out, 0, count * 8));
+        v.run();
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h_out.data(), out, count * 8, hipMemcpyDeviceToHost));
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < count; i++) bad += memcmp(&h_out[i], &h_ref[i], 8) != 0;
+        printf("check %-20s mismatches=%llu\n", v.name.c_str(), (unsigned long long)bad);
+    }
+    // ---- IMIX (offset table) ----
+    const uint64_t icount = count;
+    uint32_t* ilen;
+    uint64_t* ioff;
+    CK(hipMalloc(&ilen, icount * 4));
+    CK(hipMalloc(&ioff, (icount + 1) * 8));
+    if (nexg_gen_lengths(ctx, 2, 0x6E6578, 0, icount, ilen, nullptr) != 0) return 1;
+    std::vector<uint32_t> hl(icount);
+    std::vector<uint64_t> ho(icount + 1, 0);
+    CK(hipMemcpy(hl.data(), ilen, icount * 4, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < icount; i++) ho[i + 1] = ho[i] + hl[i];
+    CK(hipMemcpy(ioff, ho.data(), (icount + 1) * 8, hipMemcpyHostToDevice));
+    uint8_t* idata;
+    CK(hipMalloc(&idata, ho[icount] + 64));
+    if (nexg_gen_frames(ctx, 2, 0x6E6578, 0, icount, idata, ioff, 0, nullptr) != 0) return 1;
+    CK(hipDeviceSynchronize());
+    ParseArgs ia{};
+    ia.data = idata; ia.data_bytes = ho[icount]; ia.offsets = ioff; ia.count = icount; ia.out = out;
+    const double ibytes = (double)ho[icount];
+    auto iparse = [&](auto kern) { return [=]() { hipLaunchKernelGGL(kern, grid, blk, 0, 0, ia); }; };
+    std::vector<Var> ivars;
+    ivars.push_back({"imix_coop_w128", iparse(k_parse_coop<NEXG_OUT_DESC, 128>), ibytes});
+    ivars.push_back({"imix_coop_w96", iparse(k_parse_coop<NEXG_OUT_DESC, 96>), ibytes});
+    ivars.push_back({"imix_coop_w64", iparse(k_parse_coop<NEXG_OUT_DESC, 64>), ibytes});
+    ivars.push_back({"imix_coop_w64_u4", iparse(k_parse_coop<NEXG_OUT_DESC, 64, 0, 4>), ibytes});
+    ivars.push_back({"imix_2pass_u8", [=]() {
+        hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 8>), grid, blk, 0, 0, ia);
+        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
+    ivars.push_back({"imix_2pass_u4", [=]() {
+        hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia);
+        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
+    ivars.push_back({"imix_2pass_u16", [=]() {
+        hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 16>), grid, blk, 0, 0, ia);
+        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
+    ivars.push_back({"ABL_tails_only_u8", [=]() { hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 8>), grid, blk, 0, 0, ia); }, ibytes});
+    ivars.push_back({"ABL_lane80_only", [=]() { hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
+    ivars.push_back({"udp64_lane80_2pass", [=]() {
+        hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 8>), grid, blk, 0, 0, a);
+        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, a); }, count * 64.0});
+    ivars.push_back({"imix_wave_w64", iparse(k_parse_wave<NEXG_OUT_DESC, 64>), ibytes});
+    ivars.push_back({"imix_wave_w64_u8", iparse(k_parse_wave<NEXG_OUT_DESC, 64, 8>), ibytes});
+    ivars.push_back({"imix_wave_w80", iparse(k_parse_wave<NEXG_OUT_DESC, 80>), ibytes});
+    ivars.push_back({"imix_wave_w96", iparse(k_parse_wave<NEXG_OUT_DESC, 96>), ibytes});
+    ivars.push_back({"imix_coop_w80", iparse(k_parse_coop<NEXG_OUT_DESC, 80>), ibytes});
+    ivars.push_back({"imix_stream_w64", iparse(k_parse_stream<NEXG_OUT_DESC, 64>), ibytes});
+    ivars.push_back({"imix_streamsrch_w64", iparse(k_parse_stream<NEXG_OUT_DESC, 64, false>), ibytes});
+    ivars.push_back({"imix_stream_w96", iparse(k_parse_stream<NEXG_OUT_DESC, 96>), ibytes});
+    ivars.push_back({"imix_stream_w128", iparse(k_parse_stream<NEXG_OUT_DESC, 128>), ibytes});
+    ivars.push_back({"imix_lanewindow", iparse(k_parse<1, NEXG_OUT_DESC, 0, 128>), ibytes});
+    hipLaunchKernelGGL((k_parse<1, NEXG_OUT_DESC, 0, 128>), grid, blk, 0, 0, ParseArgs{idata, ho[icount], ioff, nullptr, 0, icount, 0, 0, ref});
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(h_ref.data(), ref, count * 8, hipMemcpyDeviceToHost));
+    for (auto& v : ivars) {
+        if (v.name.rfind("ABL", 0) == 0 || v.name.rfind("udp64", 0) == 0) continue;
+        CK(hipMemset(out, 0, count * 8));
+        v.run();
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h_out.data(), out, count * 8, hipMemcpyDeviceToHost));
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < count; i++) bad += memcmp(&h_out[i], &h_ref[i], 8) != 0;
+        printf("check %-20s mismatches=%llu\n", v.name.c_str(), (unsigned long long)bad);
+    }
+    ivars.push_back({"ABL_coop64_noparse", iparse(k_parse_coop<NEXG_OUT_DESC, 64, 1>), ibytes});
+    ivars.push_back({"ABL_coop64_nopieces", iparse(k_parse_coop<NEXG_OUT_DESC, 64, 2>), ibytes});
+    ivars.push_back({"ABL_imix_stream_noparse", iparse(k_parse_stream<NEXG_OUT_DESC, 64, true, 1>), ibytes});
+    ivars.push_back({"ABL_imix_srch_noparse", iparse(k_parse_stream<NEXG_OUT_DESC, 64, false, 1>), ibytes});
+    ivars.push_back({"ABL_udp64_srch_noparse", parse(k_parse_stream<NEXG_OUT_DESC, 64, false, 1>), count * 64.0});
+    for (auto& v : ivars) vars.push_back(v);
+    printf("imix bytes %.3f GB, mean frame %.1f B\n", ibytes / 1e9, ibytes / icount);
+
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int r = 0; r < rounds; r++) {
+        for (auto& v : vars) {
+            v.run();
+            CK(hipEventRecord(e0, 0));
+            for (int i = 0; i < reps; i++) v.run();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            v.ms.push_back(ms / reps);
+        }
+    }
+    printf("%-22s %10s %10s %10s %8s\n", "variant", "med_us", "min_us", "GB/s(med)", "frac8T");
+    for (auto& v : vars) {
+        std::sort(v.ms.begin(), v.ms.end());
+        double med = v.ms[v.ms.size() / 2];
+        double gbs = v.bytes / (med * 1e-3) / 1e9;
+        printf("%-22s %10.1f %10.1f %10.1f %8.3f\n", v.name.c_str(), med * 1e3, v.ms[0] * 1e3, gbs, gbs / 8000.0);
+    }
+    return 0;
+}
