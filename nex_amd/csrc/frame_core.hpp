@@ -112,6 +112,16 @@ NEXG_HD uint32_t range_mask(uint64_t j, uint64_t A, uint64_t B) {
 NEXG_HD uint32_t halves(uint32_t w) { return (w & 0xFFFFu) + (w >> 16); }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// 16-B global load from a 4-B aligned address (global_load_dwordx4 needs
+// dword alignment only); NT = non-temporal
+template <bool NT = false>
+NEXG_HD uint4 load16a4(const void* p) {
+    u32x4a4 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(p))
+                   : *reinterpret_cast<const u32x4a4*>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 // 16-B global load; NT = non-temporal (streamed once, do not keep in cache)
 template <bool NT = false>
@@ -569,7 +579,7 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w)[20], uint32_t len, uint32_t op
     t4 += (icmp && !v6) ? 0u : (proto + n);  // pseudo proto + length (BE constants)
     if (udp) t4 += n;                       // UDP length word as serialised
     const uint32_t l4_calc = fold_complement(t4);
-    const uint32_t l4_cs = L(tcp ? 16u : (udp ? 6u : 2u));
+    const uint32_t l4_cs = tcp ? L(16) : (udp ? L(6) : L(2));
     r = nexg_record{};
     uint32_t fl = NEXG_L_ETHERNET | NEXG_L_IP | (v6 ? NEXG_L_IPV6 : NEXG_L_IPV4) | NEXG_C_L4_CHECKED |
                   (l4_calc == l4_cs ? NEXG_C_L4_OK : 0u);

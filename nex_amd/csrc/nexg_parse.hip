@@ -21,7 +21,7 @@ ParseVariant choose_parse_variant(const ParseArgs& a) {
         a.count * (uint64_t)a.stride <= a.data_bytes) {
         return a.stride == 64u ? ParseVariant::TileStride64 : ParseVariant::TileStride;
     }
-    return ParseVariant::LaneWindowCoop;
+    return ParseVariant::TwoPass;
 }
 
 template <int OUT>
@@ -39,7 +39,11 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             hipLaunchKernelGGL((k_parse<1, OUT, 0, 128>), grid, block, 0, s, a);
             break;
         case ParseVariant::LaneWindowCoop:
-            hipLaunchKernelGGL((k_parse_coop<OUT, 128>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((k_parse_coop<OUT, 64, 0, 4>), grid, block, 0, s, a);
+            break;
+        case ParseVariant::TwoPass:
+            hipLaunchKernelGGL((k_tail_sums<OUT, 4>), grid, block, 0, s, a);
+            hipLaunchKernelGGL(k_parse_lane80<OUT>, grid, block, 0, s, a);
             break;
     }
     return hipGetLastError();

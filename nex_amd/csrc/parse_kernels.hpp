@@ -760,29 +760,44 @@ template <int OUT, uint32_t PU = 8>
 __global__ __launch_bounds__(256) void k_tail_sums(ParseArgs a) {
     __shared__ uint32_t s_pfx[4][65];
     __shared__ uint32_t s_acc[4][64];
-    __shared__ uint64_t s_ta[4][64];
-    __shared__ uint32_t s_tl[4][64];
+    __shared__ uint32_t s_ta[4][64];  // tail start relative to the wave base
+    __shared__ uint32_t s_tb[4][64];  // tail end   relative to the wave base
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     uint32_t* pfx = s_pfx[wv];
     uint32_t* acc = s_acc[wv];
-    uint64_t* tail_a = s_ta[wv];
-    uint32_t* tail_len = s_tl[wv];
+    uint32_t* tail_a = s_ta[wv];
+    uint32_t* tail_b = s_tb[wv];
     const uint64_t wfirst = (uint64_t)blockIdx.x * kTile + 64u * wv;
     if (wfirst >= a.count) return;
     const uint64_t left = a.count - wfirst;
     const uint32_t nf = left < 64u ? (uint32_t)left : 64u;
     const uint64_t idx = wfirst + lane;
     uint32_t np = 0;
-    if (lane < nf) {
-        uint64_t off;
-        uint32_t len;
-        if (frame_extent(a, idx, off, len) && len > kLaneWin) {
-            const uint64_t A = reinterpret_cast<uint64_t>(a.data) + off + kLaneWin;
-            const uint64_t B = reinterpret_cast<uint64_t>(a.data) + off + len;
-            np = (uint32_t)(((B - 1) / kPiece) - (A / kPiece) + 1);
-            tail_a[lane] = A;
-            tail_len[lane] = len - kLaneWin;
+    uint64_t off = 0;
+    uint32_t len = 0;
+    const bool have = lane < nf && frame_extent(a, idx, off, len) && len > kLaneWin;
+    // wave base: lowest 256-B aligned tail start of the wave (wave-uniform)
+    uint64_t myA = have ? reinterpret_cast<uint64_t>(a.data) + off + kLaneWin : ~0ull;
+    uint64_t wbase = myA;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t o2 = __shfl_xor(wbase, d, 64);
+        wbase = o2 < wbase ? o2 : wbase;
+    }
+    wbase &= ~(uint64_t)(kPiece - 1);
+    bool fits = true;
+    if (have) {
+        const uint64_t ra = myA - wbase, rb = ra + (len - kLaneWin);
+        fits = rb < (1ull << 31);
+        if (fits) {
+            np = (uint32_t)(((rb - 1) / kPiece) - (ra / kPiece) + 1);
+            tail_a[lane] = (uint32_t)ra;
+            tail_b[lane] = (uint32_t)rb;
         }
+    }
+    if (!__all(fits)) {  // wave spans >2 GiB (unordered offsets): each lane sums its own tail
+        if (have) *handoff_slot<OUT>(a.out, idx) = (uint32_t)global_le_sum(myA, myA + len - kLaneWin);
+        return;
     }
     acc[lane] = 0;
     const uint32_t incl = wave_incl_scan(np);
@@ -793,6 +808,7 @@ __global__ __launch_bounds__(256) void k_tail_sums(ParseArgs a) {
     const uint32_t grp = lane >> 4, gl = lane & 15u;
     const uint32_t pb = (uint32_t)((uint64_t)total * grp / 4u);
     const uint32_t pe = (uint32_t)((uint64_t)total * (grp + 1u) / 4u);
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(wbase);
     if (pb < pe) {
         uint32_t lo = 0, hi = 64;
         while (hi - lo > 1) {
@@ -801,13 +817,12 @@ __global__ __launch_bounds__(256) void k_tail_sums(ParseArgs a) {
         }
         uint32_t fi = lo;
         uint32_t cf = lo, ce = pfx[lo + 1];
-        uint64_t ca = tail_a[lo], cb = ca + tail_len[lo];
-        uint64_t cpb = (ca & ~(uint64_t)(kPiece - 1)) - (uint64_t)pfx[lo] * kPiece;
+        uint32_t ca = tail_a[lo], cb = tail_b[lo];
+        uint32_t cpb = (ca & ~(kPiece - 1)) - pfx[lo] * kPiece;  // mod 2^32
         uint32_t run = 0;
         for (uint32_t p0 = pb; p0 < pe; p0 += PU) {
             uint4 v[PU];
-            uint64_t C[PU], AA[PU], BB[PU];
-            uint32_t F[PU];
+            uint32_t C[PU], AA[PU], BB[PU], F[PU];
 #pragma unroll
             for (uint32_t u = 0; u < PU; u++) {
                 const uint32_t pp = p0 + u;
@@ -815,19 +830,18 @@ __global__ __launch_bounds__(256) void k_tail_sums(ParseArgs a) {
                     cf++;
                     ce = pfx[cf + 1];
                     ca = tail_a[cf];
-                    cb = ca + tail_len[cf];
-                    cpb = (ca & ~(uint64_t)(kPiece - 1)) - (uint64_t)pfx[cf] * kPiece;
+                    cb = tail_b[cf];
+                    cpb = (ca & ~(kPiece - 1)) - pfx[cf] * kPiece;
                 }
                 F[u] = cf;
                 AA[u] = ca;
                 BB[u] = cb;
-                C[u] = cpb + (uint64_t)pp * kPiece + 16u * gl;
+                C[u] = cpb + pp * kPiece + 16u * gl;
             }
 #pragma unroll
             for (uint32_t u = 0; u < PU; u++) {
                 v[u] = make_uint4(0, 0, 0, 0);
-                if (p0 + u < pe && C[u] < BB[u] && C[u] + 16u > AA[u])
-                    v[u] = load16<true>(reinterpret_cast<const void*>(C[u]));
+                if (p0 + u < pe && C[u] < BB[u] && C[u] + 16u > AA[u]) v[u] = load16<true>(wb + C[u]);
             }
 #pragma unroll
             for (uint32_t u = 0; u < PU; u++) {
@@ -842,7 +856,7 @@ __global__ __launch_bounds__(256) void k_tail_sums(ParseArgs a) {
                     run = 0;
                     fi = F[u];
                 }
-                const uint64_t c = C[u], A = AA[u], B = BB[u];
+                const uint32_t c = C[u], A = AA[u], B = BB[u];
                 if (c < B && c + 16u > A) {
                     if (c >= A && c + 16u <= B) {
                         run += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) + halves(v[u].w);
@@ -863,7 +877,249 @@ __global__ __launch_bounds__(256) void k_tail_sums(ParseArgs a) {
         if (gl == 0 && s) atomicAdd(&acc[fi], s);
     }
     wave_lds_sync();
-    if (lane < nf && np) *handoff_slot<OUT>(a.out, idx) = acc[lane];
+    if (have) *handoff_slot<OUT>(a.out, idx) = acc[lane];
+}
+
+// MODE 5 (offset-table batches, the IMIX path): one wave = 64 frames, no
+// workgroup barrier. Each lane issues its frame's first 80 bytes into
+// registers, then the wave streams all its frames' bytes past 80 in 256-B
+// quarter-wave pieces (k_tail_sums' scheme) while those head loads are in
+// flight; finally each lane finishes its frame: fast_canonical80 for the six
+// canonical IMIX shapes, generic parse_frame from HBM for anything else.
+template <int OUT, uint32_t PU = 4>
+__global__ __launch_bounds__(256) void k_parse_imix(ParseArgs a) {
+    __shared__ uint32_t s_pfx[4][65];
+    __shared__ uint32_t s_acc[4][64];
+    __shared__ uint32_t s_ta[4][64];  // tail start relative to the wave base
+    __shared__ uint32_t s_tb[4][64];  // tail end   relative to the wave base
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    uint32_t* pfx = s_pfx[wv];
+    uint32_t* acc = s_acc[wv];
+    uint32_t* tail_a = s_ta[wv];
+    uint32_t* tail_b = s_tb[wv];
+    const uint64_t wfirst = (uint64_t)blockIdx.x * kTile + 64u * wv;
+    if (wfirst >= a.count) return;
+    const uint64_t left = a.count - wfirst;
+    const uint32_t nf = left < 64u ? (uint32_t)left : 64u;
+    const uint64_t idx = wfirst + lane;
+    uint32_t np = 0;
+    uint64_t off = 0;
+    uint32_t len = 0;
+    const bool valid = lane < nf && frame_extent(a, idx, off, len);
+    const bool have = valid && len > kLaneWin;
+    // head: the first 80 bytes straight into registers, issued before the
+    // tail stream so both are in flight together
+    const uint64_t abs = reinterpret_cast<uint64_t>(a.data) + off;
+    const bool head_ok = valid && (abs & 3u) == 0 &&
+                         abs + kLaneWin <= reinterpret_cast<uint64_t>(a.data) + a.data_bytes;
+    uint32_t w[20];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const uint4 v = head_ok ? load16a4<true>(reinterpret_cast<const void*>(abs + 16u * k))
+                                : make_uint4(0, 0, 0, 0);
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+    // wave base: lowest 256-B aligned tail start of the wave (wave-uniform)
+    uint64_t myA = have ? reinterpret_cast<uint64_t>(a.data) + off + kLaneWin : ~0ull;
+    uint64_t wbase = myA;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t o2 = __shfl_xor(wbase, d, 64);
+        wbase = o2 < wbase ? o2 : wbase;
+    }
+    wbase &= ~(uint64_t)(kPiece - 1);
+    bool fits = true;
+    if (have) {
+        const uint64_t ra = myA - wbase, rb = ra + (len - kLaneWin);
+        fits = rb < (1ull << 31);
+        if (fits) {
+            np = (uint32_t)(((rb - 1) / kPiece) - (ra / kPiece) + 1);
+            tail_a[lane] = (uint32_t)ra;
+            tail_b[lane] = (uint32_t)rb;
+        }
+    }
+    const bool wave_ok = __all(fits);  // else (>2 GiB span): each lane sums its own tail
+    acc[lane] = 0;
+    if (!wave_ok) np = 0;
+    const uint32_t incl = wave_incl_scan(np);
+    pfx[lane] = incl - np;
+    const uint32_t total = __shfl(incl, 63, 64);
+    if (lane == 63) pfx[64] = total;
+    wave_lds_sync();
+    const uint32_t grp = lane >> 4, gl = lane & 15u;
+    const uint32_t pb = (uint32_t)((uint64_t)total * grp / 4u);
+    const uint32_t pe = (uint32_t)((uint64_t)total * (grp + 1u) / 4u);
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(wbase);
+    if (pb < pe) {
+        uint32_t lo = 0, hi = 64;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pfx[mid] <= pb) lo = mid; else hi = mid;
+        }
+        uint32_t fi = lo;
+        uint32_t cf = lo, ce = pfx[lo + 1];
+        uint32_t ca = tail_a[lo], cb = tail_b[lo];
+        uint32_t cpb = (ca & ~(kPiece - 1)) - pfx[lo] * kPiece;  // mod 2^32
+        uint32_t run = 0;
+        for (uint32_t p0 = pb; p0 < pe; p0 += PU) {
+            uint4 v[PU];
+            uint32_t C[PU], AA[PU], BB[PU], F[PU];
+#pragma unroll
+            for (uint32_t u = 0; u < PU; u++) {
+                const uint32_t pp = p0 + u;
+                while (pp < pe && pp >= ce) {
+                    cf++;
+                    ce = pfx[cf + 1];
+                    ca = tail_a[cf];
+                    cb = tail_b[cf];
+                    cpb = (ca & ~(kPiece - 1)) - pfx[cf] * kPiece;
+                }
+                F[u] = cf;
+                AA[u] = ca;
+                BB[u] = cb;
+                C[u] = cpb + pp * kPiece + 16u * gl;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PU; u++) {
+                v[u] = make_uint4(0, 0, 0, 0);
+                if (p0 + u < pe && C[u] < BB[u] && C[u] + 16u > AA[u]) v[u] = load16<true>(wb + C[u]);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PU; u++) {
+                if (p0 + u >= pe) break;
+                if (F[u] != fi) {
+                    uint32_t s = run;
+                    s += __shfl_xor(s, 8, 16);
+                    s += __shfl_xor(s, 4, 16);
+                    s += __shfl_xor(s, 2, 16);
+                    s += __shfl_xor(s, 1, 16);
+                    if (gl == 0 && s) atomicAdd(&acc[fi], s);
+                    run = 0;
+                    fi = F[u];
+                }
+                const uint32_t c = C[u], A = AA[u], B = BB[u];
+                if (c < B && c + 16u > A) {
+                    if (c >= A && c + 16u <= B) {
+                        run += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) + halves(v[u].w);
+                    } else {
+                        if (c + 0 < B) run += halves(v[u].x & range_mask(c + 0, A, B));
+                        if (c + 4 < B) run += halves(v[u].y & range_mask(c + 4, A, B));
+                        if (c + 8 < B) run += halves(v[u].z & range_mask(c + 8, A, B));
+                        if (c + 12 < B) run += halves(v[u].w & range_mask(c + 12, A, B));
+                    }
+                }
+            }
+        }
+        uint32_t s = run;
+        s += __shfl_xor(s, 8, 16);
+        s += __shfl_xor(s, 4, 16);
+        s += __shfl_xor(s, 2, 16);
+        s += __shfl_xor(s, 1, 16);
+        if (gl == 0 && s) atomicAdd(&acc[fi], s);
+    }
+    wave_lds_sync();
+    if (lane >= nf) return;
+    nexg_record r{};
+    if (!valid) {
+        r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
+    } else {
+        bool done = false;
+        if (head_ok) {
+            const uint32_t tail = !have ? 0u
+                                : (wave_ok ? acc[lane] : (uint32_t)global_le_sum(myA, myA + len - kLaneWin));
+#pragma unroll
+            for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
+            done = fast_canonical80(w, len, a.opt_flags, tail, r);
+        }
+        if (!done) {
+            GlobalFrame gf{a.data + off};
+            parse_frame(gf, (uint32_t)(abs & 1u), len, a.opt_flags, a.ip_offset, r);
+        }
+    }
+    store_result<OUT>(a.out, idx, r);
+}
+
+__device__ __forceinline__ uint32_t wave_sum64(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Pass 1, alternative shape: the whole wave streams one frame tail at a time
+// (lane l takes 16-B chunks l, l+64 of the tail), TW tails in flight per
+// round; frames are picked from the wave's 64 by ballot. No LDS, no cursor.
+template <int OUT, uint32_t TW = 4>
+__global__ __launch_bounds__(256) void k_tail_sums_wave(ParseArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
+    uint64_t off = 0;
+    uint32_t len = 0;
+    const bool have = idx < a.count && frame_extent(a, idx, off, len) && len > kLaneWin;
+    const uint64_t myA = reinterpret_cast<uint64_t>(a.data) + off + kLaneWin;
+    const uint64_t myB = reinterpret_cast<uint64_t>(a.data) + off + len;
+    uint64_t mask = __ballot(have);
+    uint32_t mine = 0;
+    while (mask) {
+        uint32_t fl[TW];
+        uint64_t A[TW], B[TW];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < TW; j++) {
+            fl[j] = 64;
+            A[j] = B[j] = 0;
+            if (mask) {
+                const uint32_t f = (uint32_t)__builtin_ctzll(mask);
+                mask &= mask - 1;
+                fl[j] = f;
+                A[j] = __shfl(myA, f, 64);
+                B[j] = __shfl(myB, f, 64);
+                cnt++;
+            }
+        }
+        uint4 v[TW][2];
+        uint64_t C[TW][2];
+#pragma unroll
+        for (uint32_t j = 0; j < TW; j++)
+#pragma unroll
+            for (uint32_t rr = 0; rr < 2; rr++) {
+                C[j][rr] = (A[j] & ~15ull) + 16ull * (lane + 64u * rr);
+                v[j][rr] = (C[j][rr] < B[j]) ? load16<true>(reinterpret_cast<const void*>(C[j][rr]))
+                                             : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+        for (uint32_t j = 0; j < TW; j++) {
+            uint32_t s = 0;
+#pragma unroll
+            for (uint32_t rr = 0; rr < 2; rr++) {
+                const uint64_t c = C[j][rr];
+                if (c < B[j] && c + 16u > A[j]) {
+                    if (c >= A[j] && c + 16u <= B[j]) {
+                        s += halves(v[j][rr].x) + halves(v[j][rr].y) + halves(v[j][rr].z) + halves(v[j][rr].w);
+                    } else {
+                        if (c + 0 < B[j]) s += halves(v[j][rr].x & range_mask(c + 0, A[j], B[j]));
+                        if (c + 4 < B[j]) s += halves(v[j][rr].y & range_mask(c + 4, A[j], B[j]));
+                        if (c + 8 < B[j]) s += halves(v[j][rr].z & range_mask(c + 8, A[j], B[j]));
+                        if (c + 12 < B[j]) s += halves(v[j][rr].w & range_mask(c + 12, A[j], B[j]));
+                    }
+                }
+            }
+            // tails longer than 2 KB: rest of the frame, same lane pattern
+            for (uint64_t c = (A[j] & ~15ull) + 16ull * (lane + 128u); c < B[j]; c += 1024u) {
+                const uint4 w = load16<true>(reinterpret_cast<const void*>(c));
+                if (c + 16u <= B[j]) s += halves(w.x) + halves(w.y) + halves(w.z) + halves(w.w);
+                else {
+                    if (c + 0 < B[j]) s += halves(w.x & range_mask(c + 0, A[j], B[j]));
+                    if (c + 4 < B[j]) s += halves(w.y & range_mask(c + 4, A[j], B[j]));
+                    if (c + 8 < B[j]) s += halves(w.z & range_mask(c + 8, A[j], B[j]));
+                    if (c + 12 < B[j]) s += halves(w.w & range_mask(c + 12, A[j], B[j]));
+                }
+            }
+            s = wave_sum64(s);
+            if (lane == fl[j]) mine = s;
+        }
+        (void)cnt;
+    }
+    if (have) *handoff_slot<OUT>(a.out, idx) = mine;
 }
 
 // Pass 2: one lane per frame. The first 80 bytes are loaded straight into
@@ -885,23 +1141,16 @@ __global__ __launch_bounds__(256) void k_parse_lane80(ParseArgs a) {
     const uint64_t abs = reinterpret_cast<uint64_t>(a.data) + off;
     const uint64_t dend = reinterpret_cast<uint64_t>(a.data) + a.data_bytes;
     bool done = false;
-    if ((abs & 3u) == 0) {
+    if ((abs & 3u) == 0 && abs + kLaneWin <= dend) {
         const uint32_t tail = len > kLaneWin ? *handoff_slot<OUT>(a.out, idx) : 0u;
-        const uint64_t A0 = abs & ~15ull;
-        uint32_t c[24];
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-            uint4 v = A0 + 16u * k < dend ? load16<true>(reinterpret_cast<const void*>(A0 + 16u * k))
-                                          : make_uint4(0, 0, 0, 0);
-            c[4 * k] = v.x; c[4 * k + 1] = v.y; c[4 * k + 2] = v.z; c[4 * k + 3] = v.w;
-        }
-        const uint32_t s = (uint32_t)(abs & 15u) >> 2;
         uint32_t w[20];
 #pragma unroll
-        for (int k = 0; k < 20; k++) {
-            const uint32_t x = s == 0 ? c[k] : (s == 1 ? c[k + 1] : (s == 2 ? c[k + 2] : c[k + 3]));
-            w[k] = 4u * k < len ? (x & range_mask(4u * k, 0, len)) : 0u;
+        for (int k = 0; k < 5; k++) {
+            const uint4 v = load16a4<true>(reinterpret_cast<const void*>(abs + 16u * k));
+            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
         }
+#pragma unroll
+        for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
         done = fast_canonical80(w, len, a.opt_flags, tail, r);
     }
     if (!done) {

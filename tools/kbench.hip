@@ -160,6 +160,18 @@ int main(int argc, char** argv) {
     ivars.push_back({"imix_2pass_u16", [=]() {
         hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 16>), grid, blk, 0, 0, ia);
         hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
+    ivars.push_back({"imix_fused_u4", iparse(k_parse_imix<NEXG_OUT_DESC, 4>), ibytes});
+    ivars.push_back({"imix_fused_u2", iparse(k_parse_imix<NEXG_OUT_DESC, 2>), ibytes});
+    ivars.push_back({"imix_fused_u6", iparse(k_parse_imix<NEXG_OUT_DESC, 6>), ibytes});
+    ivars.push_back({"udp64_fused_u4", parse(k_parse_imix<NEXG_OUT_DESC, 4>), count * 64.0});
+    ivars.push_back({"imix_2pass_wave4", [=]() {
+        hipLaunchKernelGGL((k_tail_sums_wave<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia);
+        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
+    ivars.push_back({"imix_2pass_wave2", [=]() {
+        hipLaunchKernelGGL((k_tail_sums_wave<NEXG_OUT_DESC, 2>), grid, blk, 0, 0, ia);
+        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
+    ivars.push_back({"ABL_tailswave4_only", [=]() { hipLaunchKernelGGL((k_tail_sums_wave<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia); }, ibytes});
+    ivars.push_back({"ABL_tails_only_u4", [=]() { hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia); }, ibytes});
     ivars.push_back({"ABL_tails_only_u8", [=]() { hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 8>), grid, blk, 0, 0, ia); }, ibytes});
     ivars.push_back({"ABL_lane80_only", [=]() { hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
     ivars.push_back({"udp64_lane80_2pass", [=]() {
