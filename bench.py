@@ -68,7 +68,8 @@ def load_traffic(workload, out_kind):
     try:
         with open(path) as f:
             t = json.load(f)
-        return t.get(f"{workload}:{out_kind}")
+        e = t.get(f"{workload}:{out_kind}")
+        return None if e is None else e["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         return None
 
@@ -83,6 +84,10 @@ def main():
     ap.add_argument("--out", choices=["desc", "record"], default="desc")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="frames start and end in pinned host memory: chunked H2D -> parse -> "
+                         "D2H pipeline on two streams (PCIe-inclusive rate, DESIGN.md §6)")
+    ap.add_argument("--e2e-chunk", type=int, default=1 << 20, help="frames per pipelined chunk")
     args = ap.parse_args()
 
     import torch
@@ -134,6 +139,45 @@ def main():
                 "parallelism": f"{world} ranks x index-range shards, no collective",
                 "seed": hex(abi.DEFAULT_SEED)})
 
+    if args.e2e:
+        assert args.workload in ("udp64", "imix"), "--e2e covers the parse path"
+        # host-resident copy of the same frames (pinned), chunked pipeline:
+        # copy stream: H2D chunk i; compute stream: parse chunk i; D2H descs
+        host = torch.empty(batch.data.numel(), dtype=torch.uint8, pin_memory=True)
+        host.copy_(batch.data)
+        host_out = torch.empty(out.numel(), dtype=torch.uint8, pin_memory=True)
+        cs, ps = torch.cuda.Stream(device), torch.cuda.Stream(device)
+        C = args.e2e_chunk
+        width = 8 if out_kind == abi.OUT_DESC else 64
+        from nex_amd.engine import FrameBatch
+        offs_host = None if batch.offsets is None else batch.offsets.cpu()
+        chunks = []
+        for c0 in range(0, F, C):
+            c1 = min(F, c0 + C)
+            if batch.offsets is None:
+                b0, b1 = c0 * batch.stride, c1 * batch.stride
+                sub = FrameBatch(data=batch.data[b0:b1], count=c1 - c0, stride=batch.stride)
+            else:
+                b0, b1 = int(offs_host[c0]), int(offs_host[c1])
+                sub = FrameBatch(data=batch.data[b0:b1], count=c1 - c0,
+                                 offsets=batch.offsets[c0:c1 + 1] - b0)
+            chunks.append((c0, c1, b0, b1, sub))
+
+        def step():
+            ev_prev = None
+            for (c0, c1, b0, b1, sub) in chunks:
+                with torch.cuda.stream(cs):
+                    batch.data[b0:b1].copy_(host[b0:b1], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(cs)
+                ps.wait_event(ev)
+                eng.parse(sub, out_kind=out_kind, out=out[c0 * width:c1 * width], stream=ps)
+                with torch.cuda.stream(ps):
+                    host_out[c0 * width:c1 * width].copy_(out[c0 * width:c1 * width], non_blocking=True)
+            ps.synchronize()
+        cfg["workload"] += "; END-TO-END: frames in pinned host memory, chunked H2D/parse/D2H"
+        cfg["e2e_chunk_frames"] = C
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(device)
@@ -151,6 +195,8 @@ def main():
     dist.barrier(device)
     elapsed = dist.max_over_ranks(t1 - t0, device)
     kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # per launch, on the launch stream
+    if args.e2e:  # copies + kernels on two side streams: the host clock is the measure
+        kernel_s = (t1 - t0) / args.steps
     total_frames = dist.sum_over_ranks(F, device) * args.steps
     total_bytes = dist.sum_over_ranks(alg_bytes, device) * args.steps
 
