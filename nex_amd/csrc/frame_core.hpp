@@ -111,6 +111,15 @@ NEXG_HD uint32_t range_mask(uint64_t j, uint64_t A, uint64_t B) {
 
 NEXG_HD uint32_t halves(uint32_t w) { return (w & 0xFFFFu) + (w >> 16); }
 
+// acc + halves(w) in one instruction on the device (v_sad_u16 against 0)
+NEXG_HD uint32_t halves_acc(uint32_t w, uint32_t acc) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sad_u16(w, 0u, acc);
+#else
+    return acc + halves(w);
+#endif
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 

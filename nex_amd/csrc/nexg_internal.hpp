@@ -28,6 +28,7 @@ enum class ParseVariant {
     LaneWindow,     // any layout: per-lane 128-B window, lane sums its own tail
     LaneWindowCoop, // any layout: per-lane 64-B window, tails summed by quarter-waves
     TwoPass,        // any layout: k_tail_sums (bytes past 80) + k_parse_lane80
+    SpanTile,       // packed layouts: 16-KiB sub-tiles through LDS + chunk prefix sums
 };
 
 hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStream_t s);

@@ -2,15 +2,16 @@
 // gfx950 (nex-packet/src/frame.rs:299-315, 570-658; util.rs:65-183).
 //
 // One lane per frame, 256-lane workgroups, one tile of 256 consecutive frames
-// per workgroup. Header bytes are staged in LDS so the branchy per-protocol
-// parse reads LDS, not HBM; HBM is read once, coalesced where the layout
-// allows:
+// per workgroup; HBM is read once, coalesced:
 //   TileStride64 / TileStride : fixed-stride batches. The workgroup streams its
 //       whole tile (256 x stride bytes, contiguous) with 16-B loads in lane
 //       order into per-frame LDS slots, padded to break bank conflicts.
-//   LaneWindow : offset-table batches (IMIX). Each lane stages the first
-//       128 B of its frame (16-B aligned chunks) into its own LDS slot; bytes
-//       past the window (long payloads) are summed straight from HBM.
+//   SpanTile : packed batches (offset table without lengths, or any other
+//       stride). The tile's frames are one contiguous byte span, streamed
+//       through LDS in 16-KiB sub-tiles; L4 tail sums come from a prefix scan
+//       of chunk sums (k_parse_span).
+//   TwoPass : explicit lengths (frames anywhere, in any order): quarter-wave
+//       tail sums past byte 80, then one lane per frame on an 80-B head.
 #include "parse_kernels.hpp"
 
 namespace nexg {
@@ -21,6 +22,7 @@ ParseVariant choose_parse_variant(const ParseArgs& a) {
         a.count * (uint64_t)a.stride <= a.data_bytes) {
         return a.stride == 64u ? ParseVariant::TileStride64 : ParseVariant::TileStride;
     }
+    if (!a.lengths && (a.offsets || a.stride > 0)) return ParseVariant::SpanTile;
     return ParseVariant::TwoPass;
 }
 
@@ -40,6 +42,9 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             break;
         case ParseVariant::LaneWindowCoop:
             hipLaunchKernelGGL((k_parse_coop<OUT, 64, 0, 4>), grid, block, 0, s, a);
+            break;
+        case ParseVariant::SpanTile:
+            hipLaunchKernelGGL((k_parse_span<OUT, 1>), grid, block, 0, s, a);
             break;
         case ParseVariant::TwoPass:
             hipLaunchKernelGGL((k_tail_sums<OUT, 4>), grid, block, 0, s, a);

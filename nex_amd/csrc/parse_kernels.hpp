@@ -106,6 +106,24 @@ __device__ __forceinline__ void store_result(void* out, uint64_t idx, const nexg
     }
 }
 
+// Record output of a 256-frame tile through LDS: each thread has written its
+// 64-B record at stage + t * PITCH (call after a barrier); the tile's nf
+// records leave as contiguous 16-B stores (1 KiB per wave instruction)
+// instead of four 64-B-strided ones per thread.
+template <uint32_t PITCH>
+__device__ __forceinline__ void copy_out_records(const uint8_t* stage, void* out, uint64_t first, uint32_t nf) {
+    uint4* dst = reinterpret_cast<uint4*>(out) + first * 4u;
+    for (uint32_t c = threadIdx.x; c < nf * 4u; c += kTile)
+        dst[c] = *reinterpret_cast<const uint4*>(stage + (c >> 2) * PITCH + 16u * (c & 3u));
+}
+
+__device__ __forceinline__ void stage_record(uint8_t* slot, const nexg_record& r) {
+    uint4 v[4];
+    __builtin_memcpy(v, &r, sizeof(r));
+#pragma unroll
+    for (int k = 0; k < 4; k++) reinterpret_cast<uint4*>(slot)[k] = v[k];
+}
+
 // MODE 0: fixed stride tile staging (STRIDE = 0 -> runtime stride).
 // MODE 1: per-lane window staging.
 template <int MODE, int OUT, int STRIDE, int WIN, bool FAST = true, bool NT = false>
@@ -132,11 +150,12 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
             *reinterpret_cast<uint4*>(smem + f * PITCH + (byte - f * S)) = v;
         }
         __syncthreads();
-        if (tid >= nf) return;
-        g = T + (uint64_t)tid * S;
-        len = a.lengths ? a.lengths[idx] : S;
-        wlen = len < S ? len : S;
-        bad = len > 65535u || (first + tid) * S + len > a.data_bytes;
+        if (tid < nf) {
+            g = T + (uint64_t)tid * S;
+            len = a.lengths ? a.lengths[idx] : S;
+            wlen = len < S ? len : S;
+            bad = len > 65535u || (first + tid) * S + len > a.data_bytes;
+        }
     } else {
         if (tid >= nf) return;
         const uint64_t off = a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride;
@@ -154,28 +173,37 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
                 *reinterpret_cast<uint4*>(slot + 16u * k) = *reinterpret_cast<const uint4*>(A0 + 16u * k);
         }
     }
+    // MODE 0 + RECORD: every thread stays for the coalesced copy-out
+    constexpr bool kStaged = MODE == 0 && OUT == NEXG_OUT_RECORD && PITCH >= 64;
     nexg_record r;
-    if (MODE == 0 && STRIDE == 64 && FAST && !bad && len == 64u) {
-        // register copy of the whole frame: 4 x ds_read_b128 (pitch 80: conflict-free)
-        uint32_t w[16];
+    bool have = false;
+    if (tid < nf) {
+        if (MODE == 0 && STRIDE == 64 && FAST && !bad && len == 64u) {
+            // register copy of the whole frame: 4 x ds_read_b128 (pitch 80: conflict-free)
+            uint32_t w[16];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * k);
-            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            for (int k = 0; k < 4; k++) {
+                const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * k);
+                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            }
+            have = fast_udp4_64(w, a.opt_flags, r);
         }
-        if (fast_udp4_64(w, a.opt_flags, r)) {
-            store_result<OUT>(a.out, idx, r);
-            return;
+        if (!have) {
+            if (bad) {
+                r = nexg_record{};
+                r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
+            } else {
+                WinFrame f{slot, g, o, wlen};
+                parse_frame(f, (uint32_t)(reinterpret_cast<uint64_t>(g) & 1u), len, a.opt_flags, a.ip_offset, r);
+            }
         }
+        if (kStaged) stage_record(slot, r);  // own slot: no other thread reads it
+        else store_result<OUT>(a.out, idx, r);
     }
-    if (bad) {
-        r = nexg_record{};
-        r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
-    } else {
-        WinFrame f{slot, g, o, wlen};
-        parse_frame(f, (uint32_t)(reinterpret_cast<uint64_t>(g) & 1u), len, a.opt_flags, a.ip_offset, r);
+    if (kStaged) {
+        __syncthreads();
+        copy_out_records<PITCH>(smem, a.out, first, nf);
     }
-    store_result<OUT>(a.out, idx, r);
 }
 
 // util.rs:65-71 checksum(buf, skipword) per buffer; words outside the buffer
@@ -1158,6 +1186,190 @@ __global__ __launch_bounds__(256) void k_parse_lane80(ParseArgs a) {
         parse_frame(f, (uint32_t)(abs & 1u), len, a.opt_flags, a.ip_offset, r);
     }
     store_result<OUT>(a.out, idx, r);
+}
+
+}  // namespace nexg
+
+namespace nexg {
+
+// ---- packed-span path (offset tables without a lengths array, any stride) ----
+//
+// A workgroup owns 256 consecutive frames (one per thread). Packed frames are
+// contiguous, so their bytes form one span [off[f0], off[f0+256]). The span is
+// streamed through LDS in 16-KiB sub-tiles with plain coalesced 16-B loads:
+// every byte of the batch is fetched exactly once, by the one workgroup that
+// owns it (no head/tail split). Per sub-tile the 1024 chunk
+// LE-halfword sums are prefix-scanned; a frame's L4 tail sum is then the
+// difference of two prefix values Q(p) = Σ_{i<p} byte_i·256^(i mod 2) taken at
+// p = start+80 and p = end (ones-complement sums are linear, and 2^32 wrapping
+// is exact for a ≤64-KiB frame). The 80-B head window is copied from LDS into
+// registers and finished by fast_canonical80; anything it declines is parsed
+// by the generic core straight from HBM (L2-hot: the workgroup just read it).
+
+__device__ __forceinline__ uint32_t chunk_le_sum(const uint4& v) {
+    return halves_acc(v.w, halves_acc(v.z, halves_acc(v.y, halves_acc(v.x, 0u))));
+}
+
+// LE halfword sum of the first m (< 16) bytes of the 16-B LDS chunk at c
+__device__ __forceinline__ uint32_t chunk_prefix_sum(const uint8_t* c, uint32_t m) {
+    const uint4 v = *reinterpret_cast<const uint4*>(c);
+    auto msk = [&](uint32_t d) {  // bytes [4d, m) of dword d
+        return m >= 4u * d + 4u ? 0xFFFFFFFFu : (m <= 4u * d ? 0u : ((1u << (8u * (m - 4u * d))) - 1u));
+    };
+    return halves_acc(v.w & msk(3), halves_acc(v.z & msk(2), halves_acc(v.y & msk(1), halves(v.x & msk(0)))));
+}
+
+// inclusive wave64 scan on DPP (row_shr 1/2/4/8, row_bcast 15/31): no LDS traffic
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+
+// NB = 2: sub-tile k stages into buffer k&1, so the barrier that publishes
+// sub-tile k also retires every lookup into sub-tile k-2's buffer (3 barriers
+// per sub-tile, 41 KB LDS); NB = 1: one buffer and a 4th barrier (21 KB LDS,
+// more workgroups per CU).
+template <int OUT, int NB = 1, uint32_t SUB = 16384>
+__global__ __launch_bounds__(256) void k_parse_span(ParseArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[NB][SUB];
+    __shared__ __attribute__((aligned(16))) uint32_t s_pfx[NB][(SUB / 16u) + 4];  // [1024] = total
+    __shared__ uint32_t s_wsum[NB][4];
+    __shared__ uint64_t s_span[2];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint64_t f0 = (uint64_t)blockIdx.x * kTile;
+    const uint64_t idx = f0 + t;
+    const uint32_t nf = a.count - f0 < kTile ? (uint32_t)(a.count - f0) : kTile;
+    const uint64_t base = reinterpret_cast<uint64_t>(a.data);
+    uint64_t off = 0;
+    uint32_t len = 0;
+    const bool have = t < nf;
+    const bool ok = have && frame_extent(a, idx, off, len);
+    if (t == 0) s_span[0] = off;
+    if (t == nf - 1) s_span[1] = off + len;
+    __syncthreads();
+    const uint64_t lo = s_span[0], hi = s_span[1];
+    // packed contract: every frame of the group lies inside [lo, hi], and the
+    // span is small enough for 32-bit span-relative arithmetic
+    const bool inside = !have || (ok && off >= lo && off + len <= hi);
+    const bool span_ok = __syncthreads_and(inside) && hi >= lo && hi - lo <= (1ull << 30);
+    nexg_record r{};
+    if (!span_ok) {  // not packed here: every lane parses its own frame from HBM
+        if (have) {
+            if (!ok) {
+                r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
+            } else {
+                GlobalFrame f{a.data + off};
+                parse_frame(f, (uint32_t)((base + off) & 1u), len, a.opt_flags, a.ip_offset, r);
+            }
+            store_result<OUT>(a.out, idx, r);
+        }
+        return;
+    }
+    const uint64_t A0 = (base + lo) & ~15ull;
+    const uint32_t span = (uint32_t)(((base + hi + 15u) & ~15ull) - A0);
+    // span-relative positions: head, tail start (head + 80), end
+    const uint32_t hr = (uint32_t)(base + off - A0);
+    const bool want_tail = have && len > kLaneWin;
+    const bool fast = have && ((base + off) & 3u) == 0 && !(a.opt_flags & NEXG_PARSE_FROM_IP);
+    uint32_t qa = 0, qb = 0, run = 0;
+    uint32_t w[20];
+#pragma unroll
+    for (int j = 0; j < 20; j++) w[j] = 0;
+
+    constexpr int CPT = SUB / 4096u;  // 16-B chunks per thread per sub-tile
+    uint4 cur[CPT];
+    auto fetch = [&](uint32_t S, uint4 (&v)[CPT]) {
+#pragma unroll
+        for (int i = 0; i < CPT; i++) {
+            const uint32_t c = S + 16u * (t + 256u * i);
+            v[i] = c < span ? load16<true>(reinterpret_cast<const void*>(A0 + c)) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    fetch(0, cur);
+    uint32_t buf = 0;
+    for (uint32_t S = 0; S < span; S += SUB, buf = NB == 2 ? buf ^ 1u : 0u) {
+        uint8_t* sb = s_bytes[buf];
+        uint32_t* sp = s_pfx[buf];
+        // (1) stage bytes + chunk sums, put the next sub-tile in flight
+#pragma unroll
+        for (int i = 0; i < CPT; i++) {
+            const uint32_t c = t + 256u * i;
+            *reinterpret_cast<uint4*>(sb + 16u * c) = cur[i];
+            sp[c] = chunk_le_sum(cur[i]);
+        }
+        const uint32_t E = S + SUB;
+        if (E < span) fetch(E, cur);
+        __syncthreads();
+        // (2) block exclusive scan of the 1024 chunk sums (4 consecutive per thread)
+        uint32_t cs[CPT];
+        uint32_t own = 0;
+#pragma unroll
+        for (int i = 0; i < CPT; i++) own += (cs[i] = sp[CPT * t + i]);
+        const uint32_t incl = wave_incl_scan_dpp(own);
+        if (lane == 63u) s_wsum[buf][wv] = incl;
+        __syncthreads();
+        const uint4 ws = *reinterpret_cast<const uint4*>(s_wsum[buf]);
+        const uint32_t wbase = (wv > 0 ? ws.x : 0u) + (wv > 1 ? ws.y : 0u) + (wv > 2 ? ws.z : 0u);
+        const uint32_t total = ws.x + ws.y + ws.z + ws.w;
+        uint32_t ex = wbase + incl - own;
+#pragma unroll
+        for (int i = 0; i < CPT; i++) {
+            sp[CPT * t + i] = ex;
+            ex += cs[i];
+        }
+        if (t == 0) sp[(SUB / 16u)] = total;
+        __syncthreads();
+        // (3) prefix values at this sub-tile's positions, head window copy
+        const bool last = E >= span;
+        auto q_at = [&](uint32_t d) {  // d = position - S, 0 <= d <= SUB
+            const uint32_t c = d >> 4, m = d & 15u;
+            return run + sp[c] + (m ? chunk_prefix_sum(sb + 16u * c, m) : 0u);
+        };
+        const uint32_t da = hr + kLaneWin - S, db = hr + len - S;  // wrap: < 0 -> huge
+        if (want_tail && (da < SUB || (last && da == SUB))) qa = q_at(da);
+        if (have && (db < SUB || (last && db == SUB))) qb = q_at(db);
+        const uint32_t dh = hr - S;
+        if (fast) {
+            if (dh <= SUB - kLaneWin) {  // whole window in this sub-tile (the usual case)
+#pragma unroll
+                for (int j = 0; j < 20; j++) w[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4u * j);
+            } else if (dh < SUB || dh + kLaneWin - 1u < kLaneWin - 1u) {  // straddles a sub-tile edge
+#pragma unroll
+                for (int j = 0; j < 20; j++) {
+                    const uint32_t d = dh + 4u * j;
+                    if (d < SUB) w[j] = *reinterpret_cast<const uint32_t*>(sb + d);
+                }
+            }
+        }
+        run += total;
+        if (NB == 1) __syncthreads();
+    }
+    if (have) {
+        bool done = false;
+        if (fast) {
+#pragma unroll
+            for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
+            done = fast_canonical80(w, len, a.opt_flags, want_tail ? (uint32_t)(qb - qa) : 0u, r);
+        }
+        if (!done) {
+            GlobalFrame f{a.data + off};
+            parse_frame(f, (uint32_t)((base + off) & 1u), len, a.opt_flags, a.ip_offset, r);
+        }
+        if (OUT != NEXG_OUT_RECORD) store_result<OUT>(a.out, idx, r);
+    }
+    if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the (now idle) byte buffer
+        static_assert(OUT != NEXG_OUT_RECORD || NB * SUB >= kTile * 64u, "record staging needs 16 KiB");
+        uint8_t* stage = &s_bytes[0][0];
+        if (NB == 2) __syncthreads();
+        if (have) stage_record(stage + 64u * t, r);
+        __syncthreads();
+        copy_out_records<64>(stage, a.out, f0, nf);
+    }
 }
 
 }  // namespace nexg

@@ -91,6 +91,21 @@ class FrameBatch:
                    lengths=torch.from_numpy(lens).to(device))
 
     @classmethod
+    def from_packed(cls, frames: Sequence[bytes], device="cuda", pad_to=1, shift=0):
+        """Offset table only (lengths implied by consecutive offsets): frames
+        zero-padded to `pad_to`, back to back, starting `shift` bytes into an
+        allocation (the packed layout nexg_parse_batch streams by spans)."""
+        torch = _torch()
+        padded = [bytes(f) + bytes((-len(f)) % pad_to) for f in frames]
+        offs = np.zeros(len(padded) + 1, dtype=np.int64)
+        offs[1:] = np.cumsum([len(f) for f in padded])
+        buf = np.zeros(shift + int(offs[-1]) + 16, dtype=np.uint8)
+        buf[shift:shift + int(offs[-1])] = np.frombuffer(b"".join(padded), dtype=np.uint8)
+        dev = torch.from_numpy(buf).to(device)
+        return cls(data=dev[shift:shift + int(offs[-1])], count=len(padded),
+                   offsets=torch.from_numpy(offs).to(device))
+
+    @classmethod
     def from_strided(cls, array: np.ndarray, device="cuda", lengths=None):
         """count x stride uint8 host array -> fixed-stride device batch."""
         torch = _torch()

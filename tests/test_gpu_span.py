@@ -1,0 +1,111 @@
+"""GPU parity of the packed-span path (k_parse_span: offset table without a
+lengths array, or a stride the tile kernels do not take) against the oracle's
+batch parser on the very same layout (oracle/nex_oracle.c nexo_parse_batch).
+
+The span kernel streams each 256-frame group's bytes through 16-KiB LDS
+sub-tiles and derives L4 sums from chunk prefix sums, so the cases here aim at
+its edges: frames crossing sub-tile edges, frames far longer than a sub-tile
+(up to the 65535-B ceiling), odd and unaligned starts, groups with a frame
+the layout rejects (BAD_EXTENT -> per-frame fallback), partial last groups."""
+import numpy as np
+import pytest
+
+from nex_amd import abi
+from nex_amd.engine import FrameBatch
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+
+
+def _big_frames(rng):
+    """Checksum-valid long frames: IPv4/IPv6 x UDP/TCP, 1.5-64 KiB."""
+    out = []
+    for n in (1400, 4000, 9000, 16300, 16384, 20000, 40000, 65535 - 14 - 20 - 8):
+        p = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        out.append(helpers._eth(helpers._ipv4(helpers._udp(p), 17)))
+        q = p[: n - 12]
+        out.append(helpers._eth(helpers._ipv4(helpers._tcp(q), 6)))
+        if n + 40 + 8 <= 65535:
+            out.append(helpers._eth(helpers._ipv6(helpers._udp(p[: n - 40]), 17), 0x86DD))
+    return out
+
+
+def _oracle_same_layout(oracle, batch, flags=0, ip_offset=0):
+    data = batch.data.cpu().numpy()
+    offs = batch.offsets.cpu().numpy().astype(np.uint64)
+    return oracle.parse_packed(data, offs, None, flags=flags, ip_offset=ip_offset)
+
+
+@pytest.fixture(scope="module")
+def mixed(oracle):
+    rng = np.random.default_rng(2024)
+    g = helpers.golden()
+    base = ([bytes.fromhex(v["frame"]) for v in g["frames"]] + helpers.crafted_frames() +
+            [oracle.gen_frame(abi.WL_IMIX, i) for i in range(300)] + _big_frames(rng))
+    frames = base + helpers.mutate_frames(rng, base, 6000)
+    order = rng.permutation(len(frames))
+    return [frames[i] for i in order]
+
+
+@pytest.mark.parametrize("pad,shift", [(1, 0), (1, 3), (2, 1), (4, 0), (4, 8), (16, 5)])
+def test_packed_offsets_only(engine, oracle, mixed, pad, shift):
+    batch = FrameBatch.from_packed(mixed, pad_to=pad, shift=shift)
+    want = _oracle_same_layout(oracle, batch)
+    got = engine.parse_to_numpy(batch, out_kind=abi.OUT_RECORD)
+    helpers.records_equal(got, want, None, f"packed pad={pad} shift={shift}")
+    got_d = engine.parse_to_numpy(batch, out_kind=abi.OUT_DESC)
+    for n in abi.DESC_DTYPE.names:
+        assert (got_d[n] == want[n]).all(), n
+
+
+@pytest.mark.parametrize("flags,ip_offset", [(abi.PARSE_STRICT, 0), (abi.PARSE_FROM_IP, 14),
+                                             (abi.PARSE_FROM_IP | abi.PARSE_STRICT, 14)])
+def test_packed_parse_options(engine, oracle, mixed, flags, ip_offset):
+    from nex_amd.frame import ParseMode, ParseOption
+    batch = FrameBatch.from_packed(mixed[:3000], pad_to=4)
+    want = _oracle_same_layout(oracle, batch, flags, ip_offset)
+    opt = ParseOption(bool(flags & abi.PARSE_FROM_IP), ip_offset)
+    mode = ParseMode.Strict if flags & abi.PARSE_STRICT else ParseMode.Lenient
+    got = engine.parse_to_numpy(batch, opt, mode, abi.OUT_RECORD)
+    helpers.records_equal(got, want, None, f"packed flags={flags}")
+
+
+def test_packed_bad_extent_group(engine, oracle, mixed):
+    """A 70000-B gap in the offset table: that frame is BAD_EXTENT, its group
+    falls back to per-frame parsing, every other group stays on spans."""
+    import torch
+    frames = mixed[:2000]
+    batch = FrameBatch.from_packed(frames, pad_to=4)
+    offs = batch.offsets.cpu().numpy().copy()
+    data = batch.data.cpu().numpy()
+    k = 700
+    grown = np.concatenate([data[:offs[k + 1]], np.zeros(70000, np.uint8), data[offs[k + 1]:]])
+    offs[k + 1:] += 70000
+    b2 = FrameBatch(data=torch.from_numpy(grown).cuda(), count=len(frames),
+                    offsets=torch.from_numpy(offs).cuda())
+    want = oracle.parse_packed(grown, offs.astype(np.uint64), None)
+    assert abi.status_of(np.array([want["flags"][k]]))[0] == abi.ERR_BAD_EXTENT
+    got = engine.parse_to_numpy(b2, out_kind=abi.OUT_RECORD)
+    helpers.records_equal(got, want, None, "bad extent group")
+
+
+@pytest.mark.parametrize("stride", [144, 200, 1518])
+def test_wide_stride_spans(engine, oracle, mixed, stride):
+    """Fixed strides the tile kernels do not take go through spans too."""
+    sel = [f for f in mixed if len(f) <= stride][:4000]
+    rng = np.random.default_rng(stride)
+    arr = rng.integers(0, 256, (len(sel), stride), dtype=np.uint8)
+    for i, f in enumerate(sel):
+        arr[i, :len(f)] = np.frombuffer(f, np.uint8)
+    full = [bytes(arr[i]) for i in range(len(sel))]
+    want = oracle.parse_frames(full)
+    got = engine.parse_to_numpy(FrameBatch.from_strided(arr))
+    helpers.records_equal(got, want, full, f"stride={stride}")
+
+
+@pytest.mark.parametrize("count", [1, 255, 257, 1000])
+def test_partial_groups(engine, oracle, mixed, count):
+    batch = FrameBatch.from_packed(mixed[:count], pad_to=2, shift=1)
+    want = _oracle_same_layout(oracle, batch)
+    got = engine.parse_to_numpy(batch, out_kind=abi.OUT_RECORD)
+    helpers.records_equal(got, want, None, f"count={count}")

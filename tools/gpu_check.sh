@@ -27,6 +27,7 @@ if [[ $STEPS == *bench* || $STEPS == all ]]; then
   step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5
   step bench_ser 300 python bench.py --workload ser --steps 50 --warmup 5 --no-cpu-baseline
   step bench_udp64_record 300 python bench.py --out record --steps 20 --warmup 3 --no-cpu-baseline
+  step bench_imix_record 300 python bench.py --workload imix --out record --steps 10 --warmup 2 --no-cpu-baseline
 fi
 if [[ $STEPS == *prof* || $STEPS == all ]]; then
   step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline

@@ -89,10 +89,12 @@ int main(int argc, char** argv) {
     uint8_t* data;
     uint2 *out, *ref;
     uint4* cpy;
+    void* rec;
     CK(hipMalloc(&data, count * 64));
     CK(hipMalloc(&out, count * 8));
     CK(hipMalloc(&ref, count * 8));
     CK(hipMalloc(&cpy, count * 64));
+    CK(hipMalloc(&rec, count * 64));
     if (nexg_gen_frames(ctx, 1, 0x6E6578, 0, count, data, nullptr, 64, nullptr) != 0) return 1;
     CK(hipDeviceSynchronize());
     ParseArgs a{};
@@ -103,7 +105,8 @@ int main(int argc, char** argv) {
     vars.push_back({"prod_fast", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, true, false>), count * 64.0});
     vars.push_back({"prod_fast_nt", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, true, true>), count * 64.0});
     vars.push_back({"prod_generic", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, false, false>), count * 64.0});
-    vars.push_back({"udp64_stream_w64", parse(k_parse_stream<NEXG_OUT_DESC, 64>), count * 64.0});
+    vars.push_back({"span_udp64_nb2", parse(k_parse_span<NEXG_OUT_DESC, 2>), count * 64.0});
+    vars.push_back({"span_udp64_nb1", parse(k_parse_span<NEXG_OUT_DESC, 1>), count * 64.0});
     vars.push_back({"lanewindow_generic", parse(k_parse<1, NEXG_OUT_DESC, 0, 128, false, false>), count * 64.0});
     vars.push_back({"lane_direct_fast", [=]() { hipLaunchKernelGGL(k_lanedirect, grid, blk, 0, 0, data, count, out, 0u); }, count * 64.0});
     vars.push_back({"stage_only", [=]() { hipLaunchKernelGGL(k_stageonly, grid, blk, 0, 0, data, count, out); }, count * 64.0});
@@ -117,7 +120,7 @@ int main(int argc, char** argv) {
     std::vector<uint2> h_ref(count), h_out(count);
     CK(hipMemcpy(h_ref.data(), ref, count * 8, hipMemcpyDeviceToHost));
     for (auto& v : vars) {
-        if (v.name.rfind("prod", 0) != 0 && v.name.rfind("lane", 0) != 0) continue;
+        if (v.name.rfind("prod", 0) != 0 && v.name.rfind("lane", 0) != 0 && v.name.rfind("span", 0) != 0) continue;
         CK(hipMemset(out, 0, count * 8));
         v.run();
         CK(hipDeviceSynchronize());
@@ -147,51 +150,24 @@ int main(int argc, char** argv) {
     const double ibytes = (double)ho[icount];
     auto iparse = [&](auto kern) { return [=]() { hipLaunchKernelGGL(kern, grid, blk, 0, 0, ia); }; };
     std::vector<Var> ivars;
-    ivars.push_back({"imix_coop_w128", iparse(k_parse_coop<NEXG_OUT_DESC, 128>), ibytes});
-    ivars.push_back({"imix_coop_w96", iparse(k_parse_coop<NEXG_OUT_DESC, 96>), ibytes});
-    ivars.push_back({"imix_coop_w64", iparse(k_parse_coop<NEXG_OUT_DESC, 64>), ibytes});
-    ivars.push_back({"imix_coop_w64_u4", iparse(k_parse_coop<NEXG_OUT_DESC, 64, 0, 4>), ibytes});
-    ivars.push_back({"imix_2pass_u8", [=]() {
-        hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 8>), grid, blk, 0, 0, ia);
-        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
     ivars.push_back({"imix_2pass_u4", [=]() {
         hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia);
         hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
-    ivars.push_back({"imix_2pass_u16", [=]() {
-        hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 16>), grid, blk, 0, 0, ia);
-        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
-    ivars.push_back({"imix_fused_u4", iparse(k_parse_imix<NEXG_OUT_DESC, 4>), ibytes});
-    ivars.push_back({"imix_fused_u2", iparse(k_parse_imix<NEXG_OUT_DESC, 2>), ibytes});
-    ivars.push_back({"imix_fused_u6", iparse(k_parse_imix<NEXG_OUT_DESC, 6>), ibytes});
-    ivars.push_back({"udp64_fused_u4", parse(k_parse_imix<NEXG_OUT_DESC, 4>), count * 64.0});
-    ivars.push_back({"imix_2pass_wave4", [=]() {
-        hipLaunchKernelGGL((k_tail_sums_wave<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia);
-        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
-    ivars.push_back({"imix_2pass_wave2", [=]() {
-        hipLaunchKernelGGL((k_tail_sums_wave<NEXG_OUT_DESC, 2>), grid, blk, 0, 0, ia);
-        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
-    ivars.push_back({"ABL_tailswave4_only", [=]() { hipLaunchKernelGGL((k_tail_sums_wave<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia); }, ibytes});
+    ivars.push_back({"imix_span_nb2", iparse(k_parse_span<NEXG_OUT_DESC, 2>), ibytes});
+    ivars.push_back({"imix_span_nb1", iparse(k_parse_span<NEXG_OUT_DESC, 1>), ibytes});
+    ivars.push_back({"imix_span_nb1_8k", iparse(k_parse_span<NEXG_OUT_DESC, 1, 8192>), ibytes});
+    ivars.push_back({"imix_span_nb2_8k", iparse(k_parse_span<NEXG_OUT_DESC, 2, 8192>), ibytes});
+    ivars.push_back({"imix_span_nb1_32k", iparse(k_parse_span<NEXG_OUT_DESC, 1, 32768>), ibytes});
+    ivars.push_back({"imix_span_rec", [=]() {
+        ParseArgs r2 = ia; r2.out = rec;
+        hipLaunchKernelGGL((k_parse_span<NEXG_OUT_RECORD, 1>), grid, blk, 0, 0, r2); }, ibytes});
     ivars.push_back({"ABL_tails_only_u4", [=]() { hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia); }, ibytes});
-    ivars.push_back({"ABL_tails_only_u8", [=]() { hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 8>), grid, blk, 0, 0, ia); }, ibytes});
     ivars.push_back({"ABL_lane80_only", [=]() { hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
-    ivars.push_back({"udp64_lane80_2pass", [=]() {
-        hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 8>), grid, blk, 0, 0, a);
-        hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, a); }, count * 64.0});
-    ivars.push_back({"imix_wave_w64", iparse(k_parse_wave<NEXG_OUT_DESC, 64>), ibytes});
-    ivars.push_back({"imix_wave_w64_u8", iparse(k_parse_wave<NEXG_OUT_DESC, 64, 8>), ibytes});
-    ivars.push_back({"imix_wave_w80", iparse(k_parse_wave<NEXG_OUT_DESC, 80>), ibytes});
-    ivars.push_back({"imix_wave_w96", iparse(k_parse_wave<NEXG_OUT_DESC, 96>), ibytes});
-    ivars.push_back({"imix_coop_w80", iparse(k_parse_coop<NEXG_OUT_DESC, 80>), ibytes});
-    ivars.push_back({"imix_stream_w64", iparse(k_parse_stream<NEXG_OUT_DESC, 64>), ibytes});
-    ivars.push_back({"imix_streamsrch_w64", iparse(k_parse_stream<NEXG_OUT_DESC, 64, false>), ibytes});
-    ivars.push_back({"imix_stream_w96", iparse(k_parse_stream<NEXG_OUT_DESC, 96>), ibytes});
-    ivars.push_back({"imix_stream_w128", iparse(k_parse_stream<NEXG_OUT_DESC, 128>), ibytes});
-    ivars.push_back({"imix_lanewindow", iparse(k_parse<1, NEXG_OUT_DESC, 0, 128>), ibytes});
     hipLaunchKernelGGL((k_parse<1, NEXG_OUT_DESC, 0, 128>), grid, blk, 0, 0, ParseArgs{idata, ho[icount], ioff, nullptr, 0, icount, 0, 0, ref});
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(h_ref.data(), ref, count * 8, hipMemcpyDeviceToHost));
     for (auto& v : ivars) {
-        if (v.name.rfind("ABL", 0) == 0 || v.name.rfind("udp64", 0) == 0) continue;
+        if (v.name.rfind("ABL", 0) == 0 || v.name.rfind("udp64", 0) == 0 || v.name.find("_rec") != std::string::npos) continue;
         CK(hipMemset(out, 0, count * 8));
         v.run();
         CK(hipDeviceSynchronize());
@@ -200,11 +176,6 @@ int main(int argc, char** argv) {
         for (uint64_t i = 0; i < count; i++) bad += memcmp(&h_out[i], &h_ref[i], 8) != 0;
         printf("check %-20s mismatches=%llu\n", v.name.c_str(), (unsigned long long)bad);
     }
-    ivars.push_back({"ABL_coop64_noparse", iparse(k_parse_coop<NEXG_OUT_DESC, 64, 1>), ibytes});
-    ivars.push_back({"ABL_coop64_nopieces", iparse(k_parse_coop<NEXG_OUT_DESC, 64, 2>), ibytes});
-    ivars.push_back({"ABL_imix_stream_noparse", iparse(k_parse_stream<NEXG_OUT_DESC, 64, true, 1>), ibytes});
-    ivars.push_back({"ABL_imix_srch_noparse", iparse(k_parse_stream<NEXG_OUT_DESC, 64, false, 1>), ibytes});
-    ivars.push_back({"ABL_udp64_srch_noparse", parse(k_parse_stream<NEXG_OUT_DESC, 64, false, 1>), count * 64.0});
     for (auto& v : ivars) vars.push_back(v);
     printf("imix bytes %.3f GB, mean frame %.1f B\n", ibytes / 1e9, ibytes / icount);
 
