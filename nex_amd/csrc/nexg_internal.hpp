@@ -26,7 +26,6 @@ enum class ParseVariant {
     TileStride64,   // fixed 64-B stride: coalesced tile staging into LDS
     TileStride,     // fixed stride (multiple of 16, <= 128): tile staging
     LaneWindow,     // any layout: per-lane 128-B window, lane sums its own tail
-    LaneWindowCoop, // any layout: per-lane 64-B window, tails summed by quarter-waves
     TwoPass,        // any layout: k_tail_sums (bytes past 80) + k_parse_lane80
     SpanTile,       // packed layouts: 16-KiB sub-tiles through LDS + chunk prefix sums
 };

@@ -40,9 +40,6 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
         case ParseVariant::LaneWindow:
             hipLaunchKernelGGL((k_parse<1, OUT, 0, 128>), grid, block, 0, s, a);
             break;
-        case ParseVariant::LaneWindowCoop:
-            hipLaunchKernelGGL((k_parse_coop<OUT, 64, 0, 4>), grid, block, 0, s, a);
-            break;
         case ParseVariant::SpanTile:
             hipLaunchKernelGGL((k_parse_span<OUT, 1>), grid, block, 0, s, a);
             break;

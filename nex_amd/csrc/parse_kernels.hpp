@@ -21,65 +21,6 @@ struct GlobalFrame {
     }
 };
 
-// Window in LDS plus ONE deferred tail: the first byte range a checksum needs
-// beyond the window is not read here; its little-endian sum is produced by
-// the workgroup's cooperative piece pass and added in afterwards. Any further
-// beyond-window range (rare: headers past the window) is read directly.
-struct TileFrame {
-    const uint8_t* slot;
-    const uint8_t* g;
-    uint32_t o;
-    uint32_t wlen;
-    mutable uint32_t dstate = 0;  // 0 none, 1 tail recorded, 2 multiplier known, 3 claimed
-    mutable uint32_t ta = 0, tb = 0, mult = 0, stored = 0, which = 0;
-    mutable uint64_t t = 0;
-
-    NEXG_HD uint32_t u8(uint32_t i) const {
-        return i < wlen ? (uint32_t)slot[o + i] : (uint32_t)g[i];
-    }
-    NEXG_HD uint64_t le_sum(uint32_t a, uint32_t b) const {
-        uint64_t acc = 0;
-        const uint32_t lb = b < wlen ? b : wlen;
-        if (a < lb) {
-            const uint32_t A = o + a, B = o + lb;
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(slot);
-            uint32_t s = 0;
-            for (uint32_t j = A & ~3u; j < B; j += 4) s += halves(w[j >> 2] & range_mask(j, A, B));
-            acc = s;
-        }
-        const uint32_t ga = a > wlen ? a : wlen;
-        if (ga < b) {
-            if (dstate == 0) {
-                ta = ga;
-                tb = b;
-                dstate = 1;
-            } else {
-                const uint64_t base = reinterpret_cast<uint64_t>(g);
-                acc += global_le_sum(base + ga, base + b);
-            }
-        }
-        return acc;
-    }
-    NEXG_HD void note_mult(uint32_t m) const {
-        if (dstate == 1) { mult = m; dstate = 2; }
-    }
-    NEXG_HD void note_finish(uint64_t tt, uint32_t cs, uint32_t w) const {
-        if (dstate == 2) { t = tt; stored = cs; which = w; dstate = 3; }
-    }
-    // fold the deferred tail sum into the claimed checksum and patch the record
-    NEXG_HD void complete(uint64_t tail_le_sum, nexg_record& r) const {
-        if (dstate != 3) return;
-        const uint32_t calc = fold_complement(t + (uint64_t)mult * tail_le_sum);
-        if (which == kCsumIp) {
-            r.ip_csum_calc = (uint16_t)calc;
-            r.flags = (r.flags & ~NEXG_C_IP_OK) | (calc == stored ? NEXG_C_IP_OK : 0u);
-        } else {
-            r.l4_csum_calc = (uint16_t)calc;
-            r.flags = (r.flags & ~NEXG_C_L4_OK) | (calc == stored ? NEXG_C_L4_OK : 0u);
-        }
-    }
-};
-
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
@@ -232,381 +173,6 @@ __global__ __launch_bounds__(256) void k_checksum(ParseArgs a, uint32_t skipword
     out[idx] = (uint16_t)fold_complement(t);
 }
 
-// MODE 2 (offset-table batches with long frames): lane-per-frame parse of a
-// 128-B LDS window, payload tails summed cooperatively. Each frame's deferred
-// tail is cut at absolute 256-B boundaries into pieces; a piece is 16 aligned
-// 16-B chunks, one per lane of a quarter-wave, so every load is part of a
-// contiguous 256-B request. Pieces of the whole tile are spread over the 16
-// quarter-waves; partial sums meet in LDS (ds_add_u32), then each frame lane
-// finishes its checksum (TileFrame::complete).
-template <int OUT, int WIN, int ABL = 0, uint32_t PU = 8>
-__global__ __launch_bounds__(256) void k_parse_coop(ParseArgs a) {
-    constexpr uint32_t PITCH = WIN + 16;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kTile * PITCH];
-    __shared__ uint32_t pfx[kTile + 1];
-    __shared__ uint32_t acc[kTile];
-    __shared__ uint64_t tail_a[kTile];
-    __shared__ uint32_t tail_len[kTile];
-    __shared__ uint32_t wave_tot[4];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t first = (uint64_t)blockIdx.x * kTile;
-    const uint64_t left = a.count - first;
-    const uint32_t nf = left < kTile ? (uint32_t)left : kTile;
-    const uint64_t idx = first + tid;
-    const bool active = tid < nf;
-    uint8_t* slot = smem + tid * PITCH;
-    const uint8_t* g = nullptr;
-    uint32_t len = 0, o = 0, wlen = 0;
-    bool bad = !active;
-    if (active) {
-        const uint64_t off = a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride;
-        const uint64_t l64 = a.lengths ? (uint64_t)a.lengths[idx]
-                                       : (a.offsets ? a.offsets[idx + 1] - off : (uint64_t)a.stride);
-        bad = l64 > 65535u || off > a.data_bytes || l64 > a.data_bytes - off;
-        if (!bad) {
-            len = (uint32_t)l64;
-            g = a.data + off;
-            o = (uint32_t)(reinterpret_cast<uint64_t>(g) & 15u);
-            const uint8_t* A0 = g - o;
-            wlen = len < (uint32_t)WIN ? len : (uint32_t)WIN;
-            const uint32_t chunks = (o + wlen + 15u) >> 4;
-            for (uint32_t k = 0; k < chunks; k++)
-                *reinterpret_cast<uint4*>(slot + 16u * k) = load16<true>(A0 + 16u * k);
-        }
-    }
-    nexg_record r{};
-    TileFrame f{slot, g, o, wlen};
-    uint32_t np = 0;
-    if (bad) {
-        r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
-    } else if (ABL == 1) {  // ablation (kbench only): staging + pieces of the whole tail, no parse
-        r.flags = slot[o] ^ wlen;
-        if (len > wlen) {
-            f.ta = wlen; f.tb = len; f.dstate = 3;
-            const uint64_t A = reinterpret_cast<uint64_t>(g) + f.ta, B = reinterpret_cast<uint64_t>(g) + f.tb;
-            np = (uint32_t)(((B - 1) / kPiece) - (A / kPiece) + 1);
-            tail_a[tid] = A;
-            tail_len[tid] = f.tb - f.ta;
-        }
-    } else {
-        parse_frame(f, (uint32_t)(reinterpret_cast<uint64_t>(g) & 1u), len, a.opt_flags, a.ip_offset, r);
-        if (f.dstate == 3) {
-            const uint64_t A = reinterpret_cast<uint64_t>(g) + f.ta, B = reinterpret_cast<uint64_t>(g) + f.tb;
-            np = (uint32_t)(((B - 1) / kPiece) - (A / kPiece) + 1);
-            tail_a[tid] = A;
-            tail_len[tid] = f.tb - f.ta;
-        }
-    }
-    acc[tid] = 0;
-    // exclusive scan of piece counts over the tile
-    const uint32_t incl = wave_incl_scan(np);
-    if ((tid & 63u) == 63u) wave_tot[tid >> 6] = incl;
-    __syncthreads();
-    uint32_t wbase = 0;
-    for (uint32_t wv = 0; wv < (tid >> 6); wv++) wbase += wave_tot[wv];
-    pfx[tid] = wbase + incl - np;
-    if (tid == kTile - 1) pfx[kTile] = wbase + incl;
-    __syncthreads();
-    const uint32_t total = ABL == 2 ? 0u : pfx[kTile];  // ABL 2: parse without the piece pass
-    // Each quarter-wave owns a contiguous range of pieces; consecutive pieces
-    // mostly belong to one frame, so a lane keeps a running sum and the
-    // quarter-wave reduces + flushes it to LDS only when the frame changes.
-    const uint32_t grp = tid >> 4, gl = tid & 15u;
-    const uint32_t pb = (uint32_t)((uint64_t)total * grp / 16u);
-    const uint32_t pe = (uint32_t)((uint64_t)total * (grp + 1u) / 16u);
-    if (pb < pe) {
-        uint32_t lo = 0, hi = kTile;  // frame owning piece pb: last frame with pfx <= pb
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (pfx[mid] <= pb) lo = mid; else hi = mid;
-        }
-        uint32_t fi = lo;                    // frame of the running sum
-        uint32_t cf = lo, ce = pfx[lo + 1];  // resolution cursor: frame, its end piece
-        uint64_t ca = tail_a[lo], cb = ca + tail_len[lo];
-        uint64_t cpb = (ca & ~(uint64_t)(kPiece - 1)) - (uint64_t)pfx[lo] * kPiece;
-        uint32_t run = 0;
-        for (uint32_t p0 = pb; p0 < pe; p0 += PU) {
-            uint4 v[PU];
-            uint64_t C[PU], AA[PU], BB[PU];
-            uint32_t F[PU];
-#pragma unroll
-            for (uint32_t u = 0; u < PU; u++) {  // resolve pieces (cursor only moves forward)
-                const uint32_t pp = p0 + u;
-                while (pp < pe && pp >= ce) {
-                    cf++;
-                    ce = pfx[cf + 1];
-                    ca = tail_a[cf];
-                    cb = ca + tail_len[cf];
-                    cpb = (ca & ~(uint64_t)(kPiece - 1)) - (uint64_t)pfx[cf] * kPiece;
-                }
-                F[u] = cf;
-                AA[u] = ca;
-                BB[u] = cb;
-                C[u] = cpb + (uint64_t)pp * kPiece + 16u * gl;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < PU; u++) {
-                v[u] = make_uint4(0, 0, 0, 0);
-                if (p0 + u < pe && C[u] < BB[u] && C[u] + 16u > AA[u])
-                    v[u] = load16<true>(reinterpret_cast<const void*>(C[u]));
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < PU; u++) {
-                if (p0 + u >= pe) break;
-                if (F[u] != fi) {  // frame changes: flush the running sum (group-uniform)
-                    uint32_t s = run;
-                    s += __shfl_xor(s, 8, 16);
-                    s += __shfl_xor(s, 4, 16);
-                    s += __shfl_xor(s, 2, 16);
-                    s += __shfl_xor(s, 1, 16);
-                    if (gl == 0 && s) atomicAdd(&acc[fi], s);
-                    run = 0;
-                    fi = F[u];
-                }
-                const uint64_t c = C[u], A = AA[u], B = BB[u];
-                if (c < B && c + 16u > A) {
-                    if (c >= A && c + 16u <= B) {
-                        run += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) + halves(v[u].w);
-                    } else {
-                        if (c + 0 < B) run += halves(v[u].x & range_mask(c + 0, A, B));
-                        if (c + 4 < B) run += halves(v[u].y & range_mask(c + 4, A, B));
-                        if (c + 8 < B) run += halves(v[u].z & range_mask(c + 8, A, B));
-                        if (c + 12 < B) run += halves(v[u].w & range_mask(c + 12, A, B));
-                    }
-                }
-            }
-        }
-        uint32_t s = run;
-        s += __shfl_xor(s, 8, 16);
-        s += __shfl_xor(s, 4, 16);
-        s += __shfl_xor(s, 2, 16);
-        s += __shfl_xor(s, 1, 16);
-        if (gl == 0 && s) atomicAdd(&acc[fi], s);
-    }
-    __syncthreads();
-    if (!active) return;
-    if (!bad) f.complete(acc[tid], r);
-    store_result<OUT>(a.out, idx, r);
-}
-
-
-// Frame whose first wlen bytes sit in an LDS slot and whose whole-frame
-// little-endian sum `sall` was accumulated by the tile's streaming pass.
-// A range reaching past the window is summed as the complement
-// sall - prefix - suffix when that touches fewer HBM bytes than reading it.
-struct StreamFrame {
-    NEXG_NO_DEFER
-    const uint8_t* slot;
-    const uint8_t* g;
-    uint32_t o;
-    uint32_t wlen;
-    uint32_t len;
-    uint64_t sall;
-
-    NEXG_HD uint32_t u8(uint32_t i) const {
-        return i < wlen ? (uint32_t)slot[o + i] : (uint32_t)g[i];
-    }
-    NEXG_HD uint32_t lds_sum(uint32_t a, uint32_t b) const {  // a < b <= wlen
-        const uint32_t A = o + a, B = o + b;
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(slot);
-        uint32_t s = 0;
-        for (uint32_t j = A & ~3u; j < B; j += 4) s += halves(w[j >> 2] & range_mask(j, A, B));
-        return s;
-    }
-    NEXG_HD uint64_t hbm_sum(uint32_t a, uint32_t b) const {
-        if (a >= b) return 0;
-        const uint64_t base = reinterpret_cast<uint64_t>(g);
-        return global_le_sum(base + a, base + b);
-    }
-    NEXG_HD uint64_t le_sum(uint32_t a, uint32_t b) const {
-        if (b <= wlen) return lds_sum(a, b);
-        const uint32_t direct = b - (a > wlen ? a : wlen);
-        const uint32_t compl_cost = (a > wlen ? a - wlen : 0u) + (len - b);
-        if (direct <= compl_cost) {
-            uint64_t s = a < wlen ? lds_sum(a, wlen) : 0u;
-            return s + hbm_sum(a > wlen ? a : wlen, b);
-        }
-        uint64_t pre = (a ? lds_sum(0, a < wlen ? a : wlen) : 0u) + hbm_sum(wlen, a);
-        return sall - pre - hbm_sum(b, len);
-    }
-};
-
-// MODE 3 (offset-table batches, the IMIX path): per 256-frame tile,
-//   A. the tile's byte span is streamed in lane order with 16-B non-temporal
-//      loads (fully coalesced, like a copy). Each chunk adds its masked bytes
-//      to the owning frames' whole-frame sums (LDS atomics) and, when it
-//      falls in a frame's header window, is written into that frame's slot;
-//   B. one lane per frame parses from its slot (StreamFrame) and writes the
-//      result.
-// Needs the tile's frames in ascending, non-overlapping order (any gaps are
-// streamed and ignored); otherwise the tile falls back to per-lane windows.
-template <int OUT, int WIN, bool BAL = true, int ABL = 0>
-__global__ __launch_bounds__(256) void k_parse_stream(ParseArgs a) {
-    constexpr uint32_t PITCH = WIN + 16;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kTile * PITCH];
-    __shared__ uint32_t roff[kTile + 1];  // frame start relative to the 16-B aligned tile base
-    __shared__ uint32_t rlen[kTile];
-    __shared__ uint32_t sall[kTile];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t first = (uint64_t)blockIdx.x * kTile;
-    const uint64_t left = a.count - first;
-    const uint32_t nf = left < kTile ? (uint32_t)left : kTile;
-    const uint64_t idx = first + tid;
-    const bool active = tid < nf;
-    uint64_t off = 0, l64 = 0;
-    bool bad = !active;
-    if (active) {
-        off = a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride;
-        l64 = a.lengths ? (uint64_t)a.lengths[idx]
-                        : (a.offsets ? a.offsets[idx + 1] - off : (uint64_t)a.stride);
-        bad = l64 > 65535u || off > a.data_bytes || l64 > a.data_bytes - off;
-    }
-    const uint64_t f0off = a.offsets ? a.offsets[first] : first * (uint64_t)a.stride;
-    const uint64_t base = (reinterpret_cast<uint64_t>(a.data) + f0off) & ~15ull;
-    const uint64_t abs = reinterpret_cast<uint64_t>(a.data) + off;
-    // layout check: ascending, non-overlapping, span < 4 GiB, no bad extents
-    const uint64_t rel64 = abs - base;
-    const uint64_t nxt = (active && tid + 1 < nf)
-        ? (a.offsets ? a.offsets[idx + 1] : (idx + 1) * (uint64_t)a.stride) : ~0ull;
-    const bool ok_lane = !active || (!bad && off >= f0off && off + l64 <= nxt && rel64 + l64 < (1ull << 31));
-    const bool tile_ok = __syncthreads_and(ok_lane);
-    const uint32_t len = (active && !bad) ? (uint32_t)l64 : 0u;
-    uint8_t* slot = smem + tid * PITCH;
-    const uint8_t* g = a.data + off;
-    const uint32_t o = (uint32_t)(abs & 15u);
-    uint32_t wlen = 0;
-    if (tile_ok) {
-        roff[tid] = active ? (uint32_t)rel64 : 0xFFFFFFFFu;
-        rlen[tid] = len;
-        sall[tid] = 0;
-        if (tid == 0) roff[kTile] = 0xFFFFFFFFu;
-        __syncthreads();
-        const uint32_t last = nf - 1;
-        const uint32_t span = roff[last] + rlen[last];
-        const uint32_t nchunks = (span + 15u) >> 4;
-        constexpr uint32_t U = 4;
-        if (BAL) {
-            // balanced: thread t owns chunks [nchunks*t/256, nchunks*(t+1)/256)
-            const uint32_t cb = (uint32_t)((uint64_t)nchunks * tid / kTile);
-            const uint32_t ce = (uint32_t)((uint64_t)nchunks * (tid + 1) / kTile);
-            uint32_t fi = 0;
-            {
-                uint32_t lo = 0, hi = nf;
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (roff[mid] <= 16u * cb) lo = mid; else hi = mid;
-                }
-                fi = lo;
-            }
-            uint32_t acc = 0;
-            uint32_t nxt_start = fi + 1 < nf ? roff[fi + 1] : 0xFFFFFFFFu;
-            for (uint32_t c0 = cb; c0 < ce; c0 += U) {
-                uint4 v[U];
-#pragma unroll
-                for (uint32_t u = 0; u < U; u++)
-                    v[u] = c0 + u < ce ? load16<true>(reinterpret_cast<const void*>(base + 16ull * (c0 + u)))
-                                       : make_uint4(0, 0, 0, 0);
-#pragma unroll
-                for (uint32_t u = 0; u < U; u++) {
-                    const uint32_t c = c0 + u;
-                    if (c >= ce) break;
-                    const uint32_t r0 = 16u * c, r1 = r0 + 16u;
-                    for (;;) {  // frames overlapping [r0, r1), in order
-                        const uint32_t fs = roff[fi], fe = fs + rlen[fi];
-                        const uint32_t A = fs > r0 ? fs : r0, B = fe < r1 ? fe : r1;
-                        if (A < B) {
-                            uint32_t s;
-                            if (A == r0 && B == r1) {
-                                s = halves(v[u].x) + halves(v[u].y) + halves(v[u].z) + halves(v[u].w);
-                            } else {
-                                s = 0;
-                                if (r0 + 0 < B) s += halves(v[u].x & range_mask(r0 + 0, A, B));
-                                if (r0 + 4 < B) s += halves(v[u].y & range_mask(r0 + 4, A, B));
-                                if (r0 + 8 < B) s += halves(v[u].z & range_mask(r0 + 8, A, B));
-                                if (r0 + 12 < B) s += halves(v[u].w & range_mask(r0 + 12, A, B));
-                            }
-                            acc += s;
-                        }
-                        const uint32_t wb = fs & ~15u;
-                        if (fe > r0 && r0 >= wb && r0 < wb + PITCH)
-                            *reinterpret_cast<uint4*>(smem + fi * PITCH + (r0 - wb)) = v[u];
-                        if (nxt_start >= r1) break;  // next frame starts past this chunk
-                        if (acc) atomicAdd(&sall[fi], acc);
-                        acc = 0;
-                        fi++;
-                        nxt_start = fi + 1 < nf ? roff[fi + 1] : 0xFFFFFFFFu;
-                    }
-                }
-            }
-            if (acc) atomicAdd(&sall[fi], acc);
-        } else {
-        constexpr uint32_t U = 4;
-            for (uint32_t c0 = tid; c0 < nchunks; c0 += kTile * U) {
-                uint4 v[U];
-    #pragma unroll
-                for (uint32_t u = 0; u < U; u++) {
-                    const uint32_t c = c0 + kTile * u;
-                    v[u] = c < nchunks ? load16<true>(reinterpret_cast<const void*>(base + 16ull * c))
-                                       : make_uint4(0, 0, 0, 0);
-                }
-    #pragma unroll
-                for (uint32_t u = 0; u < U; u++) {
-                    const uint32_t c = c0 + kTile * u;
-                    if (c >= nchunks) break;
-                    const uint32_t r0 = 16u * c, r1 = r0 + 16u;
-                    // last frame starting at or before r0 (or frame 0)
-                    uint32_t lo = 0, hi = nf;
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (roff[mid] <= r0) lo = mid; else hi = mid;
-                    }
-                    for (uint32_t fi = lo; fi < nf && roff[fi] < r1; fi++) {
-                        const uint32_t fs = roff[fi], fe = fs + rlen[fi];
-                        if (fe <= r0) continue;
-                        const uint32_t A = fs > r0 ? fs : r0, B = fe < r1 ? fe : r1;
-                        uint32_t s = 0;
-                        if (A == r0 && B == r1) {
-                            s = halves(v[u].x) + halves(v[u].y) + halves(v[u].z) + halves(v[u].w);
-                        } else {
-                            if (r0 + 0 < B) s += halves(v[u].x & range_mask(r0 + 0, A, B));
-                            if (r0 + 4 < B) s += halves(v[u].y & range_mask(r0 + 4, A, B));
-                            if (r0 + 8 < B) s += halves(v[u].z & range_mask(r0 + 8, A, B));
-                            if (r0 + 12 < B) s += halves(v[u].w & range_mask(r0 + 12, A, B));
-                        }
-                        if (s) atomicAdd(&sall[fi], s);
-                        const uint32_t wb = fs & ~15u;
-                        if (r0 < wb + PITCH) *reinterpret_cast<uint4*>(smem + fi * PITCH + (r0 - wb)) = v[u];
-                    }
-                }
-            }
-            }
-        __syncthreads();
-        wlen = len < PITCH - o ? len : PITCH - o;
-    } else if (active && !bad) {
-        // fallback for unordered / overlapping layouts: per-lane window
-        const uint8_t* A0 = g - o;
-        wlen = len < (uint32_t)WIN ? len : (uint32_t)WIN;
-        const uint32_t chunks = (o + wlen + 15u) >> 4;
-        for (uint32_t k = 0; k < chunks; k++)
-            *reinterpret_cast<uint4*>(slot + 16u * k) = load16<true>(A0 + 16u * k);
-    }
-    if (!active) return;
-    nexg_record r{};
-    if (bad) {
-        r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
-    } else if (ABL == 1) {  // ablation (kbench only): streaming pass without the parse
-        r.flags = sall[tid] ^ wlen ^ slot[o];
-    } else if (tile_ok) {
-        StreamFrame f{slot, g, o, wlen, len, sall[tid]};
-        parse_frame(f, o & 1u, len, a.opt_flags, a.ip_offset, r);
-    } else {
-        WinFrame f{slot, g, o, wlen};
-        parse_frame(f, o & 1u, len, a.opt_flags, a.ip_offset, r);
-    }
-    store_result<OUT>(a.out, idx, r);
-}
-
-
 // wave-scope LDS visibility: the wave's LDS ops run in order; this only stops
 // the compiler from moving LDS accesses across the point
 __device__ __forceinline__ void wave_lds_sync() {
@@ -614,153 +180,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-
-// MODE 4 (offset-table batches, the IMIX path): like k_parse_coop, but every
-// wave is an independent 64-frame tile with no workgroup barrier, so one
-// wave's HBM round trips overlap the others' parse work.
-//   1. lane per frame: stage a WIN-byte window, parse (TileFrame defers the
-//      one long payload range);
-//   2. the wave's deferred tails are cut into 256-B pieces (absolute 256-B
-//      boundaries); each quarter-wave streams a contiguous run of pieces with
-//      a forward cursor and a running sum, flushed to LDS on frame change;
-//   3. each lane completes its checksum and writes its result.
-template <int OUT, int WIN, uint32_t PU = 4>
-__global__ __launch_bounds__(256) void k_parse_wave(ParseArgs a) {
-    constexpr uint32_t PITCH = WIN + 16;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kTile * PITCH];
-    __shared__ uint32_t s_pfx[4][65];
-    __shared__ uint32_t s_acc[4][64];
-    __shared__ uint64_t s_ta[4][64];
-    __shared__ uint32_t s_tl[4][64];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    uint32_t* pfx = s_pfx[wv];
-    uint32_t* acc = s_acc[wv];
-    uint64_t* tail_a = s_ta[wv];
-    uint32_t* tail_len = s_tl[wv];
-    const uint64_t wfirst = (uint64_t)blockIdx.x * kTile + 64u * wv;
-    if (wfirst >= a.count) return;  // whole wave idle (wave-uniform)
-    const uint64_t left = a.count - wfirst;
-    const uint32_t nf = left < 64u ? (uint32_t)left : 64u;
-    const uint64_t idx = wfirst + lane;
-    const bool active = lane < nf;
-    uint8_t* slot = smem + tid * PITCH;
-    const uint8_t* g = nullptr;
-    uint32_t len = 0, o = 0, wlen = 0;
-    bool bad = !active;
-    if (active) {
-        const uint64_t off = a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride;
-        const uint64_t l64 = a.lengths ? (uint64_t)a.lengths[idx]
-                                       : (a.offsets ? a.offsets[idx + 1] - off : (uint64_t)a.stride);
-        bad = l64 > 65535u || off > a.data_bytes || l64 > a.data_bytes - off;
-        if (!bad) {
-            len = (uint32_t)l64;
-            g = a.data + off;
-            o = (uint32_t)(reinterpret_cast<uint64_t>(g) & 15u);
-            const uint8_t* A0 = g - o;
-            wlen = len < (uint32_t)WIN ? len : (uint32_t)WIN;
-            const uint32_t chunks = (o + wlen + 15u) >> 4;
-            for (uint32_t k = 0; k < chunks; k++)
-                *reinterpret_cast<uint4*>(slot + 16u * k) = load16<true>(A0 + 16u * k);
-        }
-    }
-    nexg_record r{};
-    TileFrame f{slot, g, o, wlen};
-    uint32_t np = 0;
-    if (bad) {
-        r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
-    } else {
-        parse_frame(f, (uint32_t)(reinterpret_cast<uint64_t>(g) & 1u), len, a.opt_flags, a.ip_offset, r);
-        if (f.dstate == 3) {
-            const uint64_t A = reinterpret_cast<uint64_t>(g) + f.ta, B = reinterpret_cast<uint64_t>(g) + f.tb;
-            np = (uint32_t)(((B - 1) / kPiece) - (A / kPiece) + 1);
-            tail_a[lane] = A;
-            tail_len[lane] = f.tb - f.ta;
-        }
-    }
-    acc[lane] = 0;
-    const uint32_t incl = wave_incl_scan(np);
-    pfx[lane] = incl - np;
-    const uint32_t total = __shfl(incl, 63, 64);
-    if (lane == 63) pfx[64] = total;
-    wave_lds_sync();
-    const uint32_t grp = lane >> 4, gl = lane & 15u;
-    const uint32_t pb = (uint32_t)((uint64_t)total * grp / 4u);
-    const uint32_t pe = (uint32_t)((uint64_t)total * (grp + 1u) / 4u);
-    if (pb < pe) {
-        uint32_t lo = 0, hi = 64;  // frame owning piece pb
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (pfx[mid] <= pb) lo = mid; else hi = mid;
-        }
-        uint32_t fi = lo;
-        uint32_t cf = lo, ce = pfx[lo + 1];
-        uint64_t ca = tail_a[lo], cb = ca + tail_len[lo];
-        uint64_t cpb = (ca & ~(uint64_t)(kPiece - 1)) - (uint64_t)pfx[lo] * kPiece;
-        uint32_t run = 0;
-        for (uint32_t p0 = pb; p0 < pe; p0 += PU) {
-            uint4 v[PU];
-            uint64_t C[PU], AA[PU], BB[PU];
-            uint32_t F[PU];
-#pragma unroll
-            for (uint32_t u = 0; u < PU; u++) {
-                const uint32_t pp = p0 + u;
-                while (pp < pe && pp >= ce) {
-                    cf++;
-                    ce = pfx[cf + 1];
-                    ca = tail_a[cf];
-                    cb = ca + tail_len[cf];
-                    cpb = (ca & ~(uint64_t)(kPiece - 1)) - (uint64_t)pfx[cf] * kPiece;
-                }
-                F[u] = cf;
-                AA[u] = ca;
-                BB[u] = cb;
-                C[u] = cpb + (uint64_t)pp * kPiece + 16u * gl;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < PU; u++) {
-                v[u] = make_uint4(0, 0, 0, 0);
-                if (p0 + u < pe && C[u] < BB[u] && C[u] + 16u > AA[u])
-                    v[u] = load16<true>(reinterpret_cast<const void*>(C[u]));
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < PU; u++) {
-                if (p0 + u >= pe) break;
-                if (F[u] != fi) {
-                    uint32_t s = run;
-                    s += __shfl_xor(s, 8, 16);
-                    s += __shfl_xor(s, 4, 16);
-                    s += __shfl_xor(s, 2, 16);
-                    s += __shfl_xor(s, 1, 16);
-                    if (gl == 0 && s) atomicAdd(&acc[fi], s);
-                    run = 0;
-                    fi = F[u];
-                }
-                const uint64_t c = C[u], A = AA[u], B = BB[u];
-                if (c < B && c + 16u > A) {
-                    if (c >= A && c + 16u <= B) {
-                        run += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) + halves(v[u].w);
-                    } else {
-                        if (c + 0 < B) run += halves(v[u].x & range_mask(c + 0, A, B));
-                        if (c + 4 < B) run += halves(v[u].y & range_mask(c + 4, A, B));
-                        if (c + 8 < B) run += halves(v[u].z & range_mask(c + 8, A, B));
-                        if (c + 12 < B) run += halves(v[u].w & range_mask(c + 12, A, B));
-                    }
-                }
-            }
-        }
-        uint32_t s = run;
-        s += __shfl_xor(s, 8, 16);
-        s += __shfl_xor(s, 4, 16);
-        s += __shfl_xor(s, 2, 16);
-        s += __shfl_xor(s, 1, 16);
-        if (gl == 0 && s) atomicAdd(&acc[fi], s);
-    }
-    wave_lds_sync();
-    if (!active) return;
-    if (!bad) f.complete(acc[lane], r);
-    store_result<OUT>(a.out, idx, r);
-}
-
 
 constexpr uint32_t kLaneWin = 80;  // register window of k_parse_lane80
 
@@ -781,7 +200,7 @@ __device__ __forceinline__ bool frame_extent(const ParseArgs& a, uint64_t idx, u
 }
 
 // Pass 1 of the offset-table path: little-endian sum of every frame's bytes
-// [80, len), streamed by quarter-waves in 256-B pieces (see k_parse_wave);
+// [80, len), streamed by quarter-waves in 256-B pieces (16 aligned 16-B chunks);
 // no parse state, so registers and LDS stay small and many waves keep
 // loads in flight. Result -> handoff_slot.
 template <int OUT, uint32_t PU = 8>
@@ -908,248 +327,6 @@ __global__ __launch_bounds__(256) void k_tail_sums(ParseArgs a) {
     if (have) *handoff_slot<OUT>(a.out, idx) = acc[lane];
 }
 
-// MODE 5 (offset-table batches, the IMIX path): one wave = 64 frames, no
-// workgroup barrier. Each lane issues its frame's first 80 bytes into
-// registers, then the wave streams all its frames' bytes past 80 in 256-B
-// quarter-wave pieces (k_tail_sums' scheme) while those head loads are in
-// flight; finally each lane finishes its frame: fast_canonical80 for the six
-// canonical IMIX shapes, generic parse_frame from HBM for anything else.
-template <int OUT, uint32_t PU = 4>
-__global__ __launch_bounds__(256) void k_parse_imix(ParseArgs a) {
-    __shared__ uint32_t s_pfx[4][65];
-    __shared__ uint32_t s_acc[4][64];
-    __shared__ uint32_t s_ta[4][64];  // tail start relative to the wave base
-    __shared__ uint32_t s_tb[4][64];  // tail end   relative to the wave base
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    uint32_t* pfx = s_pfx[wv];
-    uint32_t* acc = s_acc[wv];
-    uint32_t* tail_a = s_ta[wv];
-    uint32_t* tail_b = s_tb[wv];
-    const uint64_t wfirst = (uint64_t)blockIdx.x * kTile + 64u * wv;
-    if (wfirst >= a.count) return;
-    const uint64_t left = a.count - wfirst;
-    const uint32_t nf = left < 64u ? (uint32_t)left : 64u;
-    const uint64_t idx = wfirst + lane;
-    uint32_t np = 0;
-    uint64_t off = 0;
-    uint32_t len = 0;
-    const bool valid = lane < nf && frame_extent(a, idx, off, len);
-    const bool have = valid && len > kLaneWin;
-    // head: the first 80 bytes straight into registers, issued before the
-    // tail stream so both are in flight together
-    const uint64_t abs = reinterpret_cast<uint64_t>(a.data) + off;
-    const bool head_ok = valid && (abs & 3u) == 0 &&
-                         abs + kLaneWin <= reinterpret_cast<uint64_t>(a.data) + a.data_bytes;
-    uint32_t w[20];
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        const uint4 v = head_ok ? load16a4<true>(reinterpret_cast<const void*>(abs + 16u * k))
-                                : make_uint4(0, 0, 0, 0);
-        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-    }
-    // wave base: lowest 256-B aligned tail start of the wave (wave-uniform)
-    uint64_t myA = have ? reinterpret_cast<uint64_t>(a.data) + off + kLaneWin : ~0ull;
-    uint64_t wbase = myA;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint64_t o2 = __shfl_xor(wbase, d, 64);
-        wbase = o2 < wbase ? o2 : wbase;
-    }
-    wbase &= ~(uint64_t)(kPiece - 1);
-    bool fits = true;
-    if (have) {
-        const uint64_t ra = myA - wbase, rb = ra + (len - kLaneWin);
-        fits = rb < (1ull << 31);
-        if (fits) {
-            np = (uint32_t)(((rb - 1) / kPiece) - (ra / kPiece) + 1);
-            tail_a[lane] = (uint32_t)ra;
-            tail_b[lane] = (uint32_t)rb;
-        }
-    }
-    const bool wave_ok = __all(fits);  // else (>2 GiB span): each lane sums its own tail
-    acc[lane] = 0;
-    if (!wave_ok) np = 0;
-    const uint32_t incl = wave_incl_scan(np);
-    pfx[lane] = incl - np;
-    const uint32_t total = __shfl(incl, 63, 64);
-    if (lane == 63) pfx[64] = total;
-    wave_lds_sync();
-    const uint32_t grp = lane >> 4, gl = lane & 15u;
-    const uint32_t pb = (uint32_t)((uint64_t)total * grp / 4u);
-    const uint32_t pe = (uint32_t)((uint64_t)total * (grp + 1u) / 4u);
-    const uint8_t* wb = reinterpret_cast<const uint8_t*>(wbase);
-    if (pb < pe) {
-        uint32_t lo = 0, hi = 64;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (pfx[mid] <= pb) lo = mid; else hi = mid;
-        }
-        uint32_t fi = lo;
-        uint32_t cf = lo, ce = pfx[lo + 1];
-        uint32_t ca = tail_a[lo], cb = tail_b[lo];
-        uint32_t cpb = (ca & ~(kPiece - 1)) - pfx[lo] * kPiece;  // mod 2^32
-        uint32_t run = 0;
-        for (uint32_t p0 = pb; p0 < pe; p0 += PU) {
-            uint4 v[PU];
-            uint32_t C[PU], AA[PU], BB[PU], F[PU];
-#pragma unroll
-            for (uint32_t u = 0; u < PU; u++) {
-                const uint32_t pp = p0 + u;
-                while (pp < pe && pp >= ce) {
-                    cf++;
-                    ce = pfx[cf + 1];
-                    ca = tail_a[cf];
-                    cb = tail_b[cf];
-                    cpb = (ca & ~(kPiece - 1)) - pfx[cf] * kPiece;
-                }
-                F[u] = cf;
-                AA[u] = ca;
-                BB[u] = cb;
-                C[u] = cpb + pp * kPiece + 16u * gl;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < PU; u++) {
-                v[u] = make_uint4(0, 0, 0, 0);
-                if (p0 + u < pe && C[u] < BB[u] && C[u] + 16u > AA[u]) v[u] = load16<true>(wb + C[u]);
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < PU; u++) {
-                if (p0 + u >= pe) break;
-                if (F[u] != fi) {
-                    uint32_t s = run;
-                    s += __shfl_xor(s, 8, 16);
-                    s += __shfl_xor(s, 4, 16);
-                    s += __shfl_xor(s, 2, 16);
-                    s += __shfl_xor(s, 1, 16);
-                    if (gl == 0 && s) atomicAdd(&acc[fi], s);
-                    run = 0;
-                    fi = F[u];
-                }
-                const uint32_t c = C[u], A = AA[u], B = BB[u];
-                if (c < B && c + 16u > A) {
-                    if (c >= A && c + 16u <= B) {
-                        run += halves(v[u].x) + halves(v[u].y) + halves(v[u].z) + halves(v[u].w);
-                    } else {
-                        if (c + 0 < B) run += halves(v[u].x & range_mask(c + 0, A, B));
-                        if (c + 4 < B) run += halves(v[u].y & range_mask(c + 4, A, B));
-                        if (c + 8 < B) run += halves(v[u].z & range_mask(c + 8, A, B));
-                        if (c + 12 < B) run += halves(v[u].w & range_mask(c + 12, A, B));
-                    }
-                }
-            }
-        }
-        uint32_t s = run;
-        s += __shfl_xor(s, 8, 16);
-        s += __shfl_xor(s, 4, 16);
-        s += __shfl_xor(s, 2, 16);
-        s += __shfl_xor(s, 1, 16);
-        if (gl == 0 && s) atomicAdd(&acc[fi], s);
-    }
-    wave_lds_sync();
-    if (lane >= nf) return;
-    nexg_record r{};
-    if (!valid) {
-        r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
-    } else {
-        bool done = false;
-        if (head_ok) {
-            const uint32_t tail = !have ? 0u
-                                : (wave_ok ? acc[lane] : (uint32_t)global_le_sum(myA, myA + len - kLaneWin));
-#pragma unroll
-            for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
-            done = fast_canonical80(w, len, a.opt_flags, tail, r);
-        }
-        if (!done) {
-            GlobalFrame gf{a.data + off};
-            parse_frame(gf, (uint32_t)(abs & 1u), len, a.opt_flags, a.ip_offset, r);
-        }
-    }
-    store_result<OUT>(a.out, idx, r);
-}
-
-__device__ __forceinline__ uint32_t wave_sum64(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
-
-// Pass 1, alternative shape: the whole wave streams one frame tail at a time
-// (lane l takes 16-B chunks l, l+64 of the tail), TW tails in flight per
-// round; frames are picked from the wave's 64 by ballot. No LDS, no cursor.
-template <int OUT, uint32_t TW = 4>
-__global__ __launch_bounds__(256) void k_tail_sums_wave(ParseArgs a) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
-    uint64_t off = 0;
-    uint32_t len = 0;
-    const bool have = idx < a.count && frame_extent(a, idx, off, len) && len > kLaneWin;
-    const uint64_t myA = reinterpret_cast<uint64_t>(a.data) + off + kLaneWin;
-    const uint64_t myB = reinterpret_cast<uint64_t>(a.data) + off + len;
-    uint64_t mask = __ballot(have);
-    uint32_t mine = 0;
-    while (mask) {
-        uint32_t fl[TW];
-        uint64_t A[TW], B[TW];
-        uint32_t cnt = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < TW; j++) {
-            fl[j] = 64;
-            A[j] = B[j] = 0;
-            if (mask) {
-                const uint32_t f = (uint32_t)__builtin_ctzll(mask);
-                mask &= mask - 1;
-                fl[j] = f;
-                A[j] = __shfl(myA, f, 64);
-                B[j] = __shfl(myB, f, 64);
-                cnt++;
-            }
-        }
-        uint4 v[TW][2];
-        uint64_t C[TW][2];
-#pragma unroll
-        for (uint32_t j = 0; j < TW; j++)
-#pragma unroll
-            for (uint32_t rr = 0; rr < 2; rr++) {
-                C[j][rr] = (A[j] & ~15ull) + 16ull * (lane + 64u * rr);
-                v[j][rr] = (C[j][rr] < B[j]) ? load16<true>(reinterpret_cast<const void*>(C[j][rr]))
-                                             : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-        for (uint32_t j = 0; j < TW; j++) {
-            uint32_t s = 0;
-#pragma unroll
-            for (uint32_t rr = 0; rr < 2; rr++) {
-                const uint64_t c = C[j][rr];
-                if (c < B[j] && c + 16u > A[j]) {
-                    if (c >= A[j] && c + 16u <= B[j]) {
-                        s += halves(v[j][rr].x) + halves(v[j][rr].y) + halves(v[j][rr].z) + halves(v[j][rr].w);
-                    } else {
-                        if (c + 0 < B[j]) s += halves(v[j][rr].x & range_mask(c + 0, A[j], B[j]));
-                        if (c + 4 < B[j]) s += halves(v[j][rr].y & range_mask(c + 4, A[j], B[j]));
-                        if (c + 8 < B[j]) s += halves(v[j][rr].z & range_mask(c + 8, A[j], B[j]));
-                        if (c + 12 < B[j]) s += halves(v[j][rr].w & range_mask(c + 12, A[j], B[j]));
-                    }
-                }
-            }
-            // tails longer than 2 KB: rest of the frame, same lane pattern
-            for (uint64_t c = (A[j] & ~15ull) + 16ull * (lane + 128u); c < B[j]; c += 1024u) {
-                const uint4 w = load16<true>(reinterpret_cast<const void*>(c));
-                if (c + 16u <= B[j]) s += halves(w.x) + halves(w.y) + halves(w.z) + halves(w.w);
-                else {
-                    if (c + 0 < B[j]) s += halves(w.x & range_mask(c + 0, A[j], B[j]));
-                    if (c + 4 < B[j]) s += halves(w.y & range_mask(c + 4, A[j], B[j]));
-                    if (c + 8 < B[j]) s += halves(w.z & range_mask(c + 8, A[j], B[j]));
-                    if (c + 12 < B[j]) s += halves(w.w & range_mask(c + 12, A[j], B[j]));
-                }
-            }
-            s = wave_sum64(s);
-            if (lane == fl[j]) mine = s;
-        }
-        (void)cnt;
-    }
-    if (have) *handoff_slot<OUT>(a.out, idx) = mine;
-}
-
 // Pass 2: one lane per frame. The first 80 bytes are loaded straight into
 // registers (six aligned 16-B loads, dword realignment by selects) and the
 // six canonical IMIX shapes finish in fast_canonical80 with the pass-1 tail
@@ -1206,12 +383,12 @@ namespace nexg {
 // registers and finished by fast_canonical80; anything it declines is parsed
 // by the generic core straight from HBM (L2-hot: the workgroup just read it).
 
-__device__ __forceinline__ uint32_t chunk_le_sum(const uint4& v) {
+NEXG_HD uint32_t chunk_le_sum(const uint4& v) {
     return halves_acc(v.w, halves_acc(v.z, halves_acc(v.y, halves_acc(v.x, 0u))));
 }
 
 // LE halfword sum of the first m (< 16) bytes of the 16-B LDS chunk at c
-__device__ __forceinline__ uint32_t chunk_prefix_sum(const uint8_t* c, uint32_t m) {
+NEXG_HD uint32_t chunk_prefix_sum(const uint8_t* c, uint32_t m) {
     const uint4 v = *reinterpret_cast<const uint4*>(c);
     auto msk = [&](uint32_t d) {  // bytes [4d, m) of dword d
         return m >= 4u * d + 4u ? 0xFFFFFFFFu : (m <= 4u * d ? 0u : ((1u << (8u * (m - 4u * d))) - 1u));

@@ -714,7 +714,13 @@ static void* batch_worker(void* arg) {
         uint64_t off, len;
         frame_extent(j->fr, i, &off, &len);
         nexg_record r;
-        nexo_parse_frame(j->fr->data + off, (size_t)len, j->flags, j->ip_offset, &r);
+        if (len > 65535u || off > j->fr->data_bytes || len > j->fr->data_bytes - off) {
+            /* include/nexg.h NEXG_ERR_BAD_EXTENT: the batch layout names no Frame */
+            memset(&r, 0, sizeof(r));
+            r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
+        } else {
+            nexo_parse_frame(j->fr->data + off, (size_t)len, j->flags, j->ip_offset, &r);
+        }
         if (j->recs) j->recs[i] = r;
         if (j->descs) nexo_record_to_desc(&r, &j->descs[i]);
     }

@@ -40,19 +40,29 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                     nexg::WinFrame f{slot, g, o, wlen};
                     nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
                 }
-            } else if (use_fast == 3) {  // StreamFrame: window = PITCH - o bytes, whole-frame sum given
-                const uint32_t pitch = window + 16;
-                const uint32_t wl = len < pitch - o ? (uint32_t)len : pitch - o;
-                memcpy(slot + o, g, wl);
-                const uint64_t base = reinterpret_cast<uint64_t>(g);
-                nexg::StreamFrame f{slot, g, o, wl, (uint32_t)len, nexg::global_le_sum(base, base + len)};
-                nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
-            } else if (use_fast == 2) {  // TileFrame: deferred tail summed separately (k_parse_coop)
-                nexg::TileFrame f{slot, g, o, wlen};
-                nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
-                if (f.dstate == 3) {
-                    const uint64_t base = reinterpret_cast<uint64_t>(g);
-                    f.complete(nexg::global_le_sum(base + f.ta, base + f.tb), r);
+            } else if (use_fast == 5 && (reinterpret_cast<uint64_t>(g) & 3u) == 0) {
+                // k_parse_span's arithmetic: the frame re-staged at its own
+                // address mod 16 in 16-B chunks; tail sum = Q(end) - Q(80) from
+                // running chunk sums + chunk_prefix_sum, in wrapping u32
+                alignas(16) static uint8_t span[65536 + 64];
+                memset(span, 0, sizeof(span));
+                memcpy(span + o, g, len);
+                auto Q = [&](uint32_t p) {  // prefix at span position p
+                    uint32_t q = 0xDEADBEEFu;  // arbitrary running base: only differences matter
+                    for (uint32_t c = 0; c < p / 16u; c++) {
+                        uint4 v;
+                        memcpy(&v, span + 16u * c, 16);
+                        q += nexg::chunk_le_sum(v);
+                    }
+                    const uint32_t m = p & 15u;
+                    return q + (m ? nexg::chunk_prefix_sum(span + (p & ~15u), m) : 0u);
+                };
+                uint32_t w80[20] = {0};
+                memcpy(w80, g, len < 80 ? len : 80);
+                const uint32_t tail = len > 80 ? Q(o + (uint32_t)len) - Q(o + 80u) : 0u;
+                if (!nexg::fast_canonical80(w80, (uint32_t)len, flags, tail, r)) {
+                    nexg::WinFrame f{slot, g, o, wlen};
+                    nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
                 }
             } else {
                 nexg::WinFrame f{slot, g, o, wlen};

@@ -184,3 +184,15 @@ def test_generator_imix_properties(oracle):
     f = recs["flags"]
     assert (f & abi.C_L4_CHECKED).all()
     assert ((f & abi.L_IPV6) != 0).mean() > 0.3 and ((f & abi.L_TCP) != 0).mean() > 0.2
+
+
+def test_oracle_batch_bad_extent(oracle):
+    """nexg.h NEXG_ERR_BAD_EXTENT: a frame longer than 65535 B or reaching past
+    data_bytes is reported, not parsed (the GPU kernels do the same)."""
+    data = np.zeros(70100, np.uint8)
+    offs = np.array([0, 64, 64 + 70000, 70100], np.uint64)
+    recs = oracle.parse_packed(data, offs, None)
+    st = list(abi.status_of(recs["flags"]))
+    assert st[1] == abi.ERR_BAD_EXTENT and st[0] != abi.ERR_BAD_EXTENT and st[2] != abi.ERR_BAD_EXTENT
+    recs = oracle.parse_packed(data[:100], np.array([0, 64], np.uint64), np.array([64, 40], np.uint32))
+    assert abi.status_of(recs["flags"])[1] == abi.ERR_BAD_EXTENT
