@@ -225,6 +225,34 @@ typedef struct nexg_udp4_build {
 int nexg_build_udp4_batch(nexg_ctx* ctx, const nexg_udp4_build* params,
                           uint8_t* out, uint32_t out_stride, void* stream);
 
+/* ---- udp_ping IPv6 branch (examples/udp_ping.rs:83-89) ---------------------
+ * UdpPacketBuilder::build over IPv6 (builder/udp.rs:67-95; checksum =
+ * udp::ipv6_checksum, udp.rs:480-505) -> Ipv6PacketBuilder::to_bytes
+ * (builder/ipv6.rs:89-152; Ipv6Packet::to_bytes ipv6.rs:50-75) ->
+ * EthernetPacketBuilder (EtherType 0x86DD). Frame = 62 + payload_len bytes. */
+typedef struct nexg_udp6_build {
+    const uint8_t* src_ip;    /* 16 bytes per frame, network order            */
+    const uint8_t* dst_ip;    /* 16 bytes per frame                           */
+    const uint16_t* src_port; /* per frame, or NULL -> def_src_port           */
+    const uint16_t* dst_port; /* per frame, or NULL -> def_dst_port           */
+    const uint8_t* src_mac;   /* 6 bytes per frame, or NULL -> def_src_mac    */
+    const uint8_t* dst_mac;   /* 6 bytes per frame, or NULL -> def_dst_mac    */
+    const uint8_t* payload;   /* UDP payload shared by all frames (may be NULL) */
+    uint32_t payload_len;
+    uint32_t flow_label;      /* low 20 bits (Ipv6PacketBuilder::flow_label masks) */
+    uint16_t def_src_port, def_dst_port;
+    uint8_t def_src_mac[6], def_dst_mac[6];
+    uint8_t hop_limit;        /* Ipv6PacketBuilder default 64 (builder/ipv6.rs:33) */
+    uint8_t traffic_class;    /* builder default 0                            */
+    uint8_t reserved[2];
+    uint64_t count;
+} nexg_udp6_build;
+
+/* Writes frame i (62 + payload_len bytes) at out + i*out_stride.
+ * NEXG_ERANGE if 8 + payload_len > 65535 (builder/udp.rs:83, builder/ipv6.rs:137). */
+int nexg_build_udp6_batch(nexg_ctx* ctx, const nexg_udp6_build* params,
+                          uint8_t* out, uint32_t out_stride, void* stream);
+
 /* ---- synthetic workloads --------------------------
  * Frame i of a workload depends only on (seed, first_index + i), so shards
  * regenerate identically on any GPU count. */

@@ -115,9 +115,32 @@ class Udp4Build(ctypes.Structure):
     ]
 
 
+class Udp6Build(ctypes.Structure):
+    """struct nexg_udp6_build"""
+    _fields_ = [
+        ("src_ip", ctypes.c_void_p),
+        ("dst_ip", ctypes.c_void_p),
+        ("src_port", ctypes.c_void_p),
+        ("dst_port", ctypes.c_void_p),
+        ("src_mac", ctypes.c_void_p),
+        ("dst_mac", ctypes.c_void_p),
+        ("payload", ctypes.c_void_p),
+        ("payload_len", ctypes.c_uint32),
+        ("flow_label", ctypes.c_uint32),
+        ("def_src_port", ctypes.c_uint16),
+        ("def_dst_port", ctypes.c_uint16),
+        ("def_src_mac", ctypes.c_uint8 * 6),
+        ("def_dst_mac", ctypes.c_uint8 * 6),
+        ("hop_limit", ctypes.c_uint8),
+        ("traffic_class", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 2),
+        ("count", ctypes.c_uint64),
+    ]
+
+
 #: every symbol include/nexg.h declares (tests check the .so exports them)
 EXPORTED_SYMBOLS = (
     "nexg_abi_version", "nexg_strerror", "nexg_ctx_create", "nexg_ctx_destroy",
     "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch",
-    "nexg_build_udp4_batch", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
+    "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
 )

@@ -136,6 +136,22 @@ int nexg_build_udp4_batch(nexg_ctx* ctx, const nexg_udp4_build* p, uint8_t* out,
                       NEXG_ELAUNCH);
 }
 
+int nexg_build_udp6_batch(nexg_ctx* ctx, const nexg_udp6_build* p, uint8_t* out,
+                          uint32_t out_stride, void* stream) {
+    if (!ctx || !p) return NEXG_EINVAL;
+    if (8ull + p->payload_len > 65535ull)
+        return fail(ctx, NEXG_ERANGE, "UDP/IPv6 length overflow%s", nullptr);
+    if (p->count && (!p->src_ip || !p->dst_ip || !out))
+        return fail(ctx, NEXG_EINVAL, "NULL address array or output%s", nullptr);
+    if (((reinterpret_cast<uint64_t>(p->src_ip) | reinterpret_cast<uint64_t>(p->dst_ip)) & 3u) != 0)
+        return fail(ctx, NEXG_EINVAL, "address arrays must be 4-B aligned%s", nullptr);
+    if (p->payload_len && !p->payload) return fail(ctx, NEXG_EINVAL, "NULL payload%s", nullptr);
+    if (out_stride < 62u + p->payload_len)
+        return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    return hip_status(ctx, nexg::launch_build_udp6(*p, out, out_stride, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
 int nexg_gen_lengths(nexg_ctx* ctx, int workload, uint64_t seed, uint64_t first_index,
                      uint64_t count, uint32_t* lengths, void* stream) {
     if (!ctx) return NEXG_EINVAL;

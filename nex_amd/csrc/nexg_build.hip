@@ -50,6 +50,34 @@ struct BuildArgs {
     uint32_t out_stride;
 };
 
+// Frame header given as NH (odd) little-endian halfwords of its bytes, written
+// to LDS at an even offset d0: (NH-1)/2 dword writes + 1 halfword write, the
+// dword run shifted by one halfword when d0 = 2 mod 4.
+template <int NH>
+__device__ __forceinline__ void lds_put_halfwords(uint8_t* smem, uint32_t d0, const uint32_t (&hw)[NH]) {
+    static_assert(NH % 2 == 1, "odd halfword count");
+    const bool al = (d0 & 2u) == 0;
+    const uint32_t b32 = al ? d0 : d0 + 2u;
+#pragma unroll
+    for (int m = 0; m < NH / 2; m++) {
+        const uint32_t v = al ? (hw[2 * m] | (hw[2 * m + 1] << 16)) : (hw[2 * m + 1] | (hw[2 * m + 2] << 16));
+        *reinterpret_cast<uint32_t*>(smem + b32 + 4u * m) = v;
+    }
+    *reinterpret_cast<uint16_t*>(smem + (al ? d0 + 2u * (NH - 1) : d0)) = (uint16_t)(al ? hw[NH - 1] : hw[0]);
+}
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }
+
+// tile copy-out shared by the builders: nf frames of `stride` bytes staged
+// contiguously in LDS leave as 16-B stores (+ byte tail of a partial tile)
+__device__ __forceinline__ void build_copy_out(const uint8_t* smem, uint8_t* T, uint32_t bytes) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t c = tid; c < bytes / 16u; c += kBuildTile)
+        reinterpret_cast<uint4*>(T)[c] = reinterpret_cast<const uint4*>(smem)[c];
+    const uint32_t tail = bytes & ~15u;
+    if (tid < bytes - tail) T[tail + tid] = smem[tail + tid];
+}
+
 template <bool STAGED>
 __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * kBuildMaxStride : 16];
@@ -96,9 +124,17 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
         h[38] = (uint8_t)(ulen >> 8); h[39] = (uint8_t)ulen;
         h[40] = (uint8_t)(ucs >> 8); h[41] = (uint8_t)ucs;
         if (STAGED) {
-            uint8_t* d = smem + tid * a.out_stride;
+            const uint32_t d0 = tid * a.out_stride;
+            uint8_t* d = smem + d0;
+            if ((a.out_stride & 1u) == 0) {  // even stride: frame starts are 2-B aligned
+                uint32_t hw[21];
 #pragma unroll
-            for (int k = 0; k < 42; k++) d[k] = h[k];
+                for (int k = 0; k < 21; k++) hw[k] = (uint32_t)h[2 * k] | ((uint32_t)h[2 * k + 1] << 8);
+                lds_put_halfwords<21>(smem, d0, hw);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 42; k++) d[k] = h[k];
+            }
             for (uint32_t k = 0; k < p.payload_len; k++) d[42 + k] = p.payload[k];
             for (uint32_t k = flen; k < a.out_stride; k++) d[k] = 0;
         } else {
@@ -110,13 +146,93 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     }
     if (STAGED) {
         __syncthreads();
-        const uint32_t bytes = nf * a.out_stride;
-        uint8_t* T = a.out + first * a.out_stride;
-        for (uint32_t c = tid; c < bytes / 16u; c += kBuildTile)
-            reinterpret_cast<uint4*>(T)[c] = reinterpret_cast<const uint4*>(smem)[c];
-        // tail of the last, partial tile (caller allocates count * out_stride)
-        const uint32_t tail = bytes & ~15u;
-        if (tid < bytes - tail) T[tail + tid] = smem[tail + tid];
+        build_copy_out(smem, a.out + first * a.out_stride, nf * a.out_stride);
+    }
+}
+
+// ---- udp_ping IPv6 branch: builder/udp.rs:67-95 over IPv6 (udp.rs:480-505),
+// Ipv6PacketBuilder::to_bytes (builder/ipv6.rs:89-152, ipv6.rs:50-75),
+// EthernetPacketBuilder; 62 + payload_len bytes per frame.
+struct Build6Args {
+    nexg_udp6_build p;
+    uint8_t* out;
+    uint32_t out_stride;
+};
+
+template <bool STAGED>
+__global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * kBuildMaxStride : 16];
+    const nexg_udp6_build& p = a.p;
+    const uint64_t first = (uint64_t)blockIdx.x * kBuildTile;
+    const uint64_t left = p.count - first;
+    const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i = first + tid;
+    const uint32_t flen = 62u + p.payload_len;
+    if (tid < nf) {
+        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(p.src_ip + 16u * i);
+        const uint32_t* d4 = reinterpret_cast<const uint32_t*>(p.dst_ip + 16u * i);
+        uint32_t sw[4], dw[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) { sw[k] = s4[k]; dw[k] = d4[k]; }
+        const uint32_t sp = p.src_port ? p.src_port[i] : p.def_src_port;
+        const uint32_t dp = p.dst_port ? p.dst_port[i] : p.def_dst_port;
+        const uint32_t ulen = 8u + p.payload_len;
+        uint64_t pw = 0;  // BE word sum of the shared payload (UDP offset 8 is even)
+        for (uint32_t k = 0; k < p.payload_len; k += 2)
+            pw += ((uint32_t)p.payload[k] << 8) | (k + 1 < p.payload_len ? (uint32_t)p.payload[k + 1] : 0u);
+        // util.rs:111-133 pseudo-header: address segments (as LE halves x 256),
+        // next header 17, length; then sport, dport, length, payload (skipword 3)
+        uint32_t addr_le = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) addr_le += halves(sw[k]) + halves(dw[k]);
+        const uint32_t ucs = fold_complement(256ull * addr_le + 17u + ulen + sp + dp + ulen + pw);
+        const uint32_t fl = p.flow_label & 0xFFFFFu, tc = p.traffic_class;
+        uint32_t hw[31];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const uint32_t b0 = p.dst_mac ? p.dst_mac[i * 6 + 2 * k] : p.def_dst_mac[2 * k];
+            const uint32_t b1 = p.dst_mac ? p.dst_mac[i * 6 + 2 * k + 1] : p.def_dst_mac[2 * k + 1];
+            const uint32_t c0 = p.src_mac ? p.src_mac[i * 6 + 2 * k] : p.def_src_mac[2 * k];
+            const uint32_t c1 = p.src_mac ? p.src_mac[i * 6 + 2 * k + 1] : p.def_src_mac[2 * k + 1];
+            hw[k] = b0 | (b1 << 8);
+            hw[3 + k] = c0 | (c1 << 8);
+        }
+        hw[6] = 0xDD86u;                                              // EtherType 0x86DD
+        hw[7] = ((6u << 4) | (tc >> 4)) | ((((tc & 0xFu) << 4) | (fl >> 16)) << 8);
+        hw[8] = ((fl >> 8) & 0xFFu) | ((fl & 0xFFu) << 8);
+        hw[9] = bswap16(ulen);                                        // payload length
+        hw[10] = 17u | ((uint32_t)p.hop_limit << 8);                  // next header, hop limit
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            hw[11 + 2 * k] = sw[k] & 0xFFFFu; hw[12 + 2 * k] = sw[k] >> 16;
+            hw[19 + 2 * k] = dw[k] & 0xFFFFu; hw[20 + 2 * k] = dw[k] >> 16;
+        }
+        hw[27] = bswap16(sp);
+        hw[28] = bswap16(dp);
+        hw[29] = bswap16(ulen);
+        hw[30] = bswap16(ucs);  // computed 0 stays 0 (Q18)
+        if (STAGED) {
+            const uint32_t d0 = tid * a.out_stride;
+            uint8_t* d = smem + d0;
+            if ((a.out_stride & 1u) == 0) {
+                lds_put_halfwords<31>(smem, d0, hw);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 31; k++) { d[2 * k] = (uint8_t)hw[k]; d[2 * k + 1] = (uint8_t)(hw[k] >> 8); }
+            }
+            for (uint32_t k = 0; k < p.payload_len; k++) d[62 + k] = p.payload[k];
+            for (uint32_t k = flen; k < a.out_stride; k++) d[k] = 0;
+        } else {
+            uint8_t* d = a.out + i * (uint64_t)a.out_stride;
+#pragma unroll
+            for (int k = 0; k < 31; k++) { d[2 * k] = (uint8_t)hw[k]; d[2 * k + 1] = (uint8_t)(hw[k] >> 8); }
+            for (uint32_t k = 0; k < p.payload_len; k++) d[62 + k] = p.payload[k];
+        }
+    }
+    if (STAGED) {
+        __syncthreads();
+        build_copy_out(smem, a.out + first * a.out_stride, nf * a.out_stride);
     }
 }
 
@@ -270,6 +386,19 @@ hipError_t launch_build_udp4(const nexg_udp4_build& p, uint8_t* out, uint32_t ou
         hipLaunchKernelGGL(k_build_udp4<true>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     else
         hipLaunchKernelGGL(k_build_udp4<false>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_udp6(const nexg_udp6_build& p, uint8_t* out, uint32_t out_stride,
+                             hipStream_t s) {
+    if (p.count == 0) return hipSuccess;
+    Build6Args a{p, out, out_stride};
+    const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
+    const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
+    if (staged)
+        hipLaunchKernelGGL(k_build_udp6<true>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_build_udp6<false>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     return hipGetLastError();
 }
 

@@ -218,6 +218,35 @@ class Engine:
                                                    self._stream(stream)))
         return out
 
+    def build_udp6(self, src_ip, dst_ip, src_port=None, dst_port=None, def_src_port=0,
+                   def_dst_port=0, src_mac=b"\0" * 6, dst_mac=b"\0" * 6, hop_limit=64,
+                   traffic_class=0, flow_label=0, payload=None, out_stride=None, out=None,
+                   stream=None):
+        """udp_ping's IPv6 branch (udp_ping.rs:83-89): UdpPacketBuilder ->
+        Ipv6PacketBuilder -> EthernetPacketBuilder on every tuple. src_ip /
+        dst_ip are (count, 16) uint8 device tensors in network order."""
+        torch = _torch()
+        count = src_ip.shape[0] if src_ip.dim() > 1 else src_ip.numel() // 16
+        plen = 0 if payload is None else payload.numel()
+        stride = out_stride or (62 + plen)
+        if out is None:
+            out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
+        p = abi.Udp6Build()
+        p.src_ip, p.dst_ip = src_ip.data_ptr(), dst_ip.data_ptr()
+        p.src_port = None if src_port is None else src_port.data_ptr()
+        p.dst_port = None if dst_port is None else dst_port.data_ptr()
+        p.src_mac = p.dst_mac = None
+        p.payload = None if payload is None else payload.data_ptr()
+        p.payload_len = plen
+        p.flow_label = flow_label
+        p.def_src_port, p.def_dst_port = def_src_port, def_dst_port
+        p.def_src_mac[:] = list(src_mac)
+        p.def_dst_mac[:] = list(dst_mac)
+        p.hop_limit, p.traffic_class, p.count = hop_limit, traffic_class, count
+        self._check(self.lib.nexg_build_udp6_batch(self.ctx, ctypes.byref(p), _ptr(out), stride,
+                                                   self._stream(stream)))
+        return out
+
     # --- synthetic workloads ----------------------------------------------
     def gen_batch(self, workload: int, count: int, seed: int = abi.DEFAULT_SEED,
                   first_index: int = 0, stream=None) -> FrameBatch:

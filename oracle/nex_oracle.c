@@ -805,6 +805,45 @@ int nexo_build_udp4(const uint8_t src_mac[6], const uint8_t dst_mac[6],
     return (int)(14 + n);
 }
 
+/* builder/udp.rs:67-95 (IPv6 pseudo-header, udp.rs:480-505) + builder/ipv6.rs:
+ * 89-152 (payload_length = payload, LengthOverflow > 65535) + Ipv6Packet::
+ * to_bytes (ipv6.rs:50-75) + builder/ethernet.rs:63-70, composed as
+ * examples/udp_ping.rs:68-109 (IPv6 branch, :83-89). */
+int nexo_build_udp6(const uint8_t src_mac[6], const uint8_t dst_mac[6],
+                    const uint8_t src_ip[16], const uint8_t dst_ip[16], uint16_t sport,
+                    uint16_t dport, uint8_t hop_limit, uint8_t traffic_class,
+                    uint32_t flow_label, const uint8_t* payload, uint32_t payload_len,
+                    uint8_t* out) {
+    size_t udp_len = 8 + (size_t)payload_len;
+    if (udp_len > 65535) return -1;
+    uint8_t* udp = out + 54;
+    put16(udp, sport);
+    put16(udp + 2, dport);
+    put16(udp + 4, (uint16_t)udp_len);
+    put16(udp + 6, 0);
+    if (payload_len) memcpy(udp + 8, payload, payload_len);
+    uint16_t ucs = nexo_ipv6_checksum(udp, udp_len, 3, NULL, 0, src_ip, dst_ip, PROTO_UDP);
+    put16(udp + 6, ucs); /* computed 0 stays 0 (Q18) */
+    /* Ipv6Packet::to_bytes: version/traffic class/flow label, payload length,
+     * next header value(), hop limit, addresses */
+    uint32_t fl = flow_label & 0xFFFFFu; /* Ipv6PacketBuilder::flow_label masks */
+    uint8_t* ip = out + 14;
+    ip[0] = (uint8_t)((6u << 4) | (traffic_class >> 4));
+    ip[1] = (uint8_t)(((traffic_class & 0x0Fu) << 4) | (uint8_t)(fl >> 16));
+    ip[2] = (uint8_t)(fl >> 8);
+    ip[3] = (uint8_t)fl;
+    put16(ip + 4, (uint16_t)udp_len);
+    ip[6] = PROTO_UDP;
+    ip[7] = hop_limit;
+    memcpy(ip + 8, src_ip, 16);
+    memcpy(ip + 24, dst_ip, 16);
+    memcpy(out, dst_mac, 6);
+    memcpy(out + 6, src_mac, 6);
+    out[12] = 0x86;
+    out[13] = 0xDD;
+    return (int)(54 + udp_len);
+}
+
 /* ======================= synthetic workloads =========================== */
 
 #define PHI 0x9E3779B97F4A7C15ULL

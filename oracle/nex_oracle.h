@@ -67,6 +67,11 @@ int nexo_build_udp4(const uint8_t src_mac[6], const uint8_t dst_mac[6],
                     uint16_t dport, uint16_t ip_id, uint8_t ttl,
                     uint8_t ip_flags, uint8_t dscp_ecn, const uint8_t* payload,
                     uint32_t payload_len, uint8_t* out);
+int nexo_build_udp6(const uint8_t src_mac[6], const uint8_t dst_mac[6],
+                    const uint8_t src_ip[16], const uint8_t dst_ip[16], uint16_t sport,
+                    uint16_t dport, uint8_t hop_limit, uint8_t traffic_class,
+                    uint32_t flow_label, const uint8_t* payload, uint32_t payload_len,
+                    uint8_t* out);
 
 /* Synthetic workloads, independent CPU implementation
  * of the generator the engine ships (nexg_gen_*). */

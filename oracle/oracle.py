@@ -47,6 +47,9 @@ def lib():
         L.nexo_build_udp4.restype = I
         L.nexo_build_udp4.argtypes = [P, P, U32, U32, U16, U16, U16, ctypes.c_uint8, ctypes.c_uint8,
                                       ctypes.c_uint8, P, U32, P]
+        L.nexo_build_udp6.restype = I
+        L.nexo_build_udp6.argtypes = [P, P, P, P, U16, U16, ctypes.c_uint8, ctypes.c_uint8, U32, P,
+                                      U32, P]
         L.nexo_gen_length.restype = U32
         L.nexo_gen_length.argtypes = [I, U64, U64]
         L.nexo_gen_frame.restype = None
@@ -122,6 +125,18 @@ def build_udp4(src_mac, dst_mac, src_ip, dst_ip, sport, dport, ip_id=0, ttl=64, 
     pb, pn = _buf(payload)
     n = lib().nexo_build_udp4(bytes(src_mac), bytes(dst_mac), src_ip, dst_ip, sport, dport, ip_id,
                               ttl, ip_flags, dscp_ecn, pb, pn, out)
+    if n < 0:
+        raise ValueError("BuildError::LengthOverflow")
+    return out.raw[:n]
+
+
+def build_udp6(src_mac, dst_mac, src_ip: bytes, dst_ip: bytes, sport, dport, hop_limit=64,
+               traffic_class=0, flow_label=0, payload=b""):
+    """udp_ping IPv6 branch (examples/udp_ping.rs:83-89): Eth/IPv6/UDP bytes."""
+    out = ctypes.create_string_buffer(62 + len(payload) + 64)
+    pb, pn = _buf(payload)
+    n = lib().nexo_build_udp6(bytes(src_mac), bytes(dst_mac), bytes(src_ip), bytes(dst_ip), sport,
+                              dport, hop_limit, traffic_class, flow_label, pb, pn, out)
     if n < 0:
         raise ValueError("BuildError::LengthOverflow")
     return out.raw[:n]

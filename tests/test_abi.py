@@ -70,6 +70,21 @@ def test_struct_layouts_match_c(tmp_path):
     assert boffs == [getattr(abi.Udp4Build, f).offset for f, _ in abi.Udp4Build._fields_]
 
 
+def test_udp6_build_layout_matches_c(tmp_path):
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', 'int main(void){',
+             'printf("%zu\\n", sizeof(nexg_udp6_build));']
+    for f, _ in abi.Udp6Build._fields_:
+        lines.append(f'printf("%zu\\n", offsetof(nexg_udp6_build, {f}));')
+    lines.append("return 0;}")
+    src = tmp_path / "probe6.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe6"
+    subprocess.check_call(["gcc", "-std=c11", "-o", str(exe), str(src)])
+    out = list(map(int, subprocess.check_output([str(exe)], text=True).split()))
+    assert out[0] == ctypes.sizeof(abi.Udp6Build)
+    assert out[1:] == [getattr(abi.Udp6Build, f).offset for f, _ in abi.Udp6Build._fields_]
+
+
 def test_engine_refuses_without_library(monkeypatch, tmp_path):
     """The product path fails loudly when the HIP library is missing."""
     from nex_amd import _lib

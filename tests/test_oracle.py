@@ -196,3 +196,40 @@ def test_oracle_batch_bad_extent(oracle):
     assert st[1] == abi.ERR_BAD_EXTENT and st[0] != abi.ERR_BAD_EXTENT and st[2] != abi.ERR_BAD_EXTENT
     recs = oracle.parse_packed(data[:100], np.array([0, 64], np.uint64), np.array([64, 40], np.uint32))
     assert abi.status_of(recs["flags"])[1] == abi.ERR_BAD_EXTENT
+
+
+def _ones_complement(words):
+    s = sum(words)
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return (~s) & 0xFFFF
+
+
+def test_udp_ping_ipv6_build_kat(oracle):
+    """udp_ping's IPv6 branch (udp_ping.rs:83-89): layout per Ipv6Packet::to_bytes
+    (ipv6.rs:50-75) and a checksum recomputed here with a plain RFC 1071 sum
+    over the IPv6 pseudo-header (util.rs:111-133); the oracle parser then
+    verifies it (l4_ok)."""
+    import ipaddress
+    src = ipaddress.IPv6Address("2001:db8::1").packed
+    dst = ipaddress.IPv6Address("2606:4700:4700::1111").packed
+    for payload in (b"", b"\x01", b"ping!", bytes(range(200))):
+        f = oracle.build_udp6(b"\x02" * 6, b"\x04" * 6, src, dst, 53443, 33435,
+                              hop_limit=64, traffic_class=0xA5, flow_label=0x12345, payload=payload)
+        ulen = 8 + len(payload)
+        assert len(f) == 62 + len(payload)
+        assert f[12:14] == b"\x86\xdd"
+        assert f[14:18] == bytes([0x6A, 0x51, 0x23, 0x45])      # version 6, tc 0xA5, flow 0x12345
+        assert f[18:20] == ulen.to_bytes(2, "big") and f[20] == 17 and f[21] == 64
+        assert f[22:38] == src and f[38:54] == dst
+        assert f[54:58] == (53443).to_bytes(2, "big") + (33435).to_bytes(2, "big")
+        seg = f[54:] + (b"\0" if len(f[54:]) % 2 else b"")
+        words = [int.from_bytes(src[i:i + 2], "big") for i in range(0, 16, 2)]
+        words += [int.from_bytes(dst[i:i + 2], "big") for i in range(0, 16, 2)]
+        words += [17, ulen]
+        words += [int.from_bytes(seg[i:i + 2], "big") for i in range(0, len(seg), 2) if i != 6]
+        assert int.from_bytes(f[60:62], "big") == _ones_complement(words)
+        r = oracle.parse_frame(f)
+        assert r["flags"] & abi.C_L4_OK and r["payload_len"] == len(payload)
+    with pytest.raises(ValueError):
+        oracle.build_udp6(b"\0" * 6, b"\0" * 6, src, dst, 1, 2, payload=bytes(65528))
