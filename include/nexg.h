@@ -153,6 +153,32 @@ typedef struct nexg_record {
 
 #define NEXG_OUT_DESC 1
 #define NEXG_OUT_RECORD 2
+#define NEXG_OUT_SLICE 3
+
+/* FrameSlice::try_from_buf (frame.rs:84-287) per frame, out_kind
+ * NEXG_OUT_SLICE, 16 bytes: layer boundaries only, no checksums. FrameSlice
+ * has no ParseMode (NEXG_PARSE_STRICT is ignored) and reports every inner
+ * failure as an error; its walk differs from Frame's (AH is walked, ICMP
+ * needs 4 B, UDP length is not checked). Ranges are frame-relative:
+ *   datalink  = [0, 14)                          if NEXG_S_DATALINK
+ *   network   = [l3_off, l3_off + l3_len)        if NEXG_S_NETWORK
+ *   transport = [l3_off + l3_len, + l4_len)      if NEXG_S_TRANSPORT
+ *   payload   = [payload_off, payload_off + payload_len)  (on success)
+ * ethertype = EtherType::value(), ip_protocol (bits 8..15) =
+ * IpNextProtocol::value() (143..252 -> 255). Status bits 24..26 as for
+ * Frame: BufferTooShort / InvalidLength / Malformed / Truncated / BAD_EXTENT. */
+#define NEXG_S_DATALINK (1u << 0)
+#define NEXG_S_NETWORK (1u << 1)
+#define NEXG_S_TRANSPORT (1u << 2)
+#define NEXG_S_ETHERTYPE (1u << 3)
+#define NEXG_S_IP_PROTOCOL (1u << 4)
+#define NEXG_S_PROTO_SHIFT 8
+typedef struct nexg_slice {
+    uint32_t flags;
+    uint16_t l3_off, l3_len, l4_len;
+    uint16_t payload_off, payload_len;
+    uint16_t ethertype;
+} nexg_slice;
 
 /* ---- frame batch layout ------------------------------------------------
  * Frame i occupies data[off(i), off(i)+len(i)):
@@ -191,7 +217,8 @@ int nexg_ctx_cu_count(const nexg_ctx* ctx);
 /* ---- hot path ----------------------------------------------------------
  * Frame::try_from_buf_with_mode on every frame + checksum verification.
  * out_kind NEXG_OUT_DESC   -> out is nexg_desc[count]
- * out_kind NEXG_OUT_RECORD -> out is nexg_record[count] */
+ * out_kind NEXG_OUT_RECORD -> out is nexg_record[count]
+ * out_kind NEXG_OUT_SLICE  -> out is nexg_slice[count] (FrameSlice, above) */
 int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames,
                      const nexg_parse_option* option, int out_kind, void* out,
                      void* stream);

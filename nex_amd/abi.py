@@ -42,6 +42,15 @@ STATUS_SHIFT = 24
 
 OUT_DESC = 1
 OUT_RECORD = 2
+OUT_SLICE = 3
+
+# FrameSlice presence bits (nexg_slice.flags)
+S_DATALINK = 1 << 0
+S_NETWORK = 1 << 1
+S_TRANSPORT = 1 << 2
+S_ETHERTYPE = 1 << 3
+S_IP_PROTOCOL = 1 << 4
+S_PROTO_SHIFT = 8
 
 WL_UDP64 = 1
 WL_IMIX = 2
@@ -56,6 +65,10 @@ def status_of(flags):
 
 DESC_DTYPE = np.dtype([("flags", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2")])
 assert DESC_DTYPE.itemsize == 8
+
+SLICE_DTYPE = np.dtype([("flags", "<u4"), ("l3_off", "<u2"), ("l3_len", "<u2"), ("l4_len", "<u2"),
+                        ("payload_off", "<u2"), ("payload_len", "<u2"), ("ethertype", "<u2")])
+assert SLICE_DTYPE.itemsize == 16
 
 RECORD_DTYPE = np.dtype([
     ("flags", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"),

@@ -51,8 +51,24 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
     return hipGetLastError();
 }
 
+// FrameSlice output: header bytes only, staged exactly as the parse kernels
+// stage them (whole tile for small fixed strides, a 128-B lane window plus
+// HBM reads for deeper IPv6 extension chains otherwise).
+static hipError_t launch_slice(ParseVariant v, const ParseArgs& a, hipStream_t s) {
+    const uint64_t blocks = (a.count + kTile - 1) / kTile;
+    dim3 grid((uint32_t)blocks), block(kTile);
+    if (v == ParseVariant::TileStride64)
+        hipLaunchKernelGGL((k_parse<0, NEXG_OUT_SLICE, 64, 64, false, true>), grid, block, 0, s, a);
+    else if (v == ParseVariant::TileStride)
+        hipLaunchKernelGGL((k_parse<0, NEXG_OUT_SLICE, 0, 128>), grid, block, 0, s, a);
+    else
+        hipLaunchKernelGGL((k_parse<1, NEXG_OUT_SLICE, 0, 128>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
+    if (out_kind == NEXG_OUT_SLICE) return launch_slice(v, a, s);
     return out_kind == NEXG_OUT_DESC ? launch_parse_out<NEXG_OUT_DESC>(v, a, s)
                                      : launch_parse_out<NEXG_OUT_RECORD>(v, a, s);
 }

@@ -116,6 +116,20 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
     }
     // MODE 0 + RECORD: every thread stays for the coalesced copy-out
     constexpr bool kStaged = MODE == 0 && OUT == NEXG_OUT_RECORD && PITCH >= 64;
+    if constexpr (OUT == NEXG_OUT_SLICE) {  // FrameSlice boundaries from the same staging
+        if (tid < nf) {
+            nexg_slice sl;
+            if (bad) {
+                sl = nexg_slice{};
+                sl.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
+            } else {
+                WinFrame f{slot, g, o, wlen};
+                slice_frame(f, len, a.opt_flags, a.ip_offset, sl);
+            }
+            reinterpret_cast<nexg_slice*>(a.out)[idx] = sl;
+        }
+        return;
+    }
     nexg_record r;
     bool have = false;
     if (tid < nf) {

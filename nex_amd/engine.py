@@ -157,12 +157,13 @@ class Engine:
     def parse(self, batch: FrameBatch, option: ParseOption = ParseOption(),
               mode: ParseMode = ParseMode.Lenient, out_kind: int = abi.OUT_DESC,
               out=None, stream=None):
-        """Frame::try_from_buf_with_mode on every frame (frame.rs:309).
+        """Frame::try_from_buf_with_mode on every frame (frame.rs:309), or
+        FrameSlice::try_from_buf (frame.rs:86) with out_kind=OUT_SLICE.
 
-        Returns a uint8 device tensor holding nexg_desc[count] (8 B each) or
-        nexg_record[count] (64 B each); see `descs_to_numpy`."""
+        Returns a uint8 device tensor holding nexg_desc[count] (8 B each),
+        nexg_record[count] (64 B) or nexg_slice[count] (16 B)."""
         torch = _torch()
-        width = 8 if out_kind == abi.OUT_DESC else 64
+        width = {abi.OUT_DESC: 8, abi.OUT_RECORD: 64, abi.OUT_SLICE: 16}[out_kind]
         if out is None:
             out = torch.empty(max(batch.count, 1) * width, dtype=torch.uint8, device=self.torch_device)
         fr = batch.to_c()
@@ -175,7 +176,8 @@ class Engine:
                        out_kind=abi.OUT_RECORD):
         out = self.parse(batch, option, mode, out_kind)
         _torch().cuda.synchronize(self.torch_device)
-        dt = abi.RECORD_DTYPE if out_kind == abi.OUT_RECORD else abi.DESC_DTYPE
+        dt = {abi.OUT_DESC: abi.DESC_DTYPE, abi.OUT_RECORD: abi.RECORD_DTYPE,
+              abi.OUT_SLICE: abi.SLICE_DTYPE}[out_kind]
         return out.cpu().numpy()[: batch.count * dt.itemsize].view(dt)
 
     def checksum(self, batch: FrameBatch, skipword: int, stream=None):

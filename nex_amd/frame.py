@@ -309,3 +309,53 @@ def frame_view_payload(frame: bytes, payload_len: int, option: ParseOption = Par
     if payload_len > len(avail):
         return b""
     return bytes(avail[len(avail) - payload_len:])
+
+
+@dataclass
+class FrameView:  # frame.rs:345-379
+    """Frame's decoded layers with the payload borrowed from the input (Q27)."""
+    datalink: Optional[DatalinkLayer]
+    ip: Optional[IpLayer]
+    transport: Optional[TransportLayer]
+    payload: bytes
+    packet_len: int
+
+
+def frame_view_from_record(rec, frame: bytes, option: ParseOption = ParseOption()) -> FrameView:
+    """FrameView::try_from_buf (frame.rs:360-372) from a NEXG_OUT_RECORD record."""
+    f = frame_from_record(rec, frame)
+    return FrameView(f.datalink, f.ip, f.transport,
+                     frame_view_payload(frame, int(rec["payload_len"]), option), f.packet_len)
+
+
+@dataclass
+class FrameSlice:  # frame.rs:62-83
+    """Borrowed layer boundaries (as memoryviews of the input)."""
+    packet: memoryview
+    datalink: Optional[memoryview]
+    network: Optional[memoryview]
+    transport: Optional[memoryview]
+    payload: memoryview
+    ethertype: Optional[int]
+    ip_protocol: Optional[int]
+
+
+def frame_slice_from_record(s, frame) -> FrameSlice:
+    """FrameSlice::try_from_buf (frame.rs:84-136) from a NEXG_OUT_SLICE entry;
+    raises the ParseError kind the reference returns."""
+    flags = int(s["flags"])
+    status = (flags >> abi.STATUS_SHIFT) & 7
+    if status:
+        raise parse_error(status)
+    mv = memoryview(bytes(frame))
+    l3, l3n, l4n = int(s["l3_off"]), int(s["l3_len"]), int(s["l4_len"])
+    po, pn = int(s["payload_off"]), int(s["payload_len"])
+    return FrameSlice(
+        packet=mv,
+        datalink=mv[:14] if flags & abi.S_DATALINK else None,
+        network=mv[l3:l3 + l3n] if flags & abi.S_NETWORK else None,
+        transport=mv[l3 + l3n:l3 + l3n + l4n] if flags & abi.S_TRANSPORT else None,
+        payload=mv[po:po + pn],
+        ethertype=int(s["ethertype"]) if flags & abi.S_ETHERTYPE else None,
+        ip_protocol=(flags >> abi.S_PROTO_SHIFT) & 0xFF if flags & abi.S_IP_PROTOCOL else None,
+    )

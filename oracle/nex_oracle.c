@@ -748,6 +748,165 @@ int nexo_parse_batch(const nexg_frames* frames, uint32_t flags, uint32_t ip_offs
     return 0;
 }
 
+/* ======================= FrameSlice (frame.rs:84-287) =================== */
+
+typedef struct {
+    const uint8_t* packet;
+    int has_datalink, has_network, has_transport, has_proto;
+    const uint8_t* network; size_t network_len;
+    const uint8_t* transport; size_t transport_len;
+    const uint8_t* payload; size_t payload_len;
+    uint16_t ethertype;
+    uint8_t ip_protocol;
+} slice_view;
+
+/* frame.rs:237-286 parse_transport */
+static int slice_transport(slice_view* v, uint8_t protocol, const uint8_t* bytes, size_t len) {
+    size_t header_len;
+    if (protocol == PROTO_TCP) {
+        if (len < 20) { v->payload = bytes; v->payload_len = len; return 0; }
+        size_t length = (size_t)(bytes[12] >> 4) * 4;
+        if (length < 20 || length > len) return NEXG_ERR_INVALID_LENGTH;
+        header_len = length;
+    } else if (protocol == PROTO_UDP) {
+        if (len < 8) { v->payload = bytes; v->payload_len = len; return 0; }
+        header_len = 8;
+    } else if (protocol == PROTO_ICMP || protocol == PROTO_ICMPV6) {
+        if (len < 4) { v->payload = bytes; v->payload_len = len; return 0; }
+        header_len = 4;
+    } else {
+        v->payload = bytes; v->payload_len = len;
+        return 0;
+    }
+    v->has_transport = 1;
+    v->transport = bytes; v->transport_len = header_len;
+    v->payload = bytes + header_len; v->payload_len = len - header_len;
+    return 0;
+}
+
+/* frame.rs:138-175 parse_ipv4 */
+static int slice_ipv4(slice_view* v, const uint8_t* bytes, size_t len) {
+    if (len < 20) return NEXG_ERR_BUFFER_TOO_SHORT;
+    if (bytes[0] >> 4 != 4) return NEXG_ERR_MALFORMED;
+    size_t header_len = (size_t)(bytes[0] & 0x0f) * 4;
+    if (header_len < 20 || header_len > len) return NEXG_ERR_INVALID_LENGTH;
+    size_t declared = ((size_t)bytes[2] << 8) | bytes[3];
+    size_t packet_len = declared == 0 ? len : (declared < len ? declared : len);
+    if (packet_len < header_len) return NEXG_ERR_INVALID_LENGTH;
+    v->has_network = 1;
+    v->network = bytes; v->network_len = header_len;
+    uint8_t protocol = ip_next_protocol_value(bytes[9]);
+    v->has_proto = 1;
+    v->ip_protocol = protocol;
+    return slice_transport(v, protocol, bytes + header_len, packet_len - header_len);
+}
+
+/* frame.rs:177-235 parse_ipv6 (extension walk incl. AH) */
+static int slice_ipv6(slice_view* v, const uint8_t* bytes, size_t len) {
+    if (len < 40) return NEXG_ERR_BUFFER_TOO_SHORT;
+    if (bytes[0] >> 4 != 6) return NEXG_ERR_MALFORMED;
+    size_t declared_payload = ((size_t)bytes[4] << 8) | bytes[5];
+    size_t packet_len = 40 + declared_payload;
+    if (packet_len > len) packet_len = len;
+    uint8_t next = bytes[6];
+    size_t cursor = 40;
+    while (cursor < packet_len) {
+        size_t extension_len;
+        if (next == 0 || next == 43 || next == 60) {
+            if (cursor + 2 > packet_len) return NEXG_ERR_TRUNCATED;
+            extension_len = ((size_t)bytes[cursor + 1] + 1) * 8;
+        } else if (next == 44) {
+            extension_len = 8;
+        } else if (next == 51) {
+            if (cursor + 2 > packet_len) return NEXG_ERR_TRUNCATED;
+            extension_len = ((size_t)bytes[cursor + 1] + 2) * 4;
+        } else {
+            break;
+        }
+        size_t end = cursor + extension_len;
+        if (end > packet_len) return NEXG_ERR_TRUNCATED;
+        next = bytes[cursor];
+        cursor = end;
+    }
+    v->has_network = 1;
+    v->network = bytes; v->network_len = cursor;
+    uint8_t protocol = ip_next_protocol_value(next);
+    v->has_proto = 1;
+    v->ip_protocol = protocol;
+    return slice_transport(v, protocol, bytes + cursor, packet_len - cursor);
+}
+
+/* frame.rs:84-136 FrameSlice::try_from_buf */
+void nexo_slice_frame(const uint8_t* packet, size_t len, uint32_t flags, uint32_t ip_offset,
+                      nexg_slice* out) {
+    memset(out, 0, sizeof(*out));
+    slice_view v;
+    memset(&v, 0, sizeof(v));
+    v.packet = packet;
+    const uint8_t* network_bytes;
+    size_t network_len;
+    uint16_t ethertype;
+    int st = 0;
+    if (flags & NEXG_PARSE_FROM_IP) {
+        if (ip_offset > len) { st = NEXG_ERR_INVALID_LENGTH; goto done; }
+        network_bytes = packet + ip_offset;
+        network_len = len - ip_offset;
+        if (network_len >= 1 && network_bytes[0] >> 4 == 4) ethertype = 0x0800;
+        else if (network_len >= 1 && network_bytes[0] >> 4 == 6) ethertype = 0x86DD;
+        else { st = NEXG_ERR_MALFORMED; goto done; }
+    } else {
+        if (len < 14) { st = NEXG_ERR_BUFFER_TOO_SHORT; goto done; }
+        v.has_datalink = 1;
+        ethertype = (uint16_t)((packet[12] << 8) | packet[13]);
+        network_bytes = packet + 14;
+        network_len = len - 14;
+    }
+    v.payload = network_bytes;
+    v.payload_len = network_len;
+    v.ethertype = ethertype;
+    if (ethertype == 0x0800) st = slice_ipv4(&v, network_bytes, network_len);
+    else if (ethertype == 0x86DD) st = slice_ipv6(&v, network_bytes, network_len);
+    else if (ethertype == 0x0806 && network_len >= 28) {
+        v.has_network = 1;
+        v.network = network_bytes; v.network_len = 28;
+        v.payload = network_bytes + 28; v.payload_len = network_len - 28;
+    }
+done:
+    if (st) {
+        out->flags = (uint32_t)st << NEXG_STATUS_SHIFT;
+        return;
+    }
+    uint32_t f = NEXG_S_ETHERTYPE;
+    if (v.has_datalink) f |= NEXG_S_DATALINK;
+    if (v.has_network) {
+        f |= NEXG_S_NETWORK;
+        out->l3_off = (uint16_t)(v.network - packet);
+        out->l3_len = (uint16_t)v.network_len;
+    }
+    if (v.has_transport) {
+        f |= NEXG_S_TRANSPORT;
+        out->l4_len = (uint16_t)v.transport_len;
+    }
+    if (v.has_proto) f |= NEXG_S_IP_PROTOCOL | ((uint32_t)v.ip_protocol << NEXG_S_PROTO_SHIFT);
+    out->flags = f;
+    out->ethertype = v.ethertype;
+    out->payload_off = (uint16_t)(v.payload - packet);
+    out->payload_len = (uint16_t)v.payload_len;
+}
+
+void nexo_slice_batch(const nexg_frames* fr, uint32_t flags, uint32_t ip_offset, nexg_slice* out) {
+    for (uint64_t i = 0; i < fr->count; i++) {
+        uint64_t off, len;
+        frame_extent(fr, i, &off, &len);
+        if (len > 65535u || off > fr->data_bytes || len > fr->data_bytes - off) {
+            memset(&out[i], 0, sizeof(out[i]));
+            out[i].flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
+        } else {
+            nexo_slice_frame(fr->data + off, (size_t)len, flags, ip_offset, &out[i]);
+        }
+    }
+}
+
 /* ======================= builders ====================================== */
 
 /* builder/udp.rs:67-95 + builder/ipv4.rs:94-170 + builder/ethernet.rs:63-70,

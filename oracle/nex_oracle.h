@@ -62,6 +62,11 @@ int nexo_parse_batch(const nexg_frames* frames, uint32_t flags,
 
 /* Builders: udp_ping.rs:68-109 composition for one tuple. Returns bytes
  * written (42 + payload_len) or -1 on BuildError. */
+/* FrameSlice::try_from_buf (frame.rs:84-287) */
+void nexo_slice_frame(const uint8_t* packet, size_t len, uint32_t flags, uint32_t ip_offset,
+                      nexg_slice* out);
+void nexo_slice_batch(const nexg_frames* fr, uint32_t flags, uint32_t ip_offset, nexg_slice* out);
+
 int nexo_build_udp4(const uint8_t src_mac[6], const uint8_t dst_mac[6],
                     uint32_t src_ip, uint32_t dst_ip, uint16_t sport,
                     uint16_t dport, uint16_t ip_id, uint8_t ttl,

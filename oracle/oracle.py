@@ -47,6 +47,10 @@ def lib():
         L.nexo_build_udp4.restype = I
         L.nexo_build_udp4.argtypes = [P, P, U32, U32, U16, U16, U16, ctypes.c_uint8, ctypes.c_uint8,
                                       ctypes.c_uint8, P, U32, P]
+        L.nexo_slice_frame.restype = None
+        L.nexo_slice_frame.argtypes = [P, ctypes.c_size_t, U32, U32, P]
+        L.nexo_slice_batch.restype = None
+        L.nexo_slice_batch.argtypes = [ctypes.POINTER(abi.Frames), U32, U32, P]
         L.nexo_build_udp6.restype = I
         L.nexo_build_udp6.argtypes = [P, P, P, P, U16, U16, ctypes.c_uint8, ctypes.c_uint8, U32, P,
                                       U32, P]
@@ -113,6 +117,29 @@ def parse_packed(data: np.ndarray, offsets=None, lengths=None, stride=0, flags=0
     recs = np.zeros(count, dtype=abi.RECORD_DTYPE)
     lib().nexo_parse_batch(ctypes.byref(fr), flags, ip_offset, recs.ctypes.data, None, nthreads)
     return recs
+
+
+def slice_frame(frame: bytes, flags=0, ip_offset=0):
+    """FrameSlice::try_from_buf (frame.rs:84-287) -> one nexg_slice."""
+    out = np.zeros(1, dtype=abi.SLICE_DTYPE)
+    b, n = _buf(frame)
+    lib().nexo_slice_frame(b, n, flags, ip_offset, out.ctypes.data)
+    return out[0]
+
+
+def slice_packed(data: np.ndarray, offsets=None, lengths=None, stride=0, flags=0, ip_offset=0):
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    count = (len(lengths) if lengths is not None else
+             (len(offsets) - 1 if offsets is not None else len(data) // stride))
+    offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.uint32)
+    fr = abi.Frames(data=data.ctypes.data, data_bytes=data.nbytes,
+                    offsets=None if offs is None else offs.ctypes.data,
+                    lengths=None if lens is None else lens.ctypes.data,
+                    stride=stride, reserved=0, count=count)
+    out = np.zeros(count, dtype=abi.SLICE_DTYPE)
+    lib().nexo_slice_batch(ctypes.byref(fr), flags, ip_offset, out.ctypes.data)
+    return out
 
 
 def parse_frames(frames, flags=0, ip_offset=0):

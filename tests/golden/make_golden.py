@@ -22,9 +22,12 @@ def eth(payload, ethertype=0x0800, dst=bytes(6), src=bytes(6)):
 V = []
 
 
-def add(name, cite, frame, expect, flags=0, ip_offset=0, note=""):
-    V.append({"name": name, "cite": cite, "frame": h(frame), "parse_flags": flags,
-              "ip_offset": ip_offset, "expect": expect, "note": note})
+def add(name, cite, frame, expect, flags=0, ip_offset=0, note="", slice_expect=None):
+    v = {"name": name, "cite": cite, "frame": h(frame), "parse_flags": flags,
+         "ip_offset": ip_offset, "expect": expect, "note": note}
+    if slice_expect is not None:  # what FrameSlice::try_from_buf asserts for the same bytes
+        v["slice_expect"] = slice_expect
+    V.append(v)
 
 
 # ---- util.rs:190-261 (checksum arithmetic) --------------------------------
@@ -104,7 +107,10 @@ add("frame_slice_ipv4_tcp", "frame.rs:747-762 (FrameSlice boundaries; same bytes
            0, 192, 0, 2, 1, 198, 51, 100, 2, 0, 80, 0x04, 0xd2, 0, 0, 0, 0, 0, 0, 0, 0, 0x50,
            0x18, 0, 0, 0, 0, 0, 0]) + b"data",
     {"layers": ["eth", "ip", "ipv4", "transport", "tcp"], "l3_off": 14, "l4_off": 34,
-     "payload": b"data".hex(), "ip_proto": 6})
+     "payload": b"data".hex(), "ip_proto": 6},
+    slice_expect={"cite": "frame.rs:747-762; tests/allocation_behavior.rs:36-49 (is_ok)",
+                  "datalink": [0, 14], "network": [14, 34], "transport": [34, 54],
+                  "payload": [54, 58], "ip_protocol": 6})
 b = bytearray(14 + 40 + 8 + 8 + 3)
 b[12:14] = (0x86DD).to_bytes(2, "big")
 b[14] = 0x60
@@ -120,7 +126,9 @@ b[70:] = b"dns"
 add("frame_slice_ipv6_hbh_udp", "frame.rs:764-784 (Frame path: HBH -> no transport, Q10)", b,
     {"layers": ["eth", "ip", "ipv6"], "ip_nopt": 1, "payload": bytes(b[62:73]).hex()},
     note="FrameSlice reports network 48 B / UDP; Frame keeps raw next_header 0 (Q10) and "
-         "exposes the bytes after the extension chain as payload")
+         "exposes the bytes after the extension chain as payload",
+    slice_expect={"cite": "frame.rs:764-784", "network_len": 48, "transport_len": 8,
+                  "payload_bytes": b"dns".hex(), "ip_protocol": 17})
 
 # ---- ipv4.rs:944-1204 ------------------------------------------------------
 IPV4_RT = bytes([0x45, 0x00, 0x00, 0x1c, 0x1c, 0x46, 0x40, 0x00, 0x40, 0x06, 0xb1, 0xe6,

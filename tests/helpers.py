@@ -202,3 +202,32 @@ def mutate_frames(rng: np.random.Generator, base, n: int):
             fr = bytearray(rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8))
         out.append(bytes(fr))
     return out
+
+
+def slice_frames():
+    """Extra edge cases for FrameSlice (frame.rs:84-287): AH walks, extension
+    truncation at each check, ARP lengths, tiny transports, from-IP prefixes."""
+    P = bytes(range(60))
+    f = []
+    for ah_len in (0, 1, 4):
+        ah = bytes([17, ah_len]) + bytes((ah_len + 2) * 4 - 2)
+        f.append(_eth(_ipv6(ah + _udp(P[:9]), 51), 0x86DD))
+    hbh = bytes([51, 0]) + bytes(6)
+    f.append(_eth(_ipv6(hbh + bytes([6, 1]) + bytes(10) + _tcp(P[:5]), 0), 0x86DD))  # HBH -> AH -> TCP
+    f.append(_eth(_ipv6(bytes([17, 0]) + bytes(6) + _udp(b""), 44), 0x86DD))         # fragment
+    f.append(_eth(_ipv6(bytes([58, 0]) + bytes(6) + bytes(4), 60), 0x86DD))            # dest opts -> ICMPv6 4 B
+    f.append(_eth(_ipv6(bytes([17]), 0), 0x86DD))                                       # ext: cursor+2 > len
+    f.append(_eth(_ipv6(bytes([17, 0]) + bytes(3), 43), 0x86DD))                        # ext overruns
+    f.append(_eth(_ipv6(bytes([17]), 51), 0x86DD))                                      # AH: cursor+2 > len
+    f.append(_eth(_ipv6(bytes([17, 9]) + bytes(4), 51), 0x86DD))                        # AH overruns
+    f.append(_eth(_ipv6(bytes(8), 44, plen=4), 0x86DD))                                 # fragment past plen
+    f.append(_eth(_ipv6(_udp(P[:3]), 17, plen=0), 0x86DD))                             # plen 0: no transport
+    f.append(_eth(_ipv6(_tcp(P[:3], doff=15), 6), 0x86DD))
+    f.append(_eth(_ipv4(bytes(3), 1)))                                                 # ICMP < 4
+    f.append(_eth(_ipv4(bytes(4), 58)))                                                # ICMPv6 in IPv4
+    f.append(_eth(_ipv4(_udp(P, length=2), 17)))
+    f.append(_eth(bytes(27), 0x0806))
+    f.append(_eth(bytes(28), 0x0806))
+    f.append(_eth(bytes(40), 0x0806))
+    f.append(_eth(P[:20], 0x8100))
+    return f

@@ -73,3 +73,29 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
     }
     return 0;
 }
+
+// FrameSlice core (frame_core.hpp slice_frame) on the host, through the same
+// LDS-window accessor the kernels use (window bytes staged, rest "HBM").
+extern "C" int harness_slice(const uint8_t* data, uint64_t data_bytes, const uint64_t* offsets,
+                             const uint32_t* lengths, uint32_t stride, uint64_t count,
+                             uint32_t flags, uint32_t ip_offset, uint32_t window, nexg_slice* out) {
+    alignas(16) uint8_t slot[65536 + 32];
+    for (uint64_t i = 0; i < count; i++) {
+        const uint64_t off = offsets ? offsets[i] : i * (uint64_t)stride;
+        const uint64_t len = lengths ? lengths[i] : (offsets ? offsets[i + 1] - off : stride);
+        nexg_slice s{};
+        if (len > 65535 || off > data_bytes || len > data_bytes - off) {
+            s.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
+        } else {
+            const uint8_t* g = data + off;
+            const uint32_t o = (uint32_t)(reinterpret_cast<uint64_t>(g) & 15u);
+            const uint32_t wlen = len < window ? (uint32_t)len : window;
+            memset(slot, 0xA5, sizeof(slot));
+            memcpy(slot + o, g, wlen);
+            nexg::WinFrame f{slot, g, o, wlen};
+            nexg::slice_frame(f, (uint32_t)len, flags, ip_offset, s);
+        }
+        out[i] = s;
+    }
+    return 0;
+}

@@ -20,6 +20,8 @@ def lib():
         P, U32, U64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
         L.harness_parse.restype = ctypes.c_int
         L.harness_parse.argtypes = [P, U64, P, P, U32, U64, U32, U32, U32, ctypes.c_int, P]
+        L.harness_slice.restype = ctypes.c_int
+        L.harness_slice.argtypes = [P, U64, P, P, U32, U64, U32, U32, U32, P]
         _lib = L
     return _lib
 
@@ -37,3 +39,17 @@ def parse_packed(data, offsets=None, lengths=None, stride=0, flags=0, ip_offset=
                         None if lens is None else lens.ctypes.data, stride, count, flags,
                         ip_offset, window, int(use_fast), recs.ctypes.data)
     return recs
+
+
+def slice_packed(data, offsets=None, lengths=None, stride=0, flags=0, ip_offset=0, window=128):
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    count = (len(lengths) if lengths is not None else
+             (len(offsets) - 1 if offsets is not None else len(data) // stride))
+    offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.uint32)
+    out = np.zeros(count, dtype=abi.SLICE_DTYPE)
+    lib().harness_slice(data.ctypes.data, data.nbytes,
+                        None if offs is None else offs.ctypes.data,
+                        None if lens is None else lens.ctypes.data, stride, count, flags,
+                        ip_offset, window, out.ctypes.data)
+    return out

@@ -92,3 +92,23 @@ def test_engine_refuses_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(_lib.NexgLibraryMissing):
         _lib.load()
+
+
+def test_slice_layout_matches_c(tmp_path):
+    names = abi.SLICE_DTYPE.names
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', 'int main(void){',
+             'printf("%zu\\n", sizeof(nexg_slice));']
+    lines += [f'printf("%zu\\n", offsetof(nexg_slice, {f}));' for f in names]
+    lines += [f'printf("%u\\n", (unsigned)({m}));' for m in
+              ("NEXG_OUT_SLICE", "NEXG_S_DATALINK", "NEXG_S_NETWORK", "NEXG_S_TRANSPORT",
+               "NEXG_S_ETHERTYPE", "NEXG_S_IP_PROTOCOL", "NEXG_S_PROTO_SHIFT")]
+    lines.append("return 0;}")
+    src = tmp_path / "probes.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probes"
+    subprocess.check_call(["gcc", "-std=c11", "-o", str(exe), str(src)])
+    out = list(map(int, subprocess.check_output([str(exe)], text=True).split()))
+    assert out[0] == abi.SLICE_DTYPE.itemsize
+    assert out[1:1 + len(names)] == [abi.SLICE_DTYPE.fields[f][1] for f in names]
+    assert out[1 + len(names):] == [abi.OUT_SLICE, abi.S_DATALINK, abi.S_NETWORK, abi.S_TRANSPORT,
+                                    abi.S_ETHERTYPE, abi.S_IP_PROTOCOL, abi.S_PROTO_SHIFT]

@@ -112,3 +112,19 @@ def test_canonical_fast_path_on_imix(oracle):
         want = oracle.parse_packed(buf, offs, lens, flags=flags)
         got = harness.parse_packed(buf, offs, lens, flags=flags, use_fast=4)
         helpers.records_equal(got, want, frames, f"canonical flags={flags}")
+
+
+@pytest.mark.parametrize("flags,ipo", [(0, 0), (abi.PARSE_FROM_IP, 14), (abi.PARSE_FROM_IP, 0),
+                                       (abi.PARSE_FROM_IP | abi.PARSE_STRICT, 14)])
+@pytest.mark.parametrize("layout", [(1, 0), (1, 3), (4, 0)], ids=str)
+def test_slice_core_matches_oracle(oracle, corpus, flags, ipo, layout):
+    """FrameSlice core (slice_frame) on the host vs the oracle's FrameSlice."""
+    frames = corpus + helpers.slice_frames()
+    buf, offs, lens = pack(frames, *layout)
+    want = oracle.slice_packed(buf, offs, lens, flags=flags, ip_offset=ipo)
+    for window in (128, 64, 0):
+        got = harness.slice_packed(buf, offs, lens, flags=flags, ip_offset=ipo, window=window)
+        bad = np.nonzero(got != want)[0]
+        assert len(bad) == 0, (window, bad[:5], got[bad[:3]], want[bad[:3]])
+    st = abi.status_of(want["flags"])
+    assert (st == 0).sum() > 1000 and len(set(st.tolist())) >= 4  # both outcomes well covered

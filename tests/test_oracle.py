@@ -233,3 +233,100 @@ def test_udp_ping_ipv6_build_kat(oracle):
         assert r["flags"] & abi.C_L4_OK and r["payload_len"] == len(payload)
     with pytest.raises(ValueError):
         oracle.build_udp6(b"\0" * 6, b"\0" * 6, src, dst, 1, 2, payload=bytes(65528))
+
+
+# ---- FrameSlice (frame.rs:84-287) ------------------------------------------
+
+def _check_slice(s, exp, frame, name):
+    assert abi.status_of(np.array([s["flags"]]))[0] == 0, name
+    f = int(s["flags"])
+    if "datalink" in exp:
+        assert f & abi.S_DATALINK and exp["datalink"] == [0, 14], name
+    if "network" in exp:
+        assert f & abi.S_NETWORK, name
+        assert [s["l3_off"], s["l3_off"] + s["l3_len"]] == exp["network"], name
+    if "network_len" in exp:
+        assert f & abi.S_NETWORK and s["l3_len"] == exp["network_len"], name
+    if "transport" in exp:
+        a = s["l3_off"] + s["l3_len"]
+        assert f & abi.S_TRANSPORT and [a, a + s["l4_len"]] == exp["transport"], name
+    if "transport_len" in exp:
+        assert f & abi.S_TRANSPORT and s["l4_len"] == exp["transport_len"], name
+    if "payload" in exp:
+        assert [s["payload_off"], s["payload_off"] + s["payload_len"]] == exp["payload"], name
+    if "payload_bytes" in exp:
+        p = frame[s["payload_off"]:s["payload_off"] + s["payload_len"]]
+        assert p.hex() == exp["payload_bytes"], name
+    if "ip_protocol" in exp:
+        assert f & abi.S_IP_PROTOCOL and (f >> abi.S_PROTO_SHIFT) & 0xFF == exp["ip_protocol"], name
+
+
+def test_frame_slice_goldens(oracle):
+    n = 0
+    for v in helpers.golden()["frames"]:
+        if "slice_expect" not in v:
+            continue
+        fr = bytes.fromhex(v["frame"])
+        _check_slice(oracle.slice_frame(fr, v["parse_flags"], v["ip_offset"]), v["slice_expect"], fr,
+                     v["name"])
+        n += 1
+    assert n == 2
+
+
+def test_frame_slice_semantics(oracle):
+    """Where FrameSlice differs from Frame (frame.rs:179-286): hard errors,
+    AH walked, ICMP from 4 B, UDP length unchecked, lossy protocol value."""
+    P = bytes(range(40))
+    st = lambda s: int(abi.status_of(np.array([s["flags"]]))[0])
+    # IPv4 with IHL < 5: Frame is lenient (ip all None), FrameSlice errors
+    assert st(oracle.slice_frame(helpers._eth(bytes([0x44]) + bytes(19)))) == abi.ERR_INVALID_LENGTH
+    assert st(oracle.slice_frame(helpers._eth(P[:19]))) == abi.ERR_BUFFER_TOO_SHORT
+    assert st(oracle.slice_frame(helpers._eth(bytes([0x55]) + bytes(19)))) == abi.ERR_MALFORMED
+    assert st(oracle.slice_frame(bytes(13))) == abi.ERR_BUFFER_TOO_SHORT
+    # UDP length field is not checked: bogus length still yields an 8-B transport
+    s = oracle.slice_frame(helpers._eth(helpers._ipv4(helpers._udp(P, length=3), 17)))
+    assert st(s) == 0 and s["l4_len"] == 8 and s["payload_len"] == len(P)
+    # ICMP header is 4 B and needs only 4 B
+    s = oracle.slice_frame(helpers._eth(helpers._ipv4(bytes(5), 1)))
+    assert s["l4_len"] == 4 and s["payload_len"] == 1
+    # TCP with a bad data offset is an error (Frame keeps going)
+    assert st(oracle.slice_frame(helpers._eth(helpers._ipv4(helpers._tcp(P, doff=4), 6)))) == \
+        abi.ERR_INVALID_LENGTH
+    # TCP shorter than 20 B: no transport, payload = the bytes
+    s = oracle.slice_frame(helpers._eth(helpers._ipv4(P[:10], 6)))
+    assert st(s) == 0 and not s["flags"] & abi.S_TRANSPORT and s["payload_len"] == 10
+    # IPv6 AH (51) is walked: (len + 2) * 4 bytes, then UDP
+    ah = bytes([17, 1]) + bytes(10)
+    s = oracle.slice_frame(helpers._eth(helpers._ipv6(ah + helpers._udp(b"xyz"), 51), 0x86DD))
+    assert st(s) == 0 and s["l3_len"] == 40 + 12 and s["l4_len"] == 8 and s["payload_len"] == 3
+    # truncated extension header
+    s = oracle.slice_frame(helpers._eth(helpers._ipv6(bytes([17, 3]) + bytes(6), 0), 0x86DD))
+    assert st(s) == abi.ERR_TRUNCATED
+    # protocol 200 reported as Reserved (255)
+    s = oracle.slice_frame(helpers._eth(helpers._ipv4(P, 200)))
+    assert (s["flags"] >> abi.S_PROTO_SHIFT) & 0xFF == 255 and s["payload_len"] == len(P)
+    # ARP: 28-B network when long enough, nothing otherwise
+    s = oracle.slice_frame(helpers._eth(bytes(30), 0x0806))
+    assert s["flags"] & abi.S_NETWORK and s["l3_len"] == 28 and s["payload_len"] == 2
+    s = oracle.slice_frame(helpers._eth(bytes(20), 0x0806))
+    assert not s["flags"] & abi.S_NETWORK and s["payload_len"] == 20
+    # from_ip_packet: offset past the end / bad version
+    assert st(oracle.slice_frame(bytes(4), abi.PARSE_FROM_IP, 5)) == abi.ERR_INVALID_LENGTH
+    assert st(oracle.slice_frame(bytes(4), abi.PARSE_FROM_IP, 4)) == abi.ERR_MALFORMED
+    s = oracle.slice_frame(bytes(2) + helpers._ipv4(helpers._udp(b"ab"), 17), abi.PARSE_FROM_IP, 2)
+    assert st(s) == 0 and not s["flags"] & abi.S_DATALINK and s["l3_off"] == 2
+    assert s["ethertype"] == 0x0800 and s["payload_len"] == 2
+
+
+def test_frame_slice_materialisation(oracle):
+    """nex_amd.frame.frame_slice_from_record rebuilds the reference's borrowed
+    views; errors raise the reference's ParseError kind."""
+    from nex_amd.frame import frame_slice_from_record, InvalidLength
+    v = [x for x in helpers.golden()["frames"] if x["name"] == "frame_slice_ipv4_tcp"][0]
+    fr = bytes.fromhex(v["frame"])
+    fs = frame_slice_from_record(oracle.slice_frame(fr), fr)
+    assert bytes(fs.datalink) == fr[:14] and bytes(fs.network) == fr[14:34]
+    assert bytes(fs.transport) == fr[34:54] and bytes(fs.payload) == b"data"
+    assert fs.ethertype == 0x0800 and fs.ip_protocol == 6
+    with pytest.raises(InvalidLength):
+        frame_slice_from_record(oracle.slice_frame(helpers._eth(bytes([0x44]) + bytes(19))), b"")
