@@ -696,109 +696,132 @@ NEXG_HD void parse_frame(const F& f, uint32_t parity, uint32_t len,
 // Layer boundaries only (no checksums, no ParseMode): every inner failure is
 // an error, AH is walked, ICMP needs 4 B, the UDP length is not checked.
 
-// frame.rs:237-286 parse_transport over [a, a + n)
+// Field values are kept in locals and the struct is assembled once at the end.
+struct SliceAcc {
+    uint32_t flags, l3_off, l3_len, l4_len, poff, plen, et;
+};
+
+// frame.rs:237-286 parse_transport over [a, a + n); returns a ParseError kind
 template <class F>
-NEXG_HD uint32_t slice_transport(const F& f, uint32_t proto, uint32_t a, uint32_t n, nexg_slice& s) {
-    uint32_t hl;
+NEXG_HD uint32_t slice_transport(const F& f, uint32_t proto, uint32_t a, uint32_t n, SliceAcc& s) {
+    uint32_t hl = 0;
     if (proto == 6u) {
-        if (n < 20u) { s.payload_off = (uint16_t)a; s.payload_len = (uint16_t)n; return 0; }
-        hl = (f.u8(a + 12u) >> 4) * 4u;
-        if (hl < 20u || hl > n) return NEXG_ERR_INVALID_LENGTH;
+        if (n >= 20u) {
+            hl = (f.u8(a + 12u) >> 4) * 4u;
+            if (hl < 20u || hl > n) return NEXG_ERR_INVALID_LENGTH;
+        }
     } else if (proto == 17u) {
-        if (n < 8u) { s.payload_off = (uint16_t)a; s.payload_len = (uint16_t)n; return 0; }
-        hl = 8u;
+        hl = n >= 8u ? 8u : 0u;
     } else if (proto == 1u || proto == 58u) {
-        if (n < 4u) { s.payload_off = (uint16_t)a; s.payload_len = (uint16_t)n; return 0; }
-        hl = 4u;
-    } else {
-        s.payload_off = (uint16_t)a;
-        s.payload_len = (uint16_t)n;
-        return 0;
+        hl = n >= 4u ? 4u : 0u;
     }
-    s.flags |= NEXG_S_TRANSPORT;
-    s.l4_len = (uint16_t)hl;
-    s.payload_off = (uint16_t)(a + hl);
-    s.payload_len = (uint16_t)(n - hl);
+    if (hl) {
+        s.flags |= NEXG_S_TRANSPORT;
+        s.l4_len = hl;
+    }
+    s.poff = a + hl;
+    s.plen = n - hl;
     return 0;
 }
 
 template <class F>
-NEXG_HD void slice_frame(const F& f, uint32_t len, uint32_t opt_flags, uint32_t ip_offset, nexg_slice& s) {
-    s = nexg_slice{};
-    uint32_t st = 0, base, n, et;
-    if (opt_flags & NEXG_PARSE_FROM_IP) {
-        if (ip_offset > len) { st = NEXG_ERR_INVALID_LENGTH; goto done; }
-        base = ip_offset;
-        n = len - ip_offset;
-        const uint32_t v = n ? (f.u8(base) >> 4) : 0u;
-        if (v == 4u) et = 0x0800u;
-        else if (v == 6u) et = 0x86DDu;
-        else { st = NEXG_ERR_MALFORMED; goto done; }
-    } else {
-        if (len < 14u) { st = NEXG_ERR_BUFFER_TOO_SHORT; goto done; }
-        s.flags |= NEXG_S_DATALINK;
-        et = (f.u8(12) << 8) | f.u8(13);
-        base = 14u;
-        n = len - 14u;
-    }
-    s.flags |= NEXG_S_ETHERTYPE;
-    s.ethertype = (uint16_t)et;
-    s.payload_off = (uint16_t)base;
-    s.payload_len = (uint16_t)n;
+NEXG_HD uint32_t slice_ip(const F& f, uint32_t et, uint32_t base, uint32_t n, SliceAcc& s) {
     if (et == 0x0800u) {  // frame.rs:138-175
-        if (n < 20u) { st = NEXG_ERR_BUFFER_TOO_SHORT; goto done; }
+        if (n < 20u) return NEXG_ERR_BUFFER_TOO_SHORT;
         const uint32_t b0 = f.u8(base);
-        if ((b0 >> 4) != 4u) { st = NEXG_ERR_MALFORMED; goto done; }
+        if ((b0 >> 4) != 4u) return NEXG_ERR_MALFORMED;
         const uint32_t hl = (b0 & 0x0Fu) * 4u;
-        if (hl < 20u || hl > n) { st = NEXG_ERR_INVALID_LENGTH; goto done; }
+        if (hl < 20u || hl > n) return NEXG_ERR_INVALID_LENGTH;
         const uint32_t declared = (f.u8(base + 2) << 8) | f.u8(base + 3);
         const uint32_t plen = declared == 0u ? n : (declared < n ? declared : n);
-        if (plen < hl) { st = NEXG_ERR_INVALID_LENGTH; goto done; }
+        if (plen < hl) return NEXG_ERR_INVALID_LENGTH;
         const uint32_t proto = ip_next_protocol_value(f.u8(base + 9));
         s.flags |= NEXG_S_NETWORK | NEXG_S_IP_PROTOCOL | (proto << NEXG_S_PROTO_SHIFT);
-        s.l3_off = (uint16_t)base;
-        s.l3_len = (uint16_t)hl;
-        st = slice_transport(f, proto, base + hl, plen - hl, s);
-    } else if (et == 0x86DDu) {  // frame.rs:177-235
-        if (n < 40u) { st = NEXG_ERR_BUFFER_TOO_SHORT; goto done; }
-        if ((f.u8(base) >> 4) != 6u) { st = NEXG_ERR_MALFORMED; goto done; }
+        s.l3_off = base;
+        s.l3_len = hl;
+        return slice_transport(f, proto, base + hl, plen - hl, s);
+    }
+    if (et == 0x86DDu) {  // frame.rs:177-235
+        if (n < 40u) return NEXG_ERR_BUFFER_TOO_SHORT;
+        if ((f.u8(base) >> 4) != 6u) return NEXG_ERR_MALFORMED;
         const uint32_t declared = (f.u8(base + 4) << 8) | f.u8(base + 5);
         const uint32_t plen = 40u + declared < n ? 40u + declared : n;
         uint32_t next = f.u8(base + 6), cur = 40u;
         while (cur < plen) {
             uint32_t el;
             if (next == 0u || next == 43u || next == 60u) {
-                if (cur + 2u > plen) { st = NEXG_ERR_TRUNCATED; goto done; }
+                if (cur + 2u > plen) return NEXG_ERR_TRUNCATED;
                 el = (f.u8(base + cur + 1) + 1u) * 8u;
             } else if (next == 44u) {
                 el = 8u;
             } else if (next == 51u) {
-                if (cur + 2u > plen) { st = NEXG_ERR_TRUNCATED; goto done; }
+                if (cur + 2u > plen) return NEXG_ERR_TRUNCATED;
                 el = (f.u8(base + cur + 1) + 2u) * 4u;
             } else {
                 break;
             }
-            if (cur + el > plen) { st = NEXG_ERR_TRUNCATED; goto done; }
+            if (cur + el > plen) return NEXG_ERR_TRUNCATED;
             next = f.u8(base + cur);
             cur += el;
         }
         const uint32_t proto = ip_next_protocol_value(next);
         s.flags |= NEXG_S_NETWORK | NEXG_S_IP_PROTOCOL | (proto << NEXG_S_PROTO_SHIFT);
-        s.l3_off = (uint16_t)base;
-        s.l3_len = (uint16_t)cur;
-        st = slice_transport(f, proto, base + cur, plen - cur, s);
-    } else if (et == 0x0806u && n >= 28u) {  // frame.rs:127-130
+        s.l3_off = base;
+        s.l3_len = cur;
+        return slice_transport(f, proto, base + cur, plen - cur, s);
+    }
+    if (et == 0x0806u && n >= 28u) {  // frame.rs:127-130
         s.flags |= NEXG_S_NETWORK;
-        s.l3_off = (uint16_t)base;
-        s.l3_len = 28;
-        s.payload_off = (uint16_t)(base + 28u);
-        s.payload_len = (uint16_t)(n - 28u);
+        s.l3_off = base;
+        s.l3_len = 28u;
+        s.poff = base + 28u;
+        s.plen = n - 28u;
     }
-done:
+    return 0;
+}
+
+// FrameSlice::try_from_buf (frame.rs:84-136)
+template <class F>
+NEXG_HD void slice_frame(const F& f, uint32_t len, uint32_t opt_flags, uint32_t ip_offset, nexg_slice& out) {
+    SliceAcc s{0, 0, 0, 0, 0, 0, 0};
+    uint32_t st = 0;
+    if (opt_flags & NEXG_PARSE_FROM_IP) {
+        if (ip_offset > len) {
+            st = NEXG_ERR_INVALID_LENGTH;
+        } else {
+            const uint32_t v = ip_offset < len ? (f.u8(ip_offset) >> 4) : 0u;
+            if (v == 4u || v == 6u) {
+                s.et = v == 4u ? 0x0800u : 0x86DDu;
+                s.poff = ip_offset;
+                s.plen = len - ip_offset;
+            } else {
+                st = NEXG_ERR_MALFORMED;
+            }
+        }
+    } else if (len < 14u) {
+        st = NEXG_ERR_BUFFER_TOO_SHORT;
+    } else {
+        s.flags = NEXG_S_DATALINK;
+        s.et = (f.u8(12) << 8) | f.u8(13);
+        s.poff = 14u;
+        s.plen = len - 14u;
+    }
+    if (st == 0) {
+        s.flags |= NEXG_S_ETHERTYPE;
+        st = slice_ip(f, s.et, s.poff, s.plen, s);
+    }
+    out = nexg_slice{};
     if (st) {
-        s = nexg_slice{};
-        s.flags = st << NEXG_STATUS_SHIFT;
+        out.flags = st << NEXG_STATUS_SHIFT;
+        return;
     }
+    out.flags = s.flags;
+    out.l3_off = (uint16_t)s.l3_off;
+    out.l3_len = (uint16_t)s.l3_len;
+    out.l4_len = (uint16_t)s.l4_len;
+    out.payload_off = (uint16_t)s.poff;
+    out.payload_len = (uint16_t)s.plen;
+    out.ethertype = (uint16_t)s.et;
 }
 
 }  // namespace nexg

@@ -144,6 +144,33 @@ __global__ __launch_bounds__(256) void k_rp_multi(const uint8_t* data, uint64_t 
     }
 }
 
+
+// cache-policy bits on the 16-B loads (one asm block: 4 loads + wait), XCD-aware tile order
+#define RP_ASM_KERNEL(NAME, BITS)                                                              \
+__global__ __launch_bounds__(256) void NAME(const uint8_t* data, uint64_t n16, uint2* out, int xcd) { \
+    uint64_t b = blockIdx.x;                                                                   \
+    if (xcd) { const uint64_t per = gridDim.x / 8; b = (blockIdx.x % 8) * per + blockIdx.x / 8; } \
+    const uint64_t base = b * 1024;                                                            \
+    const uint8_t* p0 = data + 16 * (base + threadIdx.x);                                      \
+    u32x4 v0, v1, v2, v3;                                                                      \
+    asm volatile("global_load_dwordx4 %0, %4, off " BITS "\n\t"                                \
+                 "global_load_dwordx4 %1, %5, off " BITS "\n\t"                                \
+                 "global_load_dwordx4 %2, %6, off " BITS "\n\t"                                \
+                 "global_load_dwordx4 %3, %7, off " BITS "\n\t"                                \
+                 "s_waitcnt vmcnt(0)"                                                          \
+                 : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)                                  \
+                 : "v"(p0), "v"(p0 + 4096), "v"(p0 + 8192), "v"(p0 + 12288) : "memory");       \
+    const uint32_t x = v0.x ^ v0.y ^ v0.z ^ v0.w ^ v1.x ^ v1.y ^ v1.z ^ v1.w ^                  \
+                       v2.x ^ v2.y ^ v2.z ^ v2.w ^ v3.x ^ v3.y ^ v3.z ^ v3.w;                   \
+    out[b * 256 + threadIdx.x] = make_uint2(x, 0);                                             \
+}
+RP_ASM_KERNEL(k_rp_nt, "nt")
+RP_ASM_KERNEL(k_rp_sc0nt, "sc0 nt")
+RP_ASM_KERNEL(k_rp_sc1nt, "sc1 nt")
+RP_ASM_KERNEL(k_rp_sc01nt, "sc0 sc1 nt")
+RP_ASM_KERNEL(k_rp_sc01, "sc0 sc1")
+RP_ASM_KERNEL(k_rp_plain, "")
+
 int main(int argc, char** argv) {
     const uint64_t count = argc > 1 ? strtoull(argv[1], 0, 0) : (16ull << 20), bytes = count * 64, n16 = bytes / 16;
     uint8_t* data;
@@ -167,6 +194,16 @@ int main(int argc, char** argv) {
     vs.push_back({"multi4", [=]() { hipLaunchKernelGGL(k_rp_multi<4>, dim3(n16 / 4096), dim3(256), 0, 0, data, n16, out); }});
     vs.push_back({"multi8", [=]() { hipLaunchKernelGGL(k_rp_multi<8>, dim3(n16 / 8192), dim3(256), 0, 0, data, n16, out); }});
     vs.push_back({"multi16", [=]() { hipLaunchKernelGGL(k_rp_multi<16>, dim3(n16 / 16384), dim3(256), 0, 0, data, n16, out); }});
+    {
+        const dim3 g(n16 / 1024);
+        vs.push_back({"asm_nt", [=]() { hipLaunchKernelGGL(k_rp_nt, g, dim3(256), 0, 0, data, n16, out, 0); }});
+        vs.push_back({"asm_nt_xcd", [=]() { hipLaunchKernelGGL(k_rp_nt, g, dim3(256), 0, 0, data, n16, out, 1); }});
+        vs.push_back({"asm_sc0nt", [=]() { hipLaunchKernelGGL(k_rp_sc0nt, g, dim3(256), 0, 0, data, n16, out, 0); }});
+        vs.push_back({"asm_sc1nt", [=]() { hipLaunchKernelGGL(k_rp_sc1nt, g, dim3(256), 0, 0, data, n16, out, 0); }});
+        vs.push_back({"asm_sc01nt", [=]() { hipLaunchKernelGGL(k_rp_sc01nt, g, dim3(256), 0, 0, data, n16, out, 0); }});
+        vs.push_back({"asm_sc01", [=]() { hipLaunchKernelGGL(k_rp_sc01, g, dim3(256), 0, 0, data, n16, out, 0); }});
+        vs.push_back({"asm_plain", [=]() { hipLaunchKernelGGL(k_rp_plain, g, dim3(256), 0, 0, data, n16, out, 0); }});
+    }
     vs.push_back({"ldsdma", [=]() { hipLaunchKernelGGL(k_rp_ldsdma, dim3(n16 / 1024), dim3(256), 0, 0, data, n16, out); }});
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
