@@ -32,5 +32,6 @@ fi
 if [[ $STEPS == *prof* || $STEPS == all ]]; then
   step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline
   step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 10 --warmup 2 --no-cpu-baseline
+  step prof_ser 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser -o run -- python3 bench.py --workload ser --steps 20 --warmup 2 --no-cpu-baseline
 fi
 echo done
