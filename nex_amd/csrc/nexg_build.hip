@@ -78,9 +78,11 @@ __device__ __forceinline__ void build_copy_out(const uint8_t* smem, uint8_t* T, 
     if (tid < bytes - tail) T[tail + tid] = smem[tail + tid];
 }
 
-template <bool STAGED>
+// MAXS = largest stride the LDS tile holds (0: direct global writes)
+template <uint32_t MAXS>
 __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * kBuildMaxStride : 16];
+    constexpr bool STAGED = MAXS != 0;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
     const nexg_udp4_build& p = a.p;
     const uint64_t first = (uint64_t)blockIdx.x * kBuildTile;
     const uint64_t left = p.count - first;
@@ -159,9 +161,10 @@ struct Build6Args {
     uint32_t out_stride;
 };
 
-template <bool STAGED>
+template <uint32_t MAXS>
 __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * kBuildMaxStride : 16];
+    constexpr bool STAGED = MAXS != 0;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
     const nexg_udp6_build& p = a.p;
     const uint64_t first = (uint64_t)blockIdx.x * kBuildTile;
     const uint64_t left = p.count - first;
@@ -382,10 +385,13 @@ hipError_t launch_build_udp4(const nexg_udp4_build& p, uint8_t* out, uint32_t ou
     BuildArgs a{p, out, out_stride};
     const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
-    if (staged)
-        hipLaunchKernelGGL(k_build_udp4<true>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    // a 16-KiB tile for the udp_ping shapes keeps ~10 workgroups per CU
+    if (staged && out_stride <= 64u)
+        hipLaunchKernelGGL(k_build_udp4<64>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    else if (staged)
+        hipLaunchKernelGGL(k_build_udp4<kBuildMaxStride>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     else
-        hipLaunchKernelGGL(k_build_udp4<false>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+        hipLaunchKernelGGL(k_build_udp4<0>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     return hipGetLastError();
 }
 
@@ -395,10 +401,13 @@ hipError_t launch_build_udp6(const nexg_udp6_build& p, uint8_t* out, uint32_t ou
     Build6Args a{p, out, out_stride};
     const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
-    if (staged)
-        hipLaunchKernelGGL(k_build_udp6<true>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    // a 16-KiB tile for the udp_ping shapes keeps ~10 workgroups per CU
+    if (staged && out_stride <= 64u)
+        hipLaunchKernelGGL(k_build_udp6<64>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    else if (staged)
+        hipLaunchKernelGGL(k_build_udp6<kBuildMaxStride>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     else
-        hipLaunchKernelGGL(k_build_udp6<false>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+        hipLaunchKernelGGL(k_build_udp6<0>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     return hipGetLastError();
 }
 

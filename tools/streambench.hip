@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 #include "../nex_amd/csrc/frame_core.hpp"
@@ -205,6 +206,21 @@ int main(int argc, char** argv) {
         vs.push_back({"asm_plain", [=]() { hipLaunchKernelGGL(k_rp_plain, g, dim3(256), 0, 0, data, n16, out, 0); }});
     }
     vs.push_back({"ldsdma", [=]() { hipLaunchKernelGGL(k_rp_ldsdma, dim3(n16 / 1024), dim3(256), 0, 0, data, n16, out); }});
+    // rotation over ROT separate buffers of the same size: re-use distance
+    // ROT x bytes (what a fresh batch per step sees from the memory-side cache)
+    const int ROT = 6;
+    std::vector<uint8_t*> rot(ROT, nullptr);
+    int rot_ok = 1;
+    for (int r = 0; r < ROT; r++) {
+        if (hipMalloc(&rot[r], bytes) != hipSuccess) { rot_ok = 0; break; }
+        CK(hipMemset(rot[r], 1, bytes));
+    }
+    if (rot_ok) {
+        auto cnt = std::make_shared<int>(0);
+        vs.push_back({"rot6_L4_nt", [=]() { int r = (*cnt)++ % ROT; hipLaunchKernelGGL((k_rp<4, true>), dim3(n16 / 1024), dim3(256), 0, 0, rot[r], n16, out); }});
+        auto cnt2 = std::make_shared<int>(0);
+        vs.push_back({"rot6_asm_nt_xcd", [=]() { int r = (*cnt2)++ % ROT; hipLaunchKernelGGL(k_rp_nt, dim3(n16 / 1024), dim3(256), 0, 0, rot[r], n16, out, 1); }});
+    }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
