@@ -280,6 +280,71 @@ typedef struct nexg_udp6_build {
 int nexg_build_udp6_batch(nexg_ctx* ctx, const nexg_udp6_build* params,
                           uint8_t* out, uint32_t out_stride, void* stream);
 
+/* ---- tcp_ping / icmp_ping ---------------------------------
+ * IP + Ethernet layer shared by these builders: Ipv4PacketBuilder (IHL 5,
+ * builder/ipv4.rs:94-170) or Ipv6PacketBuilder (builder/ipv6.rs:89-152), then
+ * EthernetPacketBuilder (builder/ethernet.rs:63-70). */
+typedef struct nexg_ip_build {
+    const uint8_t* src_ip;    /* per frame: 4 B (family 4) or 16 B (family 6), network order, 4-B aligned */
+    const uint8_t* dst_ip;
+    const uint16_t* ip_id;    /* family 4: per frame, or NULL -> def_ip_id */
+    const uint8_t* src_mac;   /* 6 B per frame, or NULL -> def_src_mac */
+    const uint8_t* dst_mac;
+    uint32_t family;          /* 4 or 6 */
+    uint32_t flow_label;      /* family 6, low 20 bits */
+    uint16_t def_ip_id;
+    uint8_t def_src_mac[6], def_dst_mac[6];
+    uint8_t ttl;              /* IPv4 TTL / IPv6 hop limit (builders default 64) */
+    uint8_t ip_flags;         /* IPv4 3-bit flags (tcp_ping/icmp_ping: DontFragment 0b010) */
+    uint8_t tos;              /* IPv4 dscp<<2|ecn / IPv6 traffic class */
+    uint8_t reserved[3];
+} nexg_ip_build;
+
+/* TcpPacketBuilder::build (builder/tcp.rs:93-158; tcp.rs:521-575 to_bytes:
+ * options zero-padded to 4 B, data offset = (20 + padded) / 4; checksum
+ * tcp::checksum, tcp.rs:1207-1269), composed as examples/tcp_ping.rs:111-163.
+ * Frame = 14 + (20|40) + 20 + padded options + payload_len bytes. */
+typedef struct nexg_tcp_build {
+    nexg_ip_build ip;
+    const uint16_t* src_port; /* per frame, or NULL -> def_src_port */
+    const uint16_t* dst_port;
+    const uint32_t* seq;      /* per frame, or NULL -> def_seq */
+    const uint32_t* ack;
+    const uint8_t* payload;   /* shared by all frames (may be NULL) */
+    uint32_t payload_len;
+    uint32_t def_seq, def_ack;
+    uint16_t def_src_port, def_dst_port;
+    uint16_t window, urgent_ptr;
+    uint8_t flags;
+    uint8_t options_len;      /* encoded TcpOptionPacket bytes in options[] */
+    uint8_t options[40];
+    uint8_t reserved[2];
+    uint64_t count;
+} nexg_tcp_build;
+
+/* IcmpPacketBuilder / Icmpv6PacketBuilder with echo_fields (builder/icmp.rs:
+ * 14-86, builder/icmpv6.rs:14-90; checksums icmp.rs:429-432 / icmpv6.rs:
+ * 589-599), composed as examples/icmp_ping.rs:67-102. Frame = 14 + (20|40)
+ * + 8 + payload_len bytes. */
+typedef struct nexg_icmp_echo_build {
+    nexg_ip_build ip;
+    const uint16_t* identifier; /* per frame, or NULL -> def_identifier */
+    const uint16_t* sequence;   /* per frame, or NULL -> def_sequence */
+    const uint8_t* payload;
+    uint32_t payload_len;
+    uint16_t def_identifier, def_sequence;
+    uint8_t icmp_type, icmp_code; /* EchoRequest: 8/0 (IPv4), 128/0 (IPv6) */
+    uint8_t reserved[2];
+    uint64_t count;
+} nexg_icmp_echo_build;
+
+/* NEXG_ERANGE on BuildError::LengthOverflow (padded options > 40; segment >
+ * 65515 (IPv4) / 65535 (IPv6); ICMP > 65515 / 65535). */
+int nexg_build_tcp_batch(nexg_ctx* ctx, const nexg_tcp_build* params, uint8_t* out,
+                         uint32_t out_stride, void* stream);
+int nexg_build_icmp_echo_batch(nexg_ctx* ctx, const nexg_icmp_echo_build* params,
+                               uint8_t* out, uint32_t out_stride, void* stream);
+
 /* ---- synthetic workloads --------------------------
  * Frame i of a workload depends only on (seed, first_index + i), so shards
  * regenerate identically on any GPU count. */

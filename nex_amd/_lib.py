@@ -43,6 +43,8 @@ def load():
         "nexg_checksum_batch": (I, [P, ctypes.POINTER(abi.Frames), U32, P, P]),
         "nexg_build_udp4_batch": (I, [P, ctypes.POINTER(abi.Udp4Build), P, U32, P]),
         "nexg_build_udp6_batch": (I, [P, ctypes.POINTER(abi.Udp6Build), P, U32, P]),
+        "nexg_build_tcp_batch": (I, [P, ctypes.POINTER(abi.TcpBuild), P, U32, P]),
+        "nexg_build_icmp_echo_batch": (I, [P, ctypes.POINTER(abi.IcmpEchoBuild), P, U32, P]),
         "nexg_gen_lengths": (I, [P, I, U64, U64, U64, P, P]),
         "nexg_gen_frames": (I, [P, I, U64, U64, U64, P, P, U32, P]),
         "nexg_gen_udp4_params": (I, [P, U64, U64, U64, P, P, P, P, P, P]),

@@ -151,9 +151,47 @@ class Udp6Build(ctypes.Structure):
     ]
 
 
+class IpBuild(ctypes.Structure):
+    """struct nexg_ip_build"""
+    _fields_ = [
+        ("src_ip", ctypes.c_void_p), ("dst_ip", ctypes.c_void_p), ("ip_id", ctypes.c_void_p),
+        ("src_mac", ctypes.c_void_p), ("dst_mac", ctypes.c_void_p),
+        ("family", ctypes.c_uint32), ("flow_label", ctypes.c_uint32), ("def_ip_id", ctypes.c_uint16),
+        ("def_src_mac", ctypes.c_uint8 * 6), ("def_dst_mac", ctypes.c_uint8 * 6),
+        ("ttl", ctypes.c_uint8), ("ip_flags", ctypes.c_uint8), ("tos", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 3),
+    ]
+
+
+class TcpBuild(ctypes.Structure):
+    """struct nexg_tcp_build"""
+    _fields_ = [
+        ("ip", IpBuild),
+        ("src_port", ctypes.c_void_p), ("dst_port", ctypes.c_void_p), ("seq", ctypes.c_void_p),
+        ("ack", ctypes.c_void_p), ("payload", ctypes.c_void_p), ("payload_len", ctypes.c_uint32),
+        ("def_seq", ctypes.c_uint32), ("def_ack", ctypes.c_uint32),
+        ("def_src_port", ctypes.c_uint16), ("def_dst_port", ctypes.c_uint16),
+        ("window", ctypes.c_uint16), ("urgent_ptr", ctypes.c_uint16),
+        ("flags", ctypes.c_uint8), ("options_len", ctypes.c_uint8), ("options", ctypes.c_uint8 * 40),
+        ("reserved", ctypes.c_uint8 * 2), ("count", ctypes.c_uint64),
+    ]
+
+
+class IcmpEchoBuild(ctypes.Structure):
+    """struct nexg_icmp_echo_build"""
+    _fields_ = [
+        ("ip", IpBuild),
+        ("identifier", ctypes.c_void_p), ("sequence", ctypes.c_void_p), ("payload", ctypes.c_void_p),
+        ("payload_len", ctypes.c_uint32), ("def_identifier", ctypes.c_uint16),
+        ("def_sequence", ctypes.c_uint16), ("icmp_type", ctypes.c_uint8), ("icmp_code", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 2), ("count", ctypes.c_uint64),
+    ]
+
+
 #: every symbol include/nexg.h declares (tests check the .so exports them)
 EXPORTED_SYMBOLS = (
     "nexg_abi_version", "nexg_strerror", "nexg_ctx_create", "nexg_ctx_destroy",
     "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch",
-    "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
+    "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_build_tcp_batch",
+    "nexg_build_icmp_echo_batch", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
 )

@@ -152,6 +152,46 @@ int nexg_build_udp6_batch(nexg_ctx* ctx, const nexg_udp6_build* p, uint8_t* out,
                       NEXG_ELAUNCH);
 }
 
+static int check_ip_build(nexg_ctx* ctx, const nexg_ip_build& ip, uint64_t count, const uint8_t* out) {
+    if (ip.family != 4 && ip.family != 6) return fail(ctx, NEXG_EINVAL, "IP family must be 4 or 6%s", nullptr);
+    if (count && (!ip.src_ip || !ip.dst_ip || !out))
+        return fail(ctx, NEXG_EINVAL, "NULL address array or output%s", nullptr);
+    if (((reinterpret_cast<uint64_t>(ip.src_ip) | reinterpret_cast<uint64_t>(ip.dst_ip)) & 3u) != 0)
+        return fail(ctx, NEXG_EINVAL, "address arrays must be 4-B aligned%s", nullptr);
+    return NEXG_OK;
+}
+
+int nexg_build_tcp_batch(nexg_ctx* ctx, const nexg_tcp_build* p, uint8_t* out, uint32_t out_stride,
+                         void* stream) {
+    if (!ctx || !p) return NEXG_EINVAL;
+    if (int rc = check_ip_build(ctx, p->ip, p->count, out)) return rc;
+    const uint64_t padded = (p->options_len + 3u) & ~3u;
+    if (p->options_len > 40u || padded > 40u)  // builder/tcp.rs:128-135
+        return fail(ctx, NEXG_ERANGE, "TCP options longer than 40 B%s", nullptr);
+    const uint64_t seg = 20u + padded + p->payload_len;
+    if (seg > (p->ip.family == 4 ? 65535u - 20u : 65535u))  // builder/tcp.rs:94-99, 146-152
+        return fail(ctx, NEXG_ERANGE, "TCP segment length overflow%s", nullptr);
+    if (p->payload_len && !p->payload) return fail(ctx, NEXG_EINVAL, "NULL payload%s", nullptr);
+    const uint64_t flen = 14u + (p->ip.family == 4 ? 20u : 40u) + seg;
+    if (out_stride < flen) return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    return hip_status(ctx, nexg::launch_build_tcp(*p, out, out_stride, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
+int nexg_build_icmp_echo_batch(nexg_ctx* ctx, const nexg_icmp_echo_build* p, uint8_t* out,
+                               uint32_t out_stride, void* stream) {
+    if (!ctx || !p) return NEXG_EINVAL;
+    if (int rc = check_ip_build(ctx, p->ip, p->count, out)) return rc;
+    const uint64_t len = 8u + (uint64_t)p->payload_len;
+    if (len > (p->ip.family == 4 ? 65535u - 20u : 65535u))  // builder/icmp.rs:67-80, icmpv6.rs:72-86
+        return fail(ctx, NEXG_ERANGE, "ICMP packet length overflow%s", nullptr);
+    if (p->payload_len && !p->payload) return fail(ctx, NEXG_EINVAL, "NULL payload%s", nullptr);
+    const uint64_t flen = 14u + (p->ip.family == 4 ? 20u : 40u) + len;
+    if (out_stride < flen) return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    return hip_status(ctx, nexg::launch_build_icmp_echo(*p, out, out_stride, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
 int nexg_gen_lengths(nexg_ctx* ctx, int workload, uint64_t seed, uint64_t first_index,
                      uint64_t count, uint32_t* lengths, void* stream) {
     if (!ctx) return NEXG_EINVAL;

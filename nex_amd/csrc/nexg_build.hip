@@ -239,6 +239,219 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
     }
 }
 
+// ---- tcp_ping / icmp_ping: one kernel per (family, L4 kind) ----------------
+// The header is a compile-time halfword layout (Ethernet 7, IPv4 10 / IPv6 20,
+// TCP 10 / ICMP echo 4) built in registers, then the shared TCP options and
+// payload; checksums in closed form: per-frame words + the options word sum
+// (host-computed, passed in) + the payload word sum (computed once per
+// workgroup into LDS).
+enum { kL4Tcp = 6, kL4Icmp = 1 };
+
+struct L4Args {
+    nexg_ip_build ip;
+    // TCP
+    const uint16_t* sport;
+    const uint16_t* dport;
+    const uint32_t* seq;
+    const uint32_t* ack;
+    uint32_t def_seq, def_ack;
+    uint16_t def_sport, def_dport, window, urg;
+    uint32_t flags;
+    uint32_t opt_padded;  // bytes, multiple of 4, <= 40
+    uint32_t opt_sum;     // BE word sum of the padded options
+    uint8_t options[40];
+    // ICMP
+    const uint16_t* ident;
+    const uint16_t* seqno;
+    uint16_t def_ident, def_seqno;
+    uint32_t icmp_type, icmp_code;
+    // shared
+    const uint8_t* payload;
+    uint32_t payload_len;
+    uint64_t count;
+    uint8_t* out;
+    uint32_t out_stride;
+};
+
+// halfword v (memory order: low byte first) at LDS/global byte offset p
+__device__ __forceinline__ void put_hw(uint8_t* base, uint32_t p, uint32_t v, bool odd) {
+    if (odd) {
+        base[p] = (uint8_t)v;
+        base[p + 1] = (uint8_t)(v >> 8);
+    } else {
+        *reinterpret_cast<uint16_t*>(base + p) = (uint16_t)v;
+    }
+}
+
+template <int FAM, int KIND, uint32_t MAXS>
+__global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
+    constexpr bool STAGED = MAXS != 0;
+    constexpr int NIP = FAM == 4 ? 10 : 20;             // IP header halfwords
+    constexpr int NL4 = KIND == kL4Tcp ? 10 : 4;        // fixed L4 header halfwords
+    constexpr int NH = 7 + NIP + NL4;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
+    __shared__ uint32_t s_pay;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t first = (uint64_t)blockIdx.x * kBuildTile;
+    const uint64_t left = a.count - first;
+    const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
+    const uint64_t i = first + tid;
+    // shared payload: BE word sum (payload starts at an even L4 offset)
+    if (tid == 0) s_pay = 0;
+    __syncthreads();
+    {
+        uint32_t ps = 0;
+        for (uint32_t k = 2u * tid; k < a.payload_len; k += 2u * kBuildTile)
+            ps += ((uint32_t)a.payload[k] << 8) | (k + 1 < a.payload_len ? (uint32_t)a.payload[k + 1] : 0u);
+        if (ps) atomicAdd(&s_pay, ps);
+    }
+    __syncthreads();
+    const uint32_t l4_hdr = KIND == kL4Tcp ? 20u + a.opt_padded : 8u;
+    const uint32_t l4_len = l4_hdr + a.payload_len;
+    const uint32_t flen = 14u + 2u * NIP + l4_len;
+    if (tid < nf) {
+        const nexg_ip_build& ip = a.ip;
+        uint32_t sw[FAM == 4 ? 1 : 4], dw[FAM == 4 ? 1 : 4];
+#pragma unroll
+        for (int k = 0; k < (FAM == 4 ? 1 : 4); k++) {
+            sw[k] = reinterpret_cast<const uint32_t*>(ip.src_ip + (FAM == 4 ? 4u : 16u) * i)[k];
+            dw[k] = reinterpret_cast<const uint32_t*>(ip.dst_ip + (FAM == 4 ? 4u : 16u) * i)[k];
+        }
+        uint32_t addr_le = 0;  // address words as LE halves: x256 gives the BE sum (mod 0xFFFF)
+#pragma unroll
+        for (int k = 0; k < (FAM == 4 ? 1 : 4); k++) addr_le += halves(sw[k]) + halves(dw[k]);
+        uint32_t hw[NH];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const uint32_t b0 = ip.dst_mac ? ip.dst_mac[i * 6 + 2 * k] : ip.def_dst_mac[2 * k];
+            const uint32_t b1 = ip.dst_mac ? ip.dst_mac[i * 6 + 2 * k + 1] : ip.def_dst_mac[2 * k + 1];
+            const uint32_t c0 = ip.src_mac ? ip.src_mac[i * 6 + 2 * k] : ip.def_src_mac[2 * k];
+            const uint32_t c1 = ip.src_mac ? ip.src_mac[i * 6 + 2 * k + 1] : ip.def_src_mac[2 * k + 1];
+            hw[k] = b0 | (b1 << 8);
+            hw[3 + k] = c0 | (c1 << 8);
+        }
+        const uint32_t proto = KIND == kL4Tcp ? 6u : (FAM == 4 ? 1u : 58u);
+        // ---- L4 header + checksum ----
+        uint64_t t;
+        constexpr int L = 7 + NIP;  // first L4 halfword
+        if (KIND == kL4Tcp) {
+            const uint32_t sp = a.sport ? a.sport[i] : a.def_sport;
+            const uint32_t dp = a.dport ? a.dport[i] : a.def_dport;
+            const uint32_t sq = a.seq ? a.seq[i] : a.def_seq;
+            const uint32_t ak = a.ack ? a.ack[i] : a.def_ack;
+            const uint32_t w6 = ((l4_hdr / 4u) << 12) | (a.flags & 0xFFu);
+            t = sp + dp + (sq >> 16) + (sq & 0xFFFFu) + (ak >> 16) + (ak & 0xFFFFu) + w6 + a.window + a.urg +
+                a.opt_sum + s_pay;
+            hw[L + 0] = bswap16(sp); hw[L + 1] = bswap16(dp);
+            hw[L + 2] = bswap16(sq >> 16); hw[L + 3] = bswap16(sq & 0xFFFFu);
+            hw[L + 4] = bswap16(ak >> 16); hw[L + 5] = bswap16(ak & 0xFFFFu);
+            hw[L + 6] = bswap16(w6); hw[L + 7] = bswap16(a.window);
+            hw[L + 9] = bswap16(a.urg);
+        } else {
+            const uint32_t id = a.ident ? a.ident[i] : a.def_ident;
+            const uint32_t sq = a.seqno ? a.seqno[i] : a.def_seqno;
+            const uint32_t w0 = (a.icmp_type << 8) | a.icmp_code;
+            t = w0 + id + sq + s_pay;
+            hw[L + 0] = bswap16(w0);
+            hw[L + 2] = bswap16(id); hw[L + 3] = bswap16(sq);
+        }
+        if (FAM == 6 || KIND == kL4Tcp) t += 256ull * addr_le + proto + l4_len;  // pseudo-header
+        const uint32_t cs = fold_complement(t);  // computed 0 stays 0 (Q18)
+        hw[KIND == kL4Tcp ? L + 8 : L + 1] = bswap16(cs);
+        // ---- IP header ----
+        if (FAM == 4) {
+            const uint32_t total = 20u + l4_len, id = ip.ip_id ? ip.ip_id[i] : ip.def_ip_id;
+            const uint32_t w0 = (0x45u << 8) | ip.tos, w3 = ((uint32_t)(ip.ip_flags & 7u)) << 13;
+            const uint32_t w4 = ((uint32_t)ip.ttl << 8) | proto;
+            const uint32_t ics = fold_complement(256ull * addr_le + w0 + total + id + w3 + w4);
+            hw[6] = 0x0008u;
+            hw[7] = bswap16(w0); hw[8] = bswap16(total); hw[9] = bswap16(id); hw[10] = bswap16(w3);
+            hw[11] = bswap16(w4); hw[12] = bswap16(ics);
+            hw[13] = sw[0] & 0xFFFFu; hw[14] = sw[0] >> 16; hw[15] = dw[0] & 0xFFFFu; hw[16] = dw[0] >> 16;
+        } else {
+            const uint32_t fl = ip.flow_label & 0xFFFFFu, tc = ip.tos;
+            hw[6] = 0xDD86u;
+            hw[7] = ((6u << 4) | (tc >> 4)) | ((((tc & 0xFu) << 4) | (fl >> 16)) << 8);
+            hw[8] = ((fl >> 8) & 0xFFu) | ((fl & 0xFFu) << 8);
+            hw[9] = bswap16(l4_len);
+            hw[10] = proto | ((uint32_t)ip.ttl << 8);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                hw[11 + 2 * k] = sw[k] & 0xFFFFu; hw[12 + 2 * k] = sw[k] >> 16;
+                hw[19 + 2 * k] = dw[k] & 0xFFFFu; hw[20 + 2 * k] = dw[k] >> 16;
+            }
+        }
+        // ---- write: fixed halfwords, options, payload, zero gap ----
+        uint8_t* base = STAGED ? smem : a.out + first * a.out_stride;
+        const uint32_t d0 = tid * a.out_stride;
+        const bool odd = (a.out_stride & 1u) != 0;
+#pragma unroll
+        for (int k = 0; k < NH; k++) put_hw(base, d0 + 2u * k, hw[k], odd);
+        uint32_t p = d0 + 2u * NH;
+        if (KIND == kL4Tcp) {
+            for (uint32_t k = 0; k < a.opt_padded; k += 2) put_hw(base, p + k, a.options[k] | ((uint32_t)a.options[k + 1] << 8), odd);
+            p += a.opt_padded;
+        }
+        for (uint32_t k = 0; k < a.payload_len; k++) base[p + k] = a.payload[k];
+        if (STAGED)
+            for (uint32_t k = flen; k < a.out_stride; k++) base[d0 + k] = 0;
+    }
+    if (STAGED) {
+        __syncthreads();
+        build_copy_out(smem, a.out + first * a.out_stride, nf * a.out_stride);
+    }
+}
+
+template <int FAM, int KIND>
+static void launch_l4_fam(const L4Args& a, uint32_t flen, hipStream_t s) {
+    const uint64_t blocks = (a.count + kBuildTile - 1) / kBuildTile;
+    const bool staged = a.out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(a.out) & 15u) == 0;
+    (void)flen;
+    if (staged && a.out_stride <= 64u)
+        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 64>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    else if (staged)
+        hipLaunchKernelGGL((k_build_l4<FAM, KIND, kBuildMaxStride>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 0>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+}
+
+static hipError_t launch_l4(const L4Args& a, int kind, uint32_t flen, hipStream_t s) {
+    if (a.count == 0) return hipSuccess;
+    if (kind == kL4Tcp) {
+        if (a.ip.family == 4) launch_l4_fam<4, kL4Tcp>(a, flen, s);
+        else launch_l4_fam<6, kL4Tcp>(a, flen, s);
+    } else {
+        if (a.ip.family == 4) launch_l4_fam<4, kL4Icmp>(a, flen, s);
+        else launch_l4_fam<6, kL4Icmp>(a, flen, s);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_build_tcp(const nexg_tcp_build& p, uint8_t* out, uint32_t out_stride, hipStream_t s) {
+    L4Args a{};
+    a.ip = p.ip;
+    a.sport = p.src_port; a.dport = p.dst_port; a.seq = p.seq; a.ack = p.ack;
+    a.def_seq = p.def_seq; a.def_ack = p.def_ack; a.def_sport = p.def_src_port; a.def_dport = p.def_dst_port;
+    a.window = p.window; a.urg = p.urgent_ptr; a.flags = p.flags;
+    a.opt_padded = (p.options_len + 3u) & ~3u;
+    for (uint32_t k = 0; k < 40; k++) a.options[k] = k < p.options_len ? p.options[k] : 0;
+    for (uint32_t k = 0; k < a.opt_padded; k += 2) a.opt_sum += ((uint32_t)a.options[k] << 8) | a.options[k + 1];
+    a.payload = p.payload; a.payload_len = p.payload_len; a.count = p.count;
+    a.out = out; a.out_stride = out_stride;
+    return launch_l4(a, kL4Tcp, 0, s);
+}
+
+hipError_t launch_build_icmp_echo(const nexg_icmp_echo_build& p, uint8_t* out, uint32_t out_stride,
+                                  hipStream_t s) {
+    L4Args a{};
+    a.ip = p.ip;
+    a.ident = p.identifier; a.seqno = p.sequence; a.def_ident = p.def_identifier; a.def_seqno = p.def_sequence;
+    a.icmp_type = p.icmp_type; a.icmp_code = p.icmp_code;
+    a.payload = p.payload; a.payload_len = p.payload_len; a.count = p.count;
+    a.out = out; a.out_stride = out_stride;
+    return launch_l4(a, kL4Icmp, 0, s);
+}
+
 // ------------------------------------------------------------- generators
 
 __global__ void k_gen_lengths(int workload, uint64_t seed, uint64_t first, uint64_t count,

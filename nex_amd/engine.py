@@ -249,6 +249,81 @@ class Engine:
                                                    self._stream(stream)))
         return out
 
+    @staticmethod
+    def _ip_build(family, src_ip, dst_ip, ip_id, def_ip_id, src_mac, dst_mac, ttl, ip_flags, tos,
+                  flow_label):
+        ip = abi.IpBuild()
+        ip.src_ip, ip.dst_ip = src_ip.data_ptr(), dst_ip.data_ptr()
+        ip.ip_id = None if ip_id is None else ip_id.data_ptr()
+        ip.src_mac = ip.dst_mac = None
+        ip.family, ip.flow_label, ip.def_ip_id = family, flow_label, def_ip_id
+        ip.def_src_mac[:] = list(src_mac)
+        ip.def_dst_mac[:] = list(dst_mac)
+        ip.ttl, ip.ip_flags, ip.tos = ttl, ip_flags, tos
+        return ip
+
+    def build_tcp(self, family, src_ip, dst_ip, src_port=None, dst_port=None, seq=None, ack=None,
+                  def_src_port=0, def_dst_port=0, def_seq=0, def_ack=0, flags=0, window=0xFFFF,
+                  urgent_ptr=0, options=b"", payload=None, ip_id=None, def_ip_id=0,
+                  src_mac=b"\0" * 6, dst_mac=b"\0" * 6, ttl=64, ip_flags=0, tos=0, flow_label=0,
+                  out_stride=None, out=None, stream=None):
+        """tcp_ping (examples/tcp_ping.rs:111-163): TcpPacketBuilder -> IPv4/IPv6
+        builder -> EthernetPacketBuilder on every tuple. Addresses are
+        (count, 4|16) uint8 device tensors; ports/ids int16, seq/ack int32."""
+        torch = _torch()
+        count = src_ip.shape[0]
+        plen = 0 if payload is None else payload.numel()
+        padded = (len(options) + 3) // 4 * 4
+        flen = 14 + (20 if family == 4 else 40) + 20 + padded + plen
+        stride = out_stride or flen
+        if out is None:
+            out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
+        p = abi.TcpBuild()
+        p.ip = self._ip_build(family, src_ip, dst_ip, ip_id, def_ip_id, src_mac, dst_mac, ttl,
+                              ip_flags, tos, flow_label)
+        p.src_port = None if src_port is None else src_port.data_ptr()
+        p.dst_port = None if dst_port is None else dst_port.data_ptr()
+        p.seq = None if seq is None else seq.data_ptr()
+        p.ack = None if ack is None else ack.data_ptr()
+        p.payload = None if payload is None else payload.data_ptr()
+        p.payload_len = plen
+        p.def_seq, p.def_ack, p.def_src_port, p.def_dst_port = def_seq, def_ack, def_src_port, def_dst_port
+        p.window, p.urgent_ptr, p.flags = window, urgent_ptr, flags
+        p.options_len = min(len(options), 255)
+        p.options[:min(len(options), 40)] = list(options[:40])
+        p.count = count
+        self._check(self.lib.nexg_build_tcp_batch(self.ctx, ctypes.byref(p), _ptr(out), stride,
+                                                  self._stream(stream)))
+        return out
+
+    def build_icmp_echo(self, family, src_ip, dst_ip, identifier=None, sequence=None,
+                        def_identifier=0, def_sequence=0, icmp_type=None, icmp_code=0, payload=None,
+                        ip_id=None, def_ip_id=0, src_mac=b"\0" * 6, dst_mac=b"\0" * 6, ttl=64,
+                        ip_flags=0, tos=0, flow_label=0, out_stride=None, out=None, stream=None):
+        """icmp_ping (examples/icmp_ping.rs:67-102): Icmp(v6)PacketBuilder with
+        echo_fields -> IPv4/IPv6 builder -> EthernetPacketBuilder."""
+        torch = _torch()
+        count = src_ip.shape[0]
+        plen = 0 if payload is None else payload.numel()
+        flen = 14 + (20 if family == 4 else 40) + 8 + plen
+        stride = out_stride or flen
+        if out is None:
+            out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
+        p = abi.IcmpEchoBuild()
+        p.ip = self._ip_build(family, src_ip, dst_ip, ip_id, def_ip_id, src_mac, dst_mac, ttl,
+                              ip_flags, tos, flow_label)
+        p.identifier = None if identifier is None else identifier.data_ptr()
+        p.sequence = None if sequence is None else sequence.data_ptr()
+        p.payload = None if payload is None else payload.data_ptr()
+        p.payload_len = plen
+        p.def_identifier, p.def_sequence = def_identifier, def_sequence
+        p.icmp_type = (8 if family == 4 else 128) if icmp_type is None else icmp_type
+        p.icmp_code = icmp_code
+        p.count = count
+        self._check(self.lib.nexg_build_icmp_echo_batch(self.ctx, ctypes.byref(p), _ptr(out), stride,
+                                                        self._stream(stream)))
+        return out
+
     # --- synthetic workloads ----------------------------------------------
     def gen_batch(self, workload: int, count: int, seed: int = abi.DEFAULT_SEED,
                   first_index: int = 0, stream=None) -> FrameBatch:

@@ -1003,6 +1003,115 @@ int nexo_build_udp6(const uint8_t src_mac[6], const uint8_t dst_mac[6],
     return (int)(54 + udp_len);
 }
 
+/* IP + Ethernet layers shared by the tcp_ping / icmp_ping builders:
+ * Ipv4PacketBuilder::to_bytes (builder/ipv4.rs:94-170) or Ipv6PacketBuilder::
+ * to_bytes (builder/ipv6.rs:89-152, ipv6.rs:50-75), then EthernetPacketBuilder
+ * (builder/ethernet.rs:63-70). l4 = serialized L4 bytes. Returns frame length
+ * or -1 on BuildError::LengthOverflow. */
+static int wrap_ip_eth(const nexo_ip_spec* ip, uint8_t proto, const uint8_t* l4, size_t l4_len,
+                       uint8_t* out) {
+    memcpy(out, ip->dst_mac, 6);
+    memcpy(out + 6, ip->src_mac, 6);
+    if (ip->family == 4) {
+        size_t total = 20 + l4_len;
+        if (total > 65535) return -1;
+        ipv4_packet pk;
+        memset(&pk, 0, sizeof(pk));
+        pk.version = 4;
+        pk.header_length = 5;
+        pk.dscp = ip->dscp_ecn >> 2;
+        pk.ecn = ip->dscp_ecn & 3;
+        pk.total_length = (uint16_t)total;
+        pk.identification = ip->ip_id;
+        pk.flags = ip->ip_flags & 7;
+        pk.ttl = ip->ttl;
+        pk.proto = proto;
+        memcpy(pk.source, ip->src, 4);
+        memcpy(pk.destination, ip->dst, 4);
+        pk.bytes = l4;
+        pk.payload_off = 0;
+        pk.payload_len = l4_len;
+        uint16_t ics = 0;
+        ipv4_checksum(&pk, &ics); /* builder/ipv4.rs:164 */
+        pk.checksum = ics;
+        out[12] = 0x08;
+        out[13] = 0x00;
+        return (int)(14 + ipv4_to_bytes(&pk, out + 14));
+    }
+    if (l4_len > 65535) return -1; /* builder/ipv6.rs:137 */
+    uint32_t fl = ip->flow_label & 0xFFFFFu;
+    uint8_t* h = out + 14;
+    h[0] = (uint8_t)((6u << 4) | (ip->dscp_ecn >> 4));
+    h[1] = (uint8_t)(((ip->dscp_ecn & 0x0Fu) << 4) | (uint8_t)(fl >> 16));
+    h[2] = (uint8_t)(fl >> 8);
+    h[3] = (uint8_t)fl;
+    put16(h + 4, (uint16_t)l4_len);
+    h[6] = proto;
+    h[7] = ip->ttl;
+    memcpy(h + 8, ip->src, 16);
+    memcpy(h + 24, ip->dst, 16);
+    memcpy(h + 40, l4, l4_len);
+    out[12] = 0x86;
+    out[13] = 0xDD;
+    return (int)(54 + l4_len);
+}
+
+/* TcpPacketBuilder::build (builder/tcp.rs:93-158: data offset from the padded
+ * options, checksum via tcp::checksum over to_bytes, tcp.rs:521-575 /
+ * 1207-1269), composed as examples/tcp_ping.rs:111-163. opts = the encoded
+ * TcpOptionPacket list (kind [, length, data]...). */
+int nexo_build_tcp(const nexo_ip_spec* ip, uint16_t sport, uint16_t dport, uint32_t seq,
+                   uint32_t ack, uint8_t flags, uint16_t window, uint16_t urg,
+                   const uint8_t* opts, uint32_t opt_len, const uint8_t* payload,
+                   uint32_t payload_len, uint8_t* out) {
+    size_t padded = (opt_len + 3u) & ~3u;
+    if (padded > 40) return -1;
+    size_t seg = 20 + padded + payload_len;
+    if (seg > (ip->family == 4 ? 65535u - 20u : 65535u)) return -1;
+    uint8_t* t = (uint8_t*)calloc(seg + 1, 1);
+    put16(t, sport);
+    put16(t + 2, dport);
+    put16(t + 4, (uint16_t)(seq >> 16));
+    put16(t + 6, (uint16_t)seq);
+    put16(t + 8, (uint16_t)(ack >> 16));
+    put16(t + 10, (uint16_t)ack);
+    t[12] = (uint8_t)(((20 + padded) / 4) << 4);
+    t[13] = flags;
+    put16(t + 14, window);
+    put16(t + 16, 0);
+    put16(t + 18, urg);
+    if (opt_len) memcpy(t + 20, opts, opt_len); /* zero padding already there */
+    if (payload_len) memcpy(t + 20 + padded, payload, payload_len);
+    uint16_t cs = ip->family == 4 ? nexo_ipv4_checksum(t, seg, 8, NULL, 0, ip->src, ip->dst, PROTO_TCP)
+                                  : nexo_ipv6_checksum(t, seg, 8, NULL, 0, ip->src, ip->dst, PROTO_TCP);
+    put16(t + 16, cs);
+    int n = wrap_ip_eth(ip, PROTO_TCP, t, seg, out);
+    free(t);
+    return n;
+}
+
+/* IcmpPacketBuilder / Icmpv6PacketBuilder with echo_fields (builder/icmp.rs:
+ * 14-86, builder/icmpv6.rs:14-90; checksums icmp.rs:429-432, icmpv6.rs:589-599),
+ * composed as examples/icmp_ping.rs:67-102. */
+int nexo_build_icmp_echo(const nexo_ip_spec* ip, uint8_t type, uint8_t code, uint16_t ident,
+                         uint16_t seqno, const uint8_t* payload, uint32_t payload_len,
+                         uint8_t* out) {
+    size_t len = 8 + (size_t)payload_len;
+    if (len > (ip->family == 4 ? 65535u - 20u : 65535u)) return -1;
+    uint8_t* m = (uint8_t*)calloc(len + 1, 1);
+    m[0] = type;
+    m[1] = code;
+    put16(m + 4, ident);
+    put16(m + 6, seqno);
+    if (payload_len) memcpy(m + 8, payload, payload_len);
+    uint16_t cs = ip->family == 4 ? nexo_checksum(m, len, 1)
+                                  : nexo_ipv6_checksum(m, len, 1, NULL, 0, ip->src, ip->dst, PROTO_ICMPV6);
+    put16(m + 2, cs);
+    int n = wrap_ip_eth(ip, ip->family == 4 ? PROTO_ICMP : PROTO_ICMPV6, m, len, out);
+    free(m);
+    return n;
+}
+
 /* ======================= synthetic workloads =========================== */
 
 #define PHI 0x9E3779B97F4A7C15ULL

@@ -67,6 +67,24 @@ void nexo_slice_frame(const uint8_t* packet, size_t len, uint32_t flags, uint32_
                       nexg_slice* out);
 void nexo_slice_batch(const nexg_frames* fr, uint32_t flags, uint32_t ip_offset, nexg_slice* out);
 
+/* IP/Ethernet layer parameters of the tcp_ping / icmp_ping builders. v4
+ * addresses use the first 4 bytes of src/dst. */
+typedef struct nexo_ip_spec {
+    int family; /* 4 or 6 */
+    uint8_t src[16], dst[16];
+    uint8_t src_mac[6], dst_mac[6];
+    uint16_t ip_id;
+    uint8_t ttl, ip_flags, dscp_ecn; /* v6: ttl = hop limit, dscp_ecn = traffic class */
+    uint32_t flow_label;
+} nexo_ip_spec;
+int nexo_build_tcp(const nexo_ip_spec* ip, uint16_t sport, uint16_t dport, uint32_t seq,
+                   uint32_t ack, uint8_t flags, uint16_t window, uint16_t urg,
+                   const uint8_t* opts, uint32_t opt_len, const uint8_t* payload,
+                   uint32_t payload_len, uint8_t* out);
+int nexo_build_icmp_echo(const nexo_ip_spec* ip, uint8_t type, uint8_t code, uint16_t ident,
+                         uint16_t seqno, const uint8_t* payload, uint32_t payload_len,
+                         uint8_t* out);
+
 int nexo_build_udp4(const uint8_t src_mac[6], const uint8_t dst_mac[6],
                     uint32_t src_ip, uint32_t dst_ip, uint16_t sport,
                     uint16_t dport, uint16_t ip_id, uint8_t ttl,

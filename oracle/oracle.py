@@ -51,6 +51,12 @@ def lib():
         L.nexo_slice_frame.argtypes = [P, ctypes.c_size_t, U32, U32, P]
         L.nexo_slice_batch.restype = None
         L.nexo_slice_batch.argtypes = [ctypes.POINTER(abi.Frames), U32, U32, P]
+        L.nexo_build_tcp.restype = I
+        L.nexo_build_tcp.argtypes = [ctypes.POINTER(IpSpec), U16, U16, U32, U32, ctypes.c_uint8, U16,
+                                     U16, P, U32, P, U32, P]
+        L.nexo_build_icmp_echo.restype = I
+        L.nexo_build_icmp_echo.argtypes = [ctypes.POINTER(IpSpec), ctypes.c_uint8, ctypes.c_uint8,
+                                           U16, U16, P, U32, P]
         L.nexo_build_udp6.restype = I
         L.nexo_build_udp6.argtypes = [P, P, P, P, U16, U16, ctypes.c_uint8, ctypes.c_uint8, U32, P,
                                       U32, P]
@@ -164,6 +170,48 @@ def build_udp6(src_mac, dst_mac, src_ip: bytes, dst_ip: bytes, sport, dport, hop
     pb, pn = _buf(payload)
     n = lib().nexo_build_udp6(bytes(src_mac), bytes(dst_mac), bytes(src_ip), bytes(dst_ip), sport,
                               dport, hop_limit, traffic_class, flow_label, pb, pn, out)
+    if n < 0:
+        raise ValueError("BuildError::LengthOverflow")
+    return out.raw[:n]
+
+
+class IpSpec(ctypes.Structure):
+    """struct nexo_ip_spec (oracle/nex_oracle.h)"""
+    _fields_ = [("family", ctypes.c_int), ("src", ctypes.c_uint8 * 16), ("dst", ctypes.c_uint8 * 16),
+                ("src_mac", ctypes.c_uint8 * 6), ("dst_mac", ctypes.c_uint8 * 6),
+                ("ip_id", ctypes.c_uint16), ("ttl", ctypes.c_uint8), ("ip_flags", ctypes.c_uint8),
+                ("dscp_ecn", ctypes.c_uint8), ("flow_label", ctypes.c_uint32)]
+
+
+def ip_spec(family, src: bytes, dst: bytes, src_mac=bytes(6), dst_mac=bytes(6), ip_id=0, ttl=64,
+            ip_flags=0, dscp_ecn=0, flow_label=0):
+    sp = IpSpec(family=family, ip_id=ip_id, ttl=ttl, ip_flags=ip_flags, dscp_ecn=dscp_ecn,
+                flow_label=flow_label)
+    sp.src[:len(src)] = list(src)
+    sp.dst[:len(dst)] = list(dst)
+    sp.src_mac[:] = list(src_mac)
+    sp.dst_mac[:] = list(dst_mac)
+    return sp
+
+
+def build_tcp(spec, sport, dport, seq=0, ack=0, flags=0, window=0xFFFF, urg=0, options=b"",
+              payload=b""):
+    """TcpPacketBuilder -> Ipv4/Ipv6PacketBuilder -> EthernetPacketBuilder (tcp_ping.rs)."""
+    out = ctypes.create_string_buffer(54 + 60 + len(payload) + 64)
+    ob, on = _buf(options)
+    pb, pn = _buf(payload)
+    n = lib().nexo_build_tcp(ctypes.byref(spec), sport, dport, seq, ack, flags, window, urg, ob, on,
+                             pb, pn, out)
+    if n < 0:
+        raise ValueError("BuildError::LengthOverflow")
+    return out.raw[:n]
+
+
+def build_icmp_echo(spec, icmp_type, code, ident, seqno, payload=b""):
+    """Icmp(v6)PacketBuilder.echo_fields -> IP -> Ethernet (icmp_ping.rs)."""
+    out = ctypes.create_string_buffer(62 + len(payload) + 64)
+    pb, pn = _buf(payload)
+    n = lib().nexo_build_icmp_echo(ctypes.byref(spec), icmp_type, code, ident, seqno, pb, pn, out)
     if n < 0:
         raise ValueError("BuildError::LengthOverflow")
     return out.raw[:n]

@@ -240,9 +240,36 @@ BUILD = [{
     "frame_len": 42,
 }]
 
+# TCP / ICMP builders (row 8(f)3): what the reference's builder tests assert
+BUILD_L4 = {
+    "tcp_basic": {
+        "cite": "builder/tcp.rs:175-196 (tcp_builder_basic)",
+        "src_ip": "192.168.1.100", "dst_ip": "192.168.1.1", "sport": 1234, "dport": 80,
+        "seq": 1, "ack": 2, "flags": 0x02, "window": 1024, "urg": 0, "payload": b"abc".hex(),
+    },
+    "tcp_oversized_options": {
+        "cite": "builder/tcp.rs:211-228 (5 x TcpOptionPacket::timestamp(0, 0) -> LengthOverflow)",
+        "options": (bytes([8, 10]) + bytes(8)).hex() * 5, "error": "LengthOverflow",
+    },
+    "tcp_ping_options": {
+        "cite": "examples/tcp_ping.rs:111-123 (mss 1460, sack_perm, nop, nop, wscale 7); "
+                "tcp.rs:377-407 option encoders, tcp.rs:521-565 to_bytes padding",
+        "options": "020405b4" "0402" "01" "01" "030307", "window": 64240, "flags": 0x02,
+        "sport": 53443, "data_offset": 8,
+    },
+    "icmp_too_large": {
+        "cite": "builder/icmp.rs:104-117 (payload of 65535 B -> LengthOverflow)",
+        "payload_len": 65535, "error": "LengthOverflow",
+    },
+    "icmp_ping": {
+        "cite": "examples/icmp_ping.rs:67-80 (EchoRequest, code 0, echo_fields(0x1234, 0x1), 'hello')",
+        "ident": 0x1234, "seq": 1, "payload": b"hello".hex(),
+    },
+}
+
 
 def main():
-    out = {"util": UTIL, "icmpv6": ICMPV6, "frames": V, "build": BUILD,
+    out = {"util": UTIL, "icmpv6": ICMPV6, "frames": V, "build": BUILD, "build_l4": BUILD_L4,
            "source": "shellrow/nex reference tests (see each 'cite')"}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_vectors.json")
     with open(path, "w") as f:

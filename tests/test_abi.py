@@ -112,3 +112,19 @@ def test_slice_layout_matches_c(tmp_path):
     assert out[1:1 + len(names)] == [abi.SLICE_DTYPE.fields[f][1] for f in names]
     assert out[1 + len(names):] == [abi.OUT_SLICE, abi.S_DATALINK, abi.S_NETWORK, abi.S_TRANSPORT,
                                     abi.S_ETHERTYPE, abi.S_IP_PROTOCOL, abi.S_PROTO_SHIFT]
+
+
+@pytest.mark.parametrize("cname,cls", [("nexg_ip_build", abi.IpBuild), ("nexg_tcp_build", abi.TcpBuild),
+                                       ("nexg_icmp_echo_build", abi.IcmpEchoBuild)])
+def test_l4_build_layouts_match_c(tmp_path, cname, cls):
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', 'int main(void){',
+             f'printf("%zu\\n", sizeof({cname}));']
+    lines += [f'printf("%zu\\n", offsetof({cname}, {f}));' for f, _ in cls._fields_]
+    lines.append("return 0;}")
+    src = tmp_path / "probe_l4.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe_l4"
+    subprocess.check_call(["gcc", "-std=c11", "-o", str(exe), str(src)])
+    out = list(map(int, subprocess.check_output([str(exe)], text=True).split()))
+    assert out[0] == ctypes.sizeof(cls)
+    assert out[1:] == [getattr(cls, f).offset for f, _ in cls._fields_]

@@ -330,3 +330,83 @@ def test_frame_slice_materialisation(oracle):
     assert fs.ethertype == 0x0800 and fs.ip_protocol == 6
     with pytest.raises(InvalidLength):
         frame_slice_from_record(oracle.slice_frame(helpers._eth(bytes([0x44]) + bytes(19))), b"")
+
+
+# ---- tcp_ping / icmp_ping builders (8(f)3) ---------------------------------
+
+def _pseudo_words(src, dst, proto, length):
+    w = [int.from_bytes(src[i:i + 2], "big") for i in range(0, len(src), 2)]
+    w += [int.from_bytes(dst[i:i + 2], "big") for i in range(0, len(dst), 2)]
+    return w + [proto, length]
+
+
+def _words(b, skip):
+    b = b + (b"\0" if len(b) % 2 else b"")
+    return [int.from_bytes(b[i:i + 2], "big") for i in range(0, len(b), 2) if i // 2 != skip]
+
+
+def test_tcp_builder_reference_assertions(oracle):
+    import ipaddress
+    g = helpers.golden()["build_l4"]
+    b = g["tcp_basic"]
+    src, dst = ipaddress.IPv4Address(b["src_ip"]).packed, ipaddress.IPv4Address(b["dst_ip"]).packed
+    spec = oracle.ip_spec(4, src, dst, ip_flags=2)
+    f = oracle.build_tcp(spec, b["sport"], b["dport"], b["seq"], b["ack"], b["flags"], b["window"],
+                         b["urg"], payload=bytes.fromhex(b["payload"]))
+    t = f[34:]
+    assert int.from_bytes(t[0:2], "big") == 1234 and int.from_bytes(t[2:4], "big") == 80
+    assert int.from_bytes(t[4:8], "big") == 1 and int.from_bytes(t[8:12], "big") == 2
+    assert t[13] == 0x02 and t[12] >> 4 == 5 and t[20:] == b"abc"
+    # independent RFC 1071 sum over the IPv4 pseudo-header (util.rs:81-97)
+    assert int.from_bytes(t[16:18], "big") == _ones_complement(_pseudo_words(src, dst, 6, len(t)) + _words(t, 8))
+    r = oracle.parse_frame(f)
+    assert r["flags"] & abi.C_L4_OK and r["flags"] & abi.C_IP_OK
+    with pytest.raises(ValueError):  # tcp.rs:211-228
+        oracle.build_tcp(spec, 1, 2, options=bytes.fromhex(g["tcp_oversized_options"]["options"]))
+
+
+@pytest.mark.parametrize("family", [4, 6])
+def test_tcp_ping_shape(oracle, family):
+    import ipaddress
+    g = helpers.golden()["build_l4"]["tcp_ping_options"]
+    if family == 4:
+        src, dst = ipaddress.IPv4Address("10.0.0.1").packed, ipaddress.IPv4Address("10.0.0.2").packed
+    else:
+        src, dst = ipaddress.IPv6Address("2001:db8::1").packed, ipaddress.IPv6Address("2001:db8::2").packed
+    spec = oracle.ip_spec(family, src, dst, ip_flags=2)
+    opts = bytes.fromhex(g["options"])
+    f = oracle.build_tcp(spec, g["sport"], 443, 0, 0, g["flags"], g["window"], options=opts)
+    l4 = 34 if family == 4 else 54
+    t = f[l4:]
+    assert t[12] >> 4 == g["data_offset"] and len(t) == 32
+    assert t[20:31] == opts and t[31] == 0  # zero padding to the 4-B boundary
+    ps = _pseudo_words(src, dst, 6, len(t))
+    assert int.from_bytes(t[16:18], "big") == _ones_complement(ps + _words(t, 8))
+    r = oracle.parse_frame(f)
+    assert r["flags"] & abi.C_L4_OK and r["l4_nopt"] == 6  # the zero pad parses back as EOL
+
+
+@pytest.mark.parametrize("family", [4, 6])
+def test_icmp_ping_shape(oracle, family):
+    import ipaddress
+    g = helpers.golden()["build_l4"]
+    e = g["icmp_ping"]
+    if family == 4:
+        src, dst = ipaddress.IPv4Address("10.0.0.1").packed, ipaddress.IPv4Address("10.0.0.2").packed
+        typ = 8
+    else:
+        src, dst = ipaddress.IPv6Address("2001:db8::1").packed, ipaddress.IPv6Address("2001:db8::2").packed
+        typ = 128
+    spec = oracle.ip_spec(family, src, dst, ip_flags=2)
+    f = oracle.build_icmp_echo(spec, typ, 0, e["ident"], e["seq"], bytes.fromhex(e["payload"]))
+    m = f[34:] if family == 4 else f[54:]
+    assert m[0] == typ and m[4:6] == b"\x12\x34" and m[6:8] == b"\x00\x01" and m[8:] == b"hello"
+    words = _words(m, 1)
+    if family == 6:
+        words = _pseudo_words(src, dst, 58, len(m)) + words
+    assert int.from_bytes(m[2:4], "big") == _ones_complement(words)
+    r = oracle.parse_frame(f)
+    assert r["flags"] & abi.C_L4_OK
+    with pytest.raises(ValueError):  # builder/icmp.rs:104-117
+        oracle.build_icmp_echo(oracle.ip_spec(4, src[:4], dst[:4]), 8, 0, 0, 0,
+                               bytes(g["icmp_too_large"]["payload_len"]))
