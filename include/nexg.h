@@ -345,6 +345,29 @@ int nexg_build_tcp_batch(nexg_ctx* ctx, const nexg_tcp_build* params, uint8_t* o
 int nexg_build_icmp_echo_batch(nexg_ctx* ctx, const nexg_icmp_echo_build* params,
                                uint8_t* out, uint32_t out_stride, void* stream);
 
+/* ---- capture-file batch ingest ---------------------------
+ * Replaces nex-datalink's pcap::from_file channel (nex-datalink/src/pcap.rs:
+ * 95-109) read one frame per RawReceiver::next (pcap.rs:178-190): each call
+ * copies the next records' captured bytes back to back into a host buffer
+ * (pinned for the H2D pipeline) and writes the packed offset table, ready for
+ * nexg_parse_batch (offsets without lengths). Classic pcap (µs/ns, either
+ * byte order) and pcapng (SHB, IDB, EPB, SPB, OPB). Host-side only. */
+typedef struct nexg_pcap nexg_pcap;
+int nexg_pcap_open(const char* path, nexg_pcap** out);
+/* LINKTYPE of the file (first interface for pcapng): 1 = Ethernet; 101 =
+ * raw IP (parse with NEXG_PARSE_FROM_IP, ip_offset 0). */
+int nexg_pcap_linktype(const nexg_pcap* p);
+const char* nexg_pcap_last_error(const nexg_pcap* p);
+/* Up to max_frames records: frame k at data + offsets[k], offsets[n] = end
+ * (offsets holds max_frames + 1 entries); ts_ns (optional) receives
+ * timestamps in ns. *n_frames = 0 at end of file. A record that does not fit
+ * data_cap waits for the next call (NEXG_ERANGE if not even one fits).
+ * NEXG_EINVAL on a malformed or truncated file, after the complete records
+ * before the damage were delivered. */
+int nexg_pcap_read_batch(nexg_pcap* p, uint8_t* data, uint64_t data_cap, uint64_t* offsets,
+                         uint64_t max_frames, uint64_t* ts_ns, uint64_t* n_frames);
+int nexg_pcap_close(nexg_pcap* p);
+
 /* ---- synthetic workloads --------------------------
  * Frame i of a workload depends only on (seed, first_index + i), so shards
  * regenerate identically on any GPU count. */

@@ -45,6 +45,11 @@ def load():
         "nexg_build_udp6_batch": (I, [P, ctypes.POINTER(abi.Udp6Build), P, U32, P]),
         "nexg_build_tcp_batch": (I, [P, ctypes.POINTER(abi.TcpBuild), P, U32, P]),
         "nexg_build_icmp_echo_batch": (I, [P, ctypes.POINTER(abi.IcmpEchoBuild), P, U32, P]),
+        "nexg_pcap_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
+        "nexg_pcap_linktype": (I, [P]),
+        "nexg_pcap_last_error": (ctypes.c_char_p, [P]),
+        "nexg_pcap_read_batch": (I, [P, P, U64, P, U64, P, ctypes.POINTER(U64)]),
+        "nexg_pcap_close": (I, [P]),
         "nexg_gen_lengths": (I, [P, I, U64, U64, U64, P, P]),
         "nexg_gen_frames": (I, [P, I, U64, U64, U64, P, P, U32, P]),
         "nexg_gen_udp4_params": (I, [P, U64, U64, U64, P, P, P, P, P, P]),

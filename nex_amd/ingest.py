@@ -1,0 +1,109 @@
+"""Capture-file batch ingest (nexg_pcap_* in include/nexg.h).
+
+The host half of the end-to-end path: nex-datalink hands frames over one at a
+time (`RawReceiver::next`, nex-datalink/src/lib.rs:363-366; the file channel
+is pcap::from_file, pcap.rs:95-109). Here a native reader (libnexg.so,
+nex_amd/csrc/nexg_pcap.cpp) fills a packed batch — bytes back to back plus an
+offset table — in (optionally pinned) host memory, and `device_batches`
+moves each batch to the GPU as a FrameBatch for nexg_parse_batch.
+"""
+import ctypes
+from typing import Iterator, Optional, Tuple
+
+import numpy as np
+
+from . import abi
+from ._lib import load
+
+LINKTYPE_ETHERNET = 1
+LINKTYPE_RAW = 101
+
+
+class PcapError(RuntimeError):
+    pass
+
+
+class PcapReader:
+    """Classic pcap (µs/ns, either byte order) or pcapng reader."""
+
+    def __init__(self, path: str):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        rc = self.lib.nexg_pcap_open(str(path).encode(), ctypes.byref(h))
+        if rc != abi.OK:
+            raise PcapError(f"cannot open {path} as pcap/pcapng (status {rc})")
+        self.h = h
+
+    @property
+    def linktype(self) -> int:
+        return self.lib.nexg_pcap_linktype(self.h)
+
+    def read_into(self, data: np.ndarray, offsets: np.ndarray,
+                  ts_ns: Optional[np.ndarray] = None) -> int:
+        """Fill caller arrays (data uint8, offsets uint64 with room for
+        max_frames + 1 entries); returns the frame count (0 at end of file)."""
+        n = ctypes.c_uint64()
+        max_frames = len(offsets) - 1
+        rc = self.lib.nexg_pcap_read_batch(
+            self.h, data.ctypes.data, data.nbytes, offsets.ctypes.data, max_frames,
+            None if ts_ns is None else ts_ns.ctypes.data, ctypes.byref(n))
+        if rc != abi.OK:
+            raise PcapError(self.lib.nexg_pcap_last_error(self.h).decode() or f"status {rc}")
+        return n.value
+
+    def read_batch(self, max_frames: int = 1 << 16, data_cap: int = 1 << 26
+                   ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Next batch as (data, offsets[n+1], ts_ns[n]) numpy arrays."""
+        data = np.empty(data_cap, np.uint8)
+        offs = np.empty(max_frames + 1, np.uint64)
+        ts = np.empty(max_frames, np.uint64)
+        n = self.read_into(data, offs, ts)
+        return data[: int(offs[n])] if n else data[:0], offs[: n + 1], ts[:n]
+
+    def frames(self, **kw) -> Iterator[bytes]:
+        while True:
+            data, offs, _ = self.read_batch(**kw)
+            if len(offs) <= 1:
+                return
+            for a, b in zip(offs[:-1], offs[1:]):
+                yield bytes(data[int(a):int(b)])
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.nexg_pcap_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_batches(reader: PcapReader, max_frames: int = 1 << 20, data_cap: int = 1 << 28,
+                   device="cuda", stream=None):
+    """Yield FrameBatch objects on `device`: each batch is read into pinned
+    host memory by the native reader and copied H2D on `stream` (the packed
+    offsets-only layout, parsed by the SpanTile kernel)."""
+    import torch
+    from .engine import FrameBatch
+    data = torch.empty(data_cap, dtype=torch.uint8, pin_memory=True)
+    offs = torch.empty(max_frames + 1, dtype=torch.int64, pin_memory=True)
+    dnp, onp = data.numpy(), offs.numpy().view(np.uint64)
+    while True:
+        n = reader.read_into(dnp, onp)
+        if n == 0:
+            return
+        nbytes = int(onp[n])
+        s = stream or torch.cuda.current_stream()
+        with torch.cuda.stream(s):
+            d = data[:max(nbytes, 1)].to(device, non_blocking=True)
+            o = offs[: n + 1].to(device, non_blocking=True)
+        s.synchronize()  # the pinned staging buffers are reused by the next read
+        yield FrameBatch(data=d[:nbytes], count=n, offsets=o)

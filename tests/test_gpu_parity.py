@@ -242,3 +242,21 @@ def test_bad_extent_and_empty(engine):
     assert list(abi.status_of(d["flags"])) == [0, abi.ERR_BAD_EXTENT, abi.ERR_BAD_EXTENT]
     d = engine.parse_to_numpy(FrameBatch(data=data, count=0, stride=64), out_kind=abi.OUT_DESC)
     assert len(d) == 0
+
+
+def test_pcap_ingest_to_gpu_parse(engine, oracle, tmp_path):
+    """Capture file -> native batch reader (pinned) -> H2D -> span parse ==
+    the oracle on the same frames (SURVEY.md 8(f)2 ingest path)."""
+    from nex_amd.ingest import PcapReader, device_batches
+    from tests import pcapfile
+    frames = [oracle.gen_frame(abi.WL_IMIX, i) for i in range(3000)] + helpers.crafted_frames()[1:]
+    path = tmp_path / "x.pcapng"
+    blob = pcapfile.ng_shb() + pcapfile.ng_idb(1)
+    blob += b"".join(pcapfile.ng_epb(f, i) for i, f in enumerate(frames))
+    path.write_bytes(blob)
+    got = []
+    with PcapReader(str(path)) as r:
+        for b in device_batches(r, max_frames=1000, data_cap=1 << 20):
+            got.append(engine.parse_to_numpy(b, out_kind=abi.OUT_RECORD))
+    got = np.concatenate(got)
+    helpers.records_equal(got, oracle.parse_frames(frames), frames, "pcap ingest")

@@ -1,0 +1,117 @@
+"""Capture-file batch ingest (nexg_pcap_*, nex_amd/csrc/nexg_pcap.cpp) on the
+host: classic pcap in both byte orders and resolutions, pcapng with EPB / SPB /
+OPB blocks, interface timestamp resolutions, skipped blocks, sections that
+change byte order, batch boundaries, truncated and malformed files. The GPU
+half (device_batches -> nexg_parse_batch) is in tests/test_gpu_parity.py."""
+import os
+
+import numpy as np
+import pytest
+
+from nex_amd import abi
+from nex_amd.ingest import PcapError, PcapReader
+from tests import helpers, pcapfile
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "nex_amd", "libnexg.so")
+pytestmark = pytest.mark.skipif(not os.path.exists(LIB), reason="libnexg.so not built")
+
+
+@pytest.fixture(scope="module")
+def frames(oracle):
+    rng = np.random.default_rng(5)
+    base = helpers.crafted_frames() + [oracle.gen_frame(abi.WL_IMIX, i) for i in range(200)]
+    return [f for f in base if len(f) > 0] + [bytes(rng.integers(0, 256, 9000, dtype=np.uint8))]
+
+
+def _write(tmp_path, name, blob):
+    p = tmp_path / name
+    p.write_bytes(blob)
+    return str(p)
+
+
+@pytest.mark.parametrize("big_endian", [False, True])
+@pytest.mark.parametrize("nsec", [False, True])
+def test_classic_pcap(tmp_path, frames, big_endian, nsec):
+    ts = [i * 1_234_567_891 + 17_000 for i in range(len(frames))]
+    path = _write(tmp_path, "a.pcap", pcapfile.classic(frames, ts, big_endian, nsec, linktype=1))
+    with PcapReader(path) as r:
+        assert r.linktype == 1
+        data, offs, t = r.read_batch(max_frames=len(frames) + 5)
+        got = [bytes(data[int(a):int(b)]) for a, b in zip(offs[:-1], offs[1:])]
+        assert got == frames
+        want_ts = ts if nsec else [x // 1000 * 1000 for x in ts]
+        assert list(t) == want_ts
+        assert len(r.read_batch()[1]) == 1  # end of file
+
+
+def test_batch_boundaries(tmp_path, frames):
+    path = _write(tmp_path, "b.pcap", pcapfile.classic(frames))
+    with PcapReader(path) as r:
+        got = []
+        while True:
+            data, offs, _ = r.read_batch(max_frames=7, data_cap=12000)  # both limits bind
+            if len(offs) == 1:
+                break
+            assert len(offs) - 1 <= 7 and offs[-1] <= 12000
+            got += [bytes(data[int(a):int(b)]) for a, b in zip(offs[:-1], offs[1:])]
+    assert got == frames
+    with PcapReader(path) as r, pytest.raises(PcapError):
+        for _ in range(1000):  # a record larger than data_cap can never be delivered
+            r.read_batch(max_frames=4, data_cap=2000)
+
+
+@pytest.mark.parametrize("big_endian", [False, True])
+def test_pcapng(tmp_path, frames, big_endian):
+    be = big_endian
+    fr = frames[:60]
+    blob = pcapfile.ng_shb(be) + pcapfile.ng_idb(1, 0, None, be) + pcapfile.ng_idb(1, 0, 9, be)
+    want_ts = []
+    for i, f in enumerate(fr):
+        kind = i % 4
+        if kind == 0:
+            blob += pcapfile.ng_epb(f, 1000 * i + 7, 0, big_endian=be)  # µs ticks (default resolution)
+            want_ts.append((1000 * i + 7) * 1000)
+        elif kind == 1:
+            blob += pcapfile.ng_epb(f, 10**9 * i + 3, 1, big_endian=be)  # ns ticks (if_tsresol 9)
+            want_ts.append(10**9 * i + 3)
+        elif kind == 2:
+            blob += pcapfile.ng_spb(f, be)
+            want_ts.append(0)
+        else:
+            blob += pcapfile.ng_nrb(be) + pcapfile.ng_opb(f, 5 * i, 0, be)
+            want_ts.append(5 * i * 1000)
+    # a second section in the other byte order
+    blob += pcapfile.ng_shb(not be) + pcapfile.ng_idb(1, 0, None, not be)
+    blob += pcapfile.ng_epb(fr[0], 42, 0, big_endian=not be)
+    path = _write(tmp_path, "c.pcapng", blob)
+    with PcapReader(path) as r:
+        assert r.linktype == 1
+        data, offs, t = r.read_batch(max_frames=1000)
+        got = [bytes(data[int(a):int(b)]) for a, b in zip(offs[:-1], offs[1:])]
+        assert got == fr + [fr[0]]
+        assert list(t) == want_ts + [42000]
+
+
+def test_caplen_truncated_records(tmp_path, frames):
+    caps = [max(1, len(f) // 2) for f in frames]
+    path = _write(tmp_path, "d.pcap", pcapfile.classic(frames, caplens=caps))
+    with PcapReader(path) as r:
+        got = list(r.frames())
+    assert got == [f[:c] for f, c in zip(frames, caps)]
+
+
+def test_truncated_and_bad_files(tmp_path, frames):
+    blob = pcapfile.classic(frames[:10])
+    path = _write(tmp_path, "e.pcap", blob[:-5])
+    with PcapReader(path) as r:
+        data, offs, _ = r.read_batch(max_frames=100)
+        assert len(offs) - 1 == 9  # the complete records first ...
+        with pytest.raises(PcapError):  # ... then the damage
+            r.read_batch()
+    with pytest.raises(PcapError):
+        PcapReader(_write(tmp_path, "f.pcap", b"not a capture file at all"))
+    with pytest.raises(PcapError):
+        PcapReader(str(tmp_path / "missing.pcap"))
+    raw = _write(tmp_path, "g.pcap", pcapfile.classic(frames[:3], linktype=101))
+    with PcapReader(raw) as r:
+        assert r.linktype == 101
