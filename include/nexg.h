@@ -366,6 +366,15 @@ const char* nexg_pcap_last_error(const nexg_pcap* p);
  * before the damage were delivered. */
 int nexg_pcap_read_batch(nexg_pcap* p, uint8_t* data, uint64_t data_cap, uint64_t* offsets,
                          uint64_t max_frames, uint64_t* ts_ns, uint64_t* n_frames);
+/* In-place shape: the next file bytes are read straight into buf (up to cap,
+ * one copy from the page cache) and the records found there are described by
+ * offsets[k] / lengths[k] into buf (record headers stay in place; parse with
+ * this offsets + lengths layout). Bytes of a record cut at the end of buf are
+ * carried to the next call. *bytes_used = bytes of buf holding complete
+ * records; *n_frames == 0 and *bytes_used == 0 means end of file. */
+int nexg_pcap_read_raw(nexg_pcap* p, uint8_t* buf, uint64_t cap, uint64_t* offsets,
+                       uint32_t* lengths, uint64_t max_frames, uint64_t* ts_ns,
+                       uint64_t* n_frames, uint64_t* bytes_used);
 int nexg_pcap_close(nexg_pcap* p);
 
 /* ---- synthetic workloads --------------------------

@@ -51,6 +51,20 @@ class PcapReader:
             raise PcapError(self.lib.nexg_pcap_last_error(self.h).decode() or f"status {rc}")
         return n.value
 
+    def read_raw_into(self, buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
+                      ts_ns: Optional[np.ndarray] = None) -> Tuple[int, int]:
+        """In-place shape: file bytes read straight into buf, records described
+        by offsets/lengths into it. Returns (frames, bytes used); (0, 0) at
+        end of file."""
+        n, used = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self.lib.nexg_pcap_read_raw(
+            self.h, buf.ctypes.data, buf.nbytes, offsets.ctypes.data, lengths.ctypes.data,
+            len(offsets), None if ts_ns is None else ts_ns.ctypes.data, ctypes.byref(n),
+            ctypes.byref(used))
+        if rc != abi.OK:
+            raise PcapError(self.lib.nexg_pcap_last_error(self.h).decode() or f"status {rc}")
+        return n.value, used.value
+
     def read_batch(self, max_frames: int = 1 << 16, data_cap: int = 1 << 26
                    ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Next batch as (data, offsets[n+1], ts_ns[n]) numpy arrays."""
@@ -84,6 +98,19 @@ class PcapReader:
             self.close()
         except Exception:
             pass
+
+
+def raw_frames(reader: PcapReader, cap: int = 1 << 22, max_frames: int = 1 << 14) -> Iterator[bytes]:
+    """All frames via the in-place shape (test / inspection helper)."""
+    buf = np.empty(cap, np.uint8)
+    offs = np.empty(max_frames, np.uint64)
+    lens = np.empty(max_frames, np.uint32)
+    while True:
+        n, used = reader.read_raw_into(buf, offs, lens)
+        if n == 0 and used == 0:
+            return
+        for k in range(n):
+            yield bytes(buf[int(offs[k]):int(offs[k]) + int(lens[k])])
 
 
 def device_batches(reader: PcapReader, max_frames: int = 1 << 20, data_cap: int = 1 << 28,

@@ -115,3 +115,41 @@ def test_truncated_and_bad_files(tmp_path, frames):
     raw = _write(tmp_path, "g.pcap", pcapfile.classic(frames[:3], linktype=101))
     with PcapReader(raw) as r:
         assert r.linktype == 101
+
+
+def _all_variants(tmp_path, frames):
+    fr = frames[:80]
+    out = {"classic_le": pcapfile.classic(fr), "classic_be_ns": pcapfile.classic(fr, big_endian=True, nsec=True)}
+    blob = pcapfile.ng_shb() + pcapfile.ng_idb(1, 0, 9)
+    for i, f in enumerate(fr):
+        blob += (pcapfile.ng_epb(f, i), pcapfile.ng_spb(f), pcapfile.ng_nrb() + pcapfile.ng_opb(f, i))[i % 3]
+    out["pcapng"] = blob + pcapfile.ng_shb(True) + pcapfile.ng_idb(1, 0, None, True) + pcapfile.ng_epb(fr[1], 5, big_endian=True)
+    return out, fr
+
+
+@pytest.mark.parametrize("cap", [1 << 22, 20000, 9100])
+def test_raw_shape_matches_packed(tmp_path, frames, cap):
+    from nex_amd.ingest import raw_frames
+    files, fr = _all_variants(tmp_path, frames)
+    for name, blob in files.items():
+        path = _write(tmp_path, name, blob)
+        with PcapReader(path) as r:
+            packed = list(r.frames())
+        with PcapReader(path) as r:
+            raw = list(raw_frames(r, cap=cap, max_frames=13))
+        assert raw == packed, name
+        assert packed[:len(fr)] == fr
+
+
+def test_raw_shape_errors(tmp_path, frames):
+    from nex_amd.ingest import raw_frames
+    path = _write(tmp_path, "t.pcap", pcapfile.classic(frames[:10])[:-3])
+    with PcapReader(path) as r:
+        got = []
+        with pytest.raises(PcapError):
+            for f in raw_frames(r, cap=1 << 20):
+                got.append(f)
+        assert got == frames[:9]
+    path = _write(tmp_path, "big.pcap", pcapfile.classic(frames[-1:]))  # a 9000-B record
+    with PcapReader(path) as r, pytest.raises(PcapError):
+        list(raw_frames(r, cap=4096))

@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 18, help="frames per staged batch")
     ap.add_argument("--workload", choices=["imix", "udp64"], default="imix")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--shape", choices=["raw", "packed"], default="raw",
+                    help="raw: file bytes read straight into pinned staging, frames in place "
+                         "(offsets + lengths); packed: records copied back to back (offsets only)")
     args = ap.parse_args()
 
     import numpy as np
@@ -79,10 +82,16 @@ def main():
     del data
 
     B = args.batch
-    cap = B * 1518 + 4096
+    # packed: room for B full-size frames; raw: a file chunk per batch, with
+    # enough offset slots that the frame limit never cuts a chunk short
+    cap = B * 1518 + 4096 if args.shape == "packed" else 64 << 20
+    if args.shape == "raw":
+        B = cap // 32
     nbuf = 2
     host = [torch.empty(cap, dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)]
     hoff = [torch.empty(B + 1, dtype=torch.int64, pin_memory=True) for _ in range(nbuf)]
+    hlen = [torch.empty(B, dtype=torch.int32, pin_memory=True) for _ in range(nbuf)]
+    dlen = [torch.empty(B, dtype=torch.int32, device="cuda") for _ in range(nbuf)]
     dev = [torch.empty(cap, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
     doff = [torch.empty(B + 1, dtype=torch.int64, device="cuda") for _ in range(nbuf)]
     out = torch.empty(args.frames * 8 + 8, dtype=torch.uint8, device="cuda")
@@ -100,7 +109,15 @@ def main():
             k = 0
             while True:
                 free[k].acquire()
-                n = r.read_into(host[k].numpy(), hoff[k].numpy().view(np.uint64))
+                if args.shape == "raw":
+                    while True:  # (0, >0): only non-packet blocks consumed, read on
+                        n, used = r.read_raw_into(host[k].numpy(), hoff[k].numpy()[:B].view(np.uint64),
+                                                  hlen[k].numpy().view(np.uint32))
+                        if n or not used:
+                            break
+                    hoff[k][B] = used
+                else:
+                    n = r.read_into(host[k].numpy(), hoff[k].numpy().view(np.uint64))
                 counts[k] = n
                 ready[k].release()
                 if n == 0:
@@ -115,18 +132,23 @@ def main():
             n = counts[k]
             if n == 0:
                 break
-            nb = int(hoff[k][n])
+            nb = int(hoff[k][B]) if args.shape == "raw" else int(hoff[k][n])
             if parsed[k] is not None:
                 copy_s.wait_event(parsed[k])  # device slot k still read by an earlier parse
             with torch.cuda.stream(copy_s):
                 dev[k][:nb].copy_(host[k][:nb], non_blocking=True)
                 doff[k][: n + 1].copy_(hoff[k][: n + 1], non_blocking=True)
+                if args.shape == "raw":
+                    dlen[k][:n].copy_(hlen[k][:n], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(copy_s)
             ev.synchronize()  # staging slot k may be refilled once its bytes left
             free[k].release()
             comp_s.wait_event(ev)
-            fb = FrameBatch(data=dev[k][:nb], count=n, offsets=doff[k][: n + 1])
+            if args.shape == "raw":
+                fb = FrameBatch(data=dev[k][:nb], count=n, offsets=doff[k][:n], lengths=dlen[k][:n])
+            else:
+                fb = FrameBatch(data=dev[k][:nb], count=n, offsets=doff[k][: n + 1])
             eng.parse(fb, out_kind=abi.OUT_DESC, out=out[first * 8:(first + n) * 8], stream=comp_s)
             with torch.cuda.stream(comp_s):
                 hout[first * 8:(first + n) * 8].copy_(out[first * 8:(first + n) * 8], non_blocking=True)
@@ -156,7 +178,7 @@ def main():
                   "pinned H2D -> span parse -> D2H descriptors)",
         "value": round(args.frames / best / 1e6, 2), "unit": "Mpkt/s",
         "gib_s": round(total_bytes / best / 2**30, 3), "frames": args.frames, "bytes": total_bytes,
-        "workload": args.workload, "batch_frames": B, "seconds": round(best, 4),
+        "workload": args.workload, "batch_frames": B, "shape": args.shape, "seconds": round(best, 4),
         "frames_ok": ok, "pcap_write_s": round(wr, 2),
         "note": "one reader thread (file read from the page cache + copy into pinned staging), "
                 "H2D / parse / D2H on two streams, reader one batch ahead"}))
