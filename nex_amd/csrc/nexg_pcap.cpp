@@ -319,7 +319,9 @@ int nexg_pcap_read_raw(nexg_pcap* p, uint8_t* buf, uint64_t cap, uint64_t* offse
     if (have) memcpy(buf, p->carry.data(), have);
     p->carry.erase(p->carry.begin(), p->carry.begin() + have);
     while (have < cap && p->carry.empty() && !p->file_eof) {
-        const size_t got = fread(buf + have, 1, cap - have, p->f);
+        // 4-MiB reads: one huge read() into pinned memory measured ~2x slower
+        const size_t want = cap - have < (4u << 20) ? cap - have : (4u << 20);
+        const size_t got = fread(buf + have, 1, want, p->f);
         have += got;
         if (got == 0) p->file_eof = true;
     }
