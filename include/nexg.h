@@ -71,6 +71,13 @@ enum {
 /* ---- ParseOption / ParseMode (frame.rs:47-50, parse.rs:34-46) ---------- */
 #define NEXG_PARSE_STRICT 0x1u  /* ParseMode::Strict (default Lenient)        */
 #define NEXG_PARSE_FROM_IP 0x2u /* ParseOption.from_ip_packet (ip_offset used) */
+/* Extension (Frame itself never unwraps VLAN, Q3): before
+ * dispatching on the EtherType, unwrap up to two 802.1Q / 802.1ad / QinQ tags
+ * (EtherType 0x8100 / 0x88A8 / 0x9100) as VlanPacket::try_from_buf reads one
+ * (vlan.rs:102-127: 2-B TCI, inner EtherType), when all 4 bytes are present.
+ * The record's ethertype is the inner one, l3_off moves by 4 per tag, the
+ * tags stay readable at frame bytes [12, l3_off - 2); NEXG_L_VLAN is set. */
+#define NEXG_PARSE_VLAN 0x4u
 
 typedef struct nexg_parse_option {
     uint32_t flags;     /* NEXG_PARSE_* */
@@ -99,6 +106,7 @@ typedef struct nexg_parse_option {
 #define NEXG_C_IP_PANIC (1u << 12)   /* ipv4::checksum would panic (Q17)   */
 #define NEXG_C_L4_CHECKED (1u << 13) /* L4 checksum evaluated              */
 #define NEXG_C_L4_OK (1u << 14)      /* ... and equals the stored field    */
+#define NEXG_L_VLAN (1u << 15)       /* NEXG_PARSE_VLAN unwrapped >= 1 tag  */
 #define NEXG_STATUS_SHIFT 24
 #define NEXG_STATUS(flags) (((flags) >> NEXG_STATUS_SHIFT) & 0x7u)
 

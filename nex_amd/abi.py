@@ -22,6 +22,7 @@ ERR_BAD_EXTENT = 7
 
 PARSE_STRICT = 0x1
 PARSE_FROM_IP = 0x2
+PARSE_VLAN = 0x4  # extension: unwrap up to two 802.1Q/802.1ad/QinQ tags (not Frame semantics)
 
 L_ETHERNET = 1 << 0
 L_ARP = 1 << 1
@@ -38,6 +39,7 @@ C_IP_OK = 1 << 11
 C_IP_PANIC = 1 << 12
 C_L4_CHECKED = 1 << 13
 C_L4_OK = 1 << 14
+L_VLAN = 1 << 15
 STATUS_SHIFT = 24
 
 OUT_DESC = 1

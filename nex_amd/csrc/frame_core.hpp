@@ -677,10 +677,20 @@ NEXG_HD void parse_frame(const F& f, uint32_t parity, uint32_t len,
         ethertype = o.be16(12);
         l3 = 14;
     }
+    uint32_t vflag = 0;
+    if ((opt_flags & (NEXG_PARSE_VLAN | NEXG_PARSE_FROM_IP)) == NEXG_PARSE_VLAN) {
+        // extension: up to two tags, each read as vlan.rs:102-127 reads one
+        for (int k = 0; k < 2; k++) {
+            if (!(ethertype == 0x8100u || ethertype == 0x88A8u || ethertype == 0x9100u) || len < l3 + 4u) break;
+            ethertype = o.be16(l3 + 2u);
+            l3 += 4u;
+            vflag = NEXG_L_VLAN;
+        }
+    }
     r.packet_len = (uint16_t)len;
     r.ethertype = (uint16_t)ethertype;
     r.l3_off = (uint16_t)l3;
-    r.flags = NEXG_L_ETHERNET;
+    r.flags = NEXG_L_ETHERNET | vflag;
     uint32_t err = 0;
     if (ethertype == 0x0800u) err = parse_ipv4(o, l3, len, strict, r);
     else if (ethertype == 0x86DDu) err = parse_ipv6(o, l3, len, strict, r);

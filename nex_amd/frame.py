@@ -23,12 +23,16 @@ class ParseMode(enum.Enum):
 
 @dataclass(frozen=True)
 class ParseOption:
-    """frame.rs:47-50"""
+    """frame.rs:47-50 (+ unwrap_vlan: the NEXG_PARSE_VLAN extension, off by
+    default; the reference's Frame never unwraps VLAN tags, Q3)"""
     from_ip_packet: bool = False
     offset: int = 0
+    unwrap_vlan: bool = False
 
     def flags(self, mode: ParseMode = ParseMode.Lenient) -> int:
         f = abi.PARSE_FROM_IP if self.from_ip_packet else 0
+        if self.unwrap_vlan:
+            f |= abi.PARSE_VLAN
         if mode == ParseMode.Strict:
             f |= abi.PARSE_STRICT
         return f

@@ -664,6 +664,14 @@ void nexo_parse_frame(const uint8_t* fr, size_t len, uint32_t flags,
         }
         ethertype = be16(fr + 12);
         l3 = 14;
+        if (flags & NEXG_PARSE_VLAN) {  /* extension: vlan.rs:102-127 per tag */
+            for (int k = 0; k < 2; k++) {
+                if (!(ethertype == 0x8100 || ethertype == 0x88A8 || ethertype == 0x9100) || len < l3 + 4) break;
+                ethertype = be16(fr + l3 + 2);
+                l3 += 4;
+                rec->flags |= NEXG_L_VLAN;
+            }
+        }
     }
     rec->packet_len = (uint16_t)len;
     rec->ethertype = ethertype;

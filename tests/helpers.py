@@ -231,3 +231,29 @@ def slice_frames():
     f.append(_eth(bytes(40), 0x0806))
     f.append(_eth(P[:20], 0x8100))
     return f
+
+
+def vlan(frame: bytes, tags, tpids=None) -> bytes:
+    """Insert 802.1Q-style tags (TCI values) after the MAC addresses."""
+    tpids = tpids or [0x8100] * len(tags)
+    ins = b"".join(t.to_bytes(2, "big") + tci.to_bytes(2, "big") for t, tci in zip(tpids, tags))
+    return frame[:12] + ins + frame[12:]
+
+
+def vlan_frames():
+    """VLAN-extension cases: single / double / QinQ tags over every inner type,
+    truncated tags, three tags (only two unwrapped)."""
+    P = bytes(range(40))
+    inner = [_eth(_ipv4(_udp(P), 17)), _eth(_ipv4(_tcp(P), 6)), _eth(_ipv4(P[:12], 1)),
+             _eth(_ipv6(_udp(P), 17), 0x86DD), _eth(bytes(28), 0x0806), _eth(P[:20], 0x88B5),
+             _eth(bytes([0x44]) + bytes(19))]
+    f = []
+    for x in inner:
+        f.append(vlan(x, [0x0064]))
+        f.append(vlan(x, [0xE00A, 0x0123], [0x88A8, 0x8100]))
+        f.append(vlan(x, [1, 2], [0x9100, 0x8100]))
+        f.append(vlan(x, [1, 2, 3]))
+    f.append(bytes(12) + b"\x81\x00\x00")            # tag cut short
+    f.append(bytes(12) + b"\x81\x00\x00\x01\x08")    # inner EtherType cut short
+    f.append(bytes(12) + b"\x81\x00\x00\x01\x08\x00")  # tag complete, nothing after
+    return f

@@ -128,3 +128,15 @@ def test_slice_core_matches_oracle(oracle, corpus, flags, ipo, layout):
         assert len(bad) == 0, (window, bad[:5], got[bad[:3]], want[bad[:3]])
     st = abi.status_of(want["flags"])
     assert (st == 0).sum() > 1000 and len(set(st.tolist())) >= 4  # both outcomes well covered
+
+
+@pytest.mark.parametrize("flags", [abi.PARSE_VLAN, abi.PARSE_VLAN | abi.PARSE_STRICT])
+@pytest.mark.parametrize("layout", [(1, 0), (4, 0)], ids=str)
+def test_vlan_core_matches_oracle(oracle, corpus, flags, layout):
+    frames = corpus[:3000] + helpers.vlan_frames()
+    buf, offs, lens = pack(frames, *layout)
+    want = oracle.parse_packed(buf, offs, lens, flags=flags)
+    for mode in (0, 4, 5):
+        got = harness.parse_packed(buf, offs, lens, flags=flags, use_fast=mode)
+        helpers.records_equal(got, want, None, f"vlan flags={flags} mode={mode}")
+    assert (want["flags"] & abi.L_VLAN).sum() >= len(helpers.vlan_frames()) - 3

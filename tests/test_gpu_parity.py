@@ -260,3 +260,27 @@ def test_pcap_ingest_to_gpu_parse(engine, oracle, tmp_path):
             got.append(engine.parse_to_numpy(b, out_kind=abi.OUT_RECORD))
     got = np.concatenate(got)
     helpers.records_equal(got, oracle.parse_frames(frames), frames, "pcap ingest")
+
+
+@pytest.mark.parametrize("flags", [abi.PARSE_VLAN, abi.PARSE_VLAN | abi.PARSE_STRICT])
+def test_vlan_extension_on_gpu(engine, oracle, corpus, flags):
+    """NEXG_PARSE_VLAN in every kernel variant == the oracle's extension."""
+    from nex_amd.frame import ParseMode, ParseOption
+    frames = corpus[:8000] + helpers.vlan_frames() * 20
+    opt = ParseOption(unwrap_vlan=True)
+    mode = ParseMode.Strict if flags & abi.PARSE_STRICT else ParseMode.Lenient
+    for batch in (FrameBatch.from_frames(frames, pad_to=4), FrameBatch.from_packed(frames, pad_to=2)):
+        data = batch.data.cpu().numpy()
+        offs = batch.offsets.cpu().numpy().astype(np.uint64)
+        lens = None if batch.lengths is None else batch.lengths.cpu().numpy().astype(np.uint32)
+        want = oracle.parse_packed(data, offs, lens, flags=flags)
+        got = engine.parse_to_numpy(batch, opt, mode, abi.OUT_RECORD)
+        helpers.records_equal(got, want, None, f"vlan lengths={lens is not None}")
+    for stride in (64, 128):
+        sel = [f for f in frames if len(f) <= stride][:6000]
+        arr = np.zeros((len(sel), stride), np.uint8)
+        for i, f in enumerate(sel):
+            arr[i, :len(f)] = np.frombuffer(f, np.uint8)
+        want = oracle.parse_packed(arr.reshape(-1), stride=stride, flags=flags)
+        got = engine.parse_to_numpy(FrameBatch.from_strided(arr), opt, mode, abi.OUT_RECORD)
+        helpers.records_equal(got, want, None, f"vlan stride={stride}")

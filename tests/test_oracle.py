@@ -410,3 +410,40 @@ def test_icmp_ping_shape(oracle, family):
     with pytest.raises(ValueError):  # builder/icmp.rs:104-117
         oracle.build_icmp_echo(oracle.ip_spec(4, src[:4], dst[:4]), 8, 0, 0, 0,
                                bytes(g["icmp_too_large"]["payload_len"]))
+
+
+def test_vlan_extension_oracle(oracle):
+    """NEXG_PARSE_VLAN: a tagged frame parses like the same frame with the tags
+    removed, offsets shifted by 4 per unwrapped tag; without the flag the
+    reference behaviour (Q3: no unwrapping) is untouched."""
+    shift_fields = ("payload_off", "l3_off", "l4_off")
+    for f in helpers.vlan_frames():
+        got = oracle.parse_frame(f, abi.PARSE_VLAN)
+        plain = oracle.parse_frame(f)
+        et = int.from_bytes(f[12:14], "big") if len(f) >= 14 else 0
+        ntag = 0
+        while ntag < 2 and et in (0x8100, 0x88A8, 0x9100) and len(f) >= 14 + 4 * ntag + 4:
+            et = int.from_bytes(f[14 + 4 * ntag + 2:14 + 4 * ntag + 4], "big")
+            ntag += 1
+        if ntag == 0:
+            assert got.tobytes() == plain.tobytes()
+            continue
+        detag = f[:12] + f[12 + 4 * ntag:]
+        want = oracle.parse_frame(detag).copy()
+        assert got["flags"] & abi.L_VLAN
+        assert (int(got["flags"]) & ~abi.L_VLAN) == int(want["flags"]), f.hex()
+        for n in abi.RECORD_DTYPE.names:
+            if n == "flags":
+                continue
+            w = int(want[n])
+            if n in shift_fields and (n != "payload_off" or want["payload_len"]) and \
+                    (n != "l4_off" or w):
+                w += 4 * ntag
+            if n == "packet_len":
+                w = len(f)
+            assert int(got[n]) == w, (n, f.hex())
+    # untagged frames are unchanged by the flag
+    for f in helpers.crafted_frames():
+        if len(f) >= 14 and f[12:14] in (b"\x81\x00", b"\x88\xa8", b"\x91\x00"):
+            continue
+        assert oracle.parse_frame(f, abi.PARSE_VLAN).tobytes() == oracle.parse_frame(f).tobytes()
