@@ -153,3 +153,35 @@ def test_raw_shape_errors(tmp_path, frames):
     path = _write(tmp_path, "big.pcap", pcapfile.classic(frames[-1:]))  # a 9000-B record
     with PcapReader(path) as r, pytest.raises(PcapError):
         list(raw_frames(r, cap=4096))
+
+
+def test_malformed_captures_are_memory_safe(tmp_path, frames):
+    """Random corruptions of valid pcap / pcapng files through the reader
+    built with AddressSanitizer + UBSan (tests/native/pcap_fuzz): every call
+    returns (frames or an error), nothing reads or writes out of bounds."""
+    import subprocess
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+    subprocess.check_call(["make", "-s", "-C", here, "pcap_fuzz"])
+    rng = np.random.default_rng(77)
+    files, _ = _all_variants(tmp_path, frames)
+    paths = []
+    for name, blob in files.items():
+        for k in range(60):
+            b = bytearray(blob)
+            for _ in range(int(rng.integers(1, 8))):
+                op = rng.integers(0, 3)
+                i = int(rng.integers(0, len(b)))
+                if op == 0:
+                    b[i] = int(rng.integers(0, 256))  # byte flip (lengths, magics, caplens ...)
+                elif op == 1:
+                    b[i:i + 4] = int(rng.integers(0, 2**32)).to_bytes(4, "little")
+                else:
+                    del b[i:]  # truncation
+                    break
+            p = tmp_path / f"{name}_{k}.bin"
+            p.write_bytes(bytes(b))
+            paths.append(str(p))
+    r = subprocess.run([os.path.join(here, "pcap_fuzz")] + paths, capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+                                             UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1"))
+    assert r.returncode == 0, r.stderr[-3000:]
