@@ -29,10 +29,18 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(batch, workload, count, seconds):
+def host_threads():
+    """CPU share to use for the threaded baseline: the box grants 16 CPUs per
+    GPU (os.cpu_count() shows the whole machine there), this container 8."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(16, n))
+
+
+def cpu_baseline(batch, workload, count, seconds, nthreads=1):
     """Oracle (C restatement of nex-packet's Frame path + reference-semantic
-    checksums) on the host, 1 thread, over the first `count` frames of the
-    same workload, repeated until ~`seconds` of CPU work."""
+    checksums) on the host over the first `count` frames of the same
+    workload, repeated until ~`seconds` of CPU work; `nthreads` static
+    index-range shards of the sample."""
     import numpy as np
     from nex_amd import abi
     from oracle import oracle
@@ -49,13 +57,13 @@ def cpu_baseline(batch, workload, count, seconds):
     reps, t = 0, 0.0
     while t < seconds and reps < 1000:
         t0 = time.perf_counter()
-        oracle.parse_packed(data, offs, lens, stride=stride, nthreads=1)
+        oracle.parse_packed(data, offs, lens, stride=stride, nthreads=nthreads)
         t += time.perf_counter() - t0
         reps += 1
     mpps = n * reps / t / 1e6
-    return {"value": round(mpps, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+    return {"value": round(mpps, 3), "unit": "Mpkt/s", "cores": nthreads, "kind": "port",
             "gib_s": round(nbytes * reps / t / 2**30, 3),
-            "sample": f"first {n} frames of the same {workload} workload, {reps} passes "
+            "sample": f"{nthreads} thread(s), first {n} frames of the same {workload} workload, {reps} passes "
                       f"({t:.1f} s), oracle/nex_oracle.c (literal restatement of "
                       "Frame::try_from_buf + ipv4/udp/tcp/icmp checksum; Rust reference "
                       "not buildable here)"}
@@ -74,6 +82,68 @@ def load_traffic(workload, out_kind):
         return None
 
 
+def timed(step, steps, warmup, stream, device, host_clock=False):
+    """W untimed steps, then exactly K steps bracketed by barrier + sync on
+    both sides. Returns (max-over-ranks elapsed seconds, per-launch kernel
+    seconds from HIP events on the launch stream)."""
+    import torch
+    from nex_amd import dist
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(device)
+    dist.barrier(device)
+    torch.cuda.synchronize(device)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    dist.barrier(device)
+    elapsed = dist.max_over_ranks(t1 - t0, device)
+    kernel_s = ev0.elapsed_time(ev1) / 1e3 / steps
+    if host_clock:  # copies + kernels on side streams: the host clock is the measure
+        kernel_s = (t1 - t0) / steps
+    return elapsed, kernel_s
+
+
+def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world):
+    """configs[2] beside the default configs[1] run (the metric names both
+    64B and IMIX): 16M IMIX frames per GPU, same output kind, same timing
+    discipline. Returns the object rank 0 adds to the JSON line."""
+    import torch
+    from nex_amd import abi, dist
+    batch = eng.gen_batch(abi.WL_IMIX, F, first_index=first)
+    out = torch.empty(F * width, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize(device)
+    alg = batch.total_bytes
+    steps = max(1, args.steps // 2)
+    elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
+                              steps, max(1, args.warmup // 2), stream, device)
+    frames = dist.sum_over_ranks(F, device) * steps
+    nbytes = dist.sum_over_ranks(alg, device) * steps
+    if rank != 0:
+        return None
+    ach = alg / kernel_s / 1e9
+    r = {"workload": f"configs[2]: {F} IMIX frames per GPU (64/576/1500 at 7:4:1, "
+                     "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table",
+         "value": round(frames / elapsed / 1e6, 2), "unit": "Mpkt/s", "steps": steps,
+         "ms_per_step": round(elapsed / steps * 1e3, 4),
+         "gib_s": round(nbytes / elapsed / 2**30, 2), "bytes_per_gpu": alg,
+         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("imix", args.out),
+                      "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg}}
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            r["cpu_baseline"] = cpu_baseline(batch, "imix", 1 << 20, args.cpu_seconds / 2, host_threads())
+        except Exception as e:
+            r["cpu_baseline"] = {"value": None, "error": repr(e)}
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -81,7 +151,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["udp64", "imix", "ser"], default="udp64")
     ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
-    ap.add_argument("--out", choices=["desc", "record"], default="desc")
+    ap.add_argument("--out", choices=["desc", "record", "flags"], default="desc")
+    ap.add_argument("--no-imix", action="store_true",
+                    help="skip the configs[2] IMIX line reported beside the default UDP64 run")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true",
@@ -104,21 +176,22 @@ def main():
     F = args.frames
     first = rank * F
     stream = torch.cuda.current_stream(device)
-    out_kind = abi.OUT_DESC if args.out == "desc" else abi.OUT_RECORD
+    out_kind = {"desc": abi.OUT_DESC, "record": abi.OUT_RECORD, "flags": abi.OUT_FLAGS}[args.out]
+    width = {"desc": 8, "record": 64, "flags": 4}[args.out]
 
     if args.workload in ("udp64", "imix"):
         wl = abi.WL_UDP64 if args.workload == "udp64" else abi.WL_IMIX
         batch = eng.gen_batch(wl, F, first_index=first)
         torch.cuda.synchronize(device)
         alg_bytes = batch.total_bytes  # Σ frame_len: every byte is read (L4 checksum)
-        out = torch.empty(F * (8 if out_kind == abi.OUT_DESC else 64), dtype=torch.uint8, device=device)
+        out = torch.empty(F * width, dtype=torch.uint8, device=device)
 
         def step():
             eng.parse(batch, out_kind=out_kind, out=out, stream=stream)
         if args.workload == "udp64":
             cfg = {"workload": "configs[1]: 16M x 64-B Eth/IPv4/UDP frames per GPU, fixed 64-B "
                                "stride, device-resident; Frame parse (L2/L3/L4) + IPv4 header and "
-                               "UDP checksum verify -> 8-B descriptor per frame" if F == 16 << 20
+                               f"UDP checksum verify -> {width}-B {args.out} per frame" if F == 16 << 20
                                else f"{F} x 64-B Eth/IPv4/UDP frames per GPU"}
         else:
             cfg = {"workload": f"configs[2]: {F} IMIX frames per GPU (64/576/1500 at 7:4:1, "
@@ -148,7 +221,6 @@ def main():
         host_out = torch.empty(out.numel(), dtype=torch.uint8, pin_memory=True)
         cs, ps = torch.cuda.Stream(device), torch.cuda.Stream(device)
         C = args.e2e_chunk
-        width = 8 if out_kind == abi.OUT_DESC else 64
         from nex_amd.engine import FrameBatch
         offs_host = None if batch.offsets is None else batch.offsets.cpu()
         chunks = []
@@ -178,27 +250,12 @@ def main():
         cfg["workload"] += "; END-TO-END: frames in pinned host memory, chunked H2D/parse/D2H"
         cfg["e2e_chunk_frames"] = C
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(device)
-    dist.barrier(device)
-    torch.cuda.synchronize(device)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(device)
-    t1 = time.perf_counter()
-    dist.barrier(device)
-    elapsed = dist.max_over_ranks(t1 - t0, device)
-    kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # per launch, on the launch stream
-    if args.e2e:  # copies + kernels on two side streams: the host clock is the measure
-        kernel_s = (t1 - t0) / args.steps
+    elapsed, kernel_s = timed(step, args.steps, args.warmup, stream, device, host_clock=args.e2e)
     total_frames = dist.sum_over_ranks(F, device) * args.steps
     total_bytes = dist.sum_over_ranks(alg_bytes, device) * args.steps
+    imix = None
+    if args.workload == "udp64" and not args.e2e and not args.no_imix and F == 16 << 20:
+        imix = imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
 
     if rank != 0:
         return
@@ -227,9 +284,14 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline and batch is not None:
         try:
-            res["cpu_baseline"] = cpu_baseline(batch, args.workload, 1 << 20, args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(batch, args.workload, 1 << 20, args.cpu_seconds / 2,
+                                               host_threads())
+            res["cpu_baseline"]["single_thread"] = cpu_baseline(batch, args.workload, 1 << 20,
+                                                                args.cpu_seconds / 2, 1)
         except Exception as e:  # reported, never fatal to the GPU measurement
             res["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if imix is not None:
+        res["imix"] = imix
     print(json.dumps(res), flush=True)
 
 

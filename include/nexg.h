@@ -162,6 +162,12 @@ typedef struct nexg_record {
 #define NEXG_OUT_DESC 1
 #define NEXG_OUT_RECORD 2
 #define NEXG_OUT_SLICE 3
+/* Flags-only result per frame (out_kind NEXG_OUT_FLAGS), 4 bytes: exactly
+ * nexg_desc.flags (layer presence, checksum verdicts, status) without the
+ * payload location — for consumers that only classify and verify. On HBM the
+ * 8-B descriptor stream costs ~18 % of the read rate at 64-B frames; 4 B
+ * halves that. */
+#define NEXG_OUT_FLAGS 4
 
 /* FrameSlice::try_from_buf (frame.rs:84-287) per frame, out_kind
  * NEXG_OUT_SLICE, 16 bytes: layer boundaries only, no checksums. FrameSlice

@@ -45,6 +45,7 @@ STATUS_SHIFT = 24
 OUT_DESC = 1
 OUT_RECORD = 2
 OUT_SLICE = 3
+OUT_FLAGS = 4  # nexg_desc.flags only (include/nexg.h)
 
 # FrameSlice presence bits (nexg_slice.flags)
 S_DATALINK = 1 << 0
@@ -71,6 +72,7 @@ assert DESC_DTYPE.itemsize == 8
 SLICE_DTYPE = np.dtype([("flags", "<u4"), ("l3_off", "<u2"), ("l3_len", "<u2"), ("l4_len", "<u2"),
                         ("payload_off", "<u2"), ("payload_len", "<u2"), ("ethertype", "<u2")])
 assert SLICE_DTYPE.itemsize == 16
+FLAGS_DTYPE = np.dtype([("flags", "<u4")])
 
 RECORD_DTYPE = np.dtype([
     ("flags", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"),

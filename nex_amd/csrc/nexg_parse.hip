@@ -69,6 +69,7 @@ static hipError_t launch_slice(ParseVariant v, const ParseArgs& a, hipStream_t s
 hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     if (out_kind == NEXG_OUT_SLICE) return launch_slice(v, a, s);
+    if (out_kind == NEXG_OUT_FLAGS) return launch_parse_out<NEXG_OUT_FLAGS>(v, a, s);
     return out_kind == NEXG_OUT_DESC ? launch_parse_out<NEXG_OUT_DESC>(v, a, s)
                                      : launch_parse_out<NEXG_OUT_RECORD>(v, a, s);
 }

@@ -35,7 +35,9 @@ constexpr uint32_t kPiece = 256;  // bytes per piece = 16 lanes x 16 B
 
 template <int OUT>
 __device__ __forceinline__ void store_result(void* out, uint64_t idx, const nexg_record& r) {
-    if (OUT == NEXG_OUT_DESC) {
+    if (OUT == NEXG_OUT_FLAGS) {
+        reinterpret_cast<uint32_t*>(out)[idx] = r.flags;
+    } else if (OUT == NEXG_OUT_DESC) {
         uint2 d = make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
         reinterpret_cast<uint2*>(out)[idx] = d;
     } else {
@@ -84,11 +86,34 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
         const uint32_t S = STRIDE ? (uint32_t)STRIDE : a.stride;
         const uint8_t* T = a.data + first * S;
         const uint32_t chunks = nf * (S / 16u);
-        for (uint32_t c = tid; c < chunks; c += kTile) {
-            const uint4 v = load16<NT>(T + (uint64_t)c * 16u);
-            const uint32_t byte = c * 16u;
-            const uint32_t f = byte / S;
-            *reinterpret_cast<uint4*>(smem + f * PITCH + (byte - f * S)) = v;
+        // every 16-B load of the tile issued before the first LDS write (a
+        // load -> wait -> write loop keeps one load per lane in flight)
+        constexpr uint32_t KMAX = (STRIDE ? (uint32_t)STRIDE : (uint32_t)WIN) / 16u;
+        uint4 v[KMAX];
+        if (STRIDE && nf == kTile) {  // full tile of a compile-time stride: straight line
+#pragma unroll
+            for (uint32_t k = 0; k < KMAX; k++) v[k] = load16<NT>(T + (uint64_t)(tid + k * kTile) * 16u);
+#pragma unroll
+            for (uint32_t k = 0; k < KMAX; k++) {
+                const uint32_t byte = (tid + k * kTile) * 16u;
+                const uint32_t f = byte / S;
+                *reinterpret_cast<uint4*>(smem + f * PITCH + (byte - f * S)) = v[k];
+            }
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < KMAX; k++) {
+                const uint32_t c = tid + k * kTile;
+                if (c < chunks) v[k] = load16<NT>(T + (uint64_t)c * 16u);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < KMAX; k++) {
+                const uint32_t c = tid + k * kTile;
+                if (c < chunks) {
+                    const uint32_t byte = c * 16u;
+                    const uint32_t f = byte / S;
+                    *reinterpret_cast<uint4*>(smem + f * PITCH + (byte - f * S)) = v[k];
+                }
+            }
         }
         __syncthreads();
         if (tid < nf) {
@@ -201,7 +226,7 @@ constexpr uint32_t kLaneWin = 80;  // register window of k_parse_lane80
 // first 4 bytes of the frame's own output element (overwritten by pass 2).
 template <int OUT>
 __device__ __forceinline__ uint32_t* handoff_slot(void* out, uint64_t idx) {
-    return reinterpret_cast<uint32_t*>(out) + idx * (OUT == NEXG_OUT_DESC ? 2u : 16u);
+    return reinterpret_cast<uint32_t*>(out) + idx * (OUT == NEXG_OUT_FLAGS ? 1u : OUT == NEXG_OUT_DESC ? 2u : 16u);
 }
 
 __device__ __forceinline__ bool frame_extent(const ParseArgs& a, uint64_t idx, uint64_t& off, uint32_t& len) {

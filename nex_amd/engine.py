@@ -161,9 +161,10 @@ class Engine:
         FrameSlice::try_from_buf (frame.rs:86) with out_kind=OUT_SLICE.
 
         Returns a uint8 device tensor holding nexg_desc[count] (8 B each),
-        nexg_record[count] (64 B) or nexg_slice[count] (16 B)."""
+        nexg_record[count] (64 B), nexg_slice[count] (16 B) or, with
+        out_kind=OUT_FLAGS, the nexg_desc.flags word alone (4 B)."""
         torch = _torch()
-        width = {abi.OUT_DESC: 8, abi.OUT_RECORD: 64, abi.OUT_SLICE: 16}[out_kind]
+        width = {abi.OUT_DESC: 8, abi.OUT_RECORD: 64, abi.OUT_SLICE: 16, abi.OUT_FLAGS: 4}[out_kind]
         if out is None:
             out = torch.empty(max(batch.count, 1) * width, dtype=torch.uint8, device=self.torch_device)
         fr = batch.to_c()
@@ -177,7 +178,7 @@ class Engine:
         out = self.parse(batch, option, mode, out_kind)
         _torch().cuda.synchronize(self.torch_device)
         dt = {abi.OUT_DESC: abi.DESC_DTYPE, abi.OUT_RECORD: abi.RECORD_DTYPE,
-              abi.OUT_SLICE: abi.SLICE_DTYPE}[out_kind]
+              abi.OUT_SLICE: abi.SLICE_DTYPE, abi.OUT_FLAGS: abi.FLAGS_DTYPE}[out_kind]
         return out.cpu().numpy()[: batch.count * dt.itemsize].view(dt)
 
     def checksum(self, batch: FrameBatch, skipword: int, stream=None):

@@ -284,3 +284,35 @@ def test_vlan_extension_on_gpu(engine, oracle, corpus, flags):
         want = oracle.parse_packed(arr.reshape(-1), stride=stride, flags=flags)
         got = engine.parse_to_numpy(FrameBatch.from_strided(arr), opt, mode, abi.OUT_RECORD)
         helpers.records_equal(got, want, None, f"vlan stride={stride}")
+
+
+def flags_of(recs):
+    d = np.zeros(len(recs), abi.FLAGS_DTYPE)
+    d["flags"] = recs["flags"]
+    return d
+
+
+def test_flags_output_matches_oracle(engine, oracle, corpus):
+    """NEXG_OUT_FLAGS (4 B: nexg_desc.flags alone) in every kernel layout:
+    packed (SpanTile), explicit lengths (TwoPass), fixed strides 64
+    (TileStride64 fast path) and 128 (TileStride)."""
+    import torch
+    want = oracle.parse_frames(corpus)
+    got = engine.parse_to_numpy(FrameBatch.from_packed(corpus, shift=4), out_kind=abi.OUT_FLAGS)
+    assert got.dtype == abi.FLAGS_DTYPE and len(got) == len(corpus)
+    helpers.records_equal(got, flags_of(want), corpus, "flags packed")
+    got = engine.parse_to_numpy(FrameBatch.from_frames(corpus, pad_to=4), out_kind=abi.OUT_FLAGS)
+    helpers.records_equal(got, flags_of(want), corpus, "flags explicit lengths")
+    for stride in (64, 128):
+        sel = [f for f in corpus if len(f) <= stride][:20000]
+        arr = np.zeros((len(sel), stride), np.uint8)
+        for i, f in enumerate(sel):
+            arr[i, :len(f)] = np.frombuffer(f, np.uint8)
+        full = [bytes(arr[i]) for i in range(len(sel))]
+        got = engine.parse_to_numpy(FrameBatch.from_strided(arr), out_kind=abi.OUT_FLAGS)
+        helpers.records_equal(got, flags_of(oracle.parse_frames(full)), full, f"flags stride={stride}")
+    b = engine.gen_batch(abi.WL_UDP64, 1 << 20)
+    f4 = engine.parse(b, out_kind=abi.OUT_FLAGS)
+    d8 = engine.parse(b, out_kind=abi.OUT_DESC)
+    torch.cuda.synchronize()
+    assert (f4.cpu().numpy().view("<u4") == d8.cpu().numpy().view(abi.DESC_DTYPE)["flags"]).all()

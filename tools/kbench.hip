@@ -104,6 +104,7 @@ int main(int argc, char** argv) {
     auto parse = [&](auto kern) { return [=]() { hipLaunchKernelGGL(kern, grid, blk, 0, 0, a); }; };
     vars.push_back({"prod_fast", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, true, false>), count * 64.0});
     vars.push_back({"prod_fast_nt", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, true, true>), count * 64.0});
+    vars.push_back({"flags_fast_nt", parse(k_parse<0, NEXG_OUT_FLAGS, 64, 64, true, true>), count * 64.0});
     vars.push_back({"prod_generic", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, false, false>), count * 64.0});
     vars.push_back({"span_udp64_nb2", parse(k_parse_span<NEXG_OUT_DESC, 2>), count * 64.0});
     vars.push_back({"span_udp64_nb1", parse(k_parse_span<NEXG_OUT_DESC, 1>), count * 64.0});
@@ -121,6 +122,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(h_ref.data(), ref, count * 8, hipMemcpyDeviceToHost));
     for (auto& v : vars) {
         if (v.name.rfind("prod", 0) != 0 && v.name.rfind("lane", 0) != 0 && v.name.rfind("span", 0) != 0) continue;
+        if (v.name.find("flags") != std::string::npos) continue;  // 4-B output, not comparable
         CK(hipMemset(out, 0, count * 8));
         v.run();
         CK(hipDeviceSynchronize());
@@ -154,6 +156,7 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia);
         hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
     ivars.push_back({"imix_span_nb2", iparse(k_parse_span<NEXG_OUT_DESC, 2>), ibytes});
+    ivars.push_back({"imix_flags_span_nb1", iparse(k_parse_span<NEXG_OUT_FLAGS, 1>), ibytes});
     ivars.push_back({"imix_span_nb1", iparse(k_parse_span<NEXG_OUT_DESC, 1>), ibytes});
     ivars.push_back({"imix_span_nb1_8k", iparse(k_parse_span<NEXG_OUT_DESC, 1, 8192>), ibytes});
     ivars.push_back({"imix_span_nb2_8k", iparse(k_parse_span<NEXG_OUT_DESC, 2, 8192>), ibytes});

@@ -27,6 +27,72 @@ __global__ __launch_bounds__(256) void k_rp(const uint8_t* data, uint64_t n16, u
     for (int k = 0; k < L / 4; k++) o[threadIdx.x + 256 * k] = make_uint2(x, k);
 }
 
+// read only: the output is written only on an impossible value (pure read ceiling)
+template <int L>
+__global__ __launch_bounds__(256) void k_ro(const uint8_t* data, uint64_t n16, uint2* out) {
+    const uint64_t base = (uint64_t)blockIdx.x * 256 * L;
+    uint32_t x = 0;
+    uint4 v[L];
+#pragma unroll
+    for (int k = 0; k < L; k++) v[k] = load16<true>(data + 16 * (base + threadIdx.x + 256 * k));
+#pragma unroll
+    for (int k = 0; k < L; k++) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    if (x == 0x9e3779b9u) out[threadIdx.x] = make_uint2(x, 0);
+}
+
+// write-side variants of k_rp<4,true>: W = bytes written per 64-B frame
+// (8, 4, 1), SP = store policy (0 plain, 1 nt, 2 sc0 sc1 nt)
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+template <int W, int SP>
+__global__ __launch_bounds__(256) void k_wv(const uint8_t* data, uint64_t n16, uint8_t* out) {
+    const uint64_t base = (uint64_t)blockIdx.x * 1024;
+    uint32_t x = 0;
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = load16<true>(data + 16 * (base + threadIdx.x + 256 * k));
+#pragma unroll
+    for (int k = 0; k < 4; k++) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    const uint64_t fr = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (W == 8) {
+        u32x2v d = {x, (uint32_t)fr};
+        u32x2v* o = reinterpret_cast<u32x2v*>(out) + fr;
+        if (SP == 0) *o = d;
+        else if (SP == 1) __builtin_nontemporal_store(d, o);
+        else asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1 nt" :: "v"(o), "v"(d) : "memory");
+    } else if (W == 4) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(out) + fr;
+        if (SP == 0) *o = x;
+        else __builtin_nontemporal_store(x, o);
+    } else {
+        // 1 B per frame: 4 frames per dword via a lane shuffle, 64 B per wave
+        uint32_t b = x & 0xff;
+        uint32_t b1 = __shfl_down(b, 1, 64), b2 = __shfl_down(b, 2, 64), b3 = __shfl_down(b, 3, 64);
+        if ((threadIdx.x & 3) == 0) {
+            uint32_t* o = reinterpret_cast<uint32_t*>(out) + fr / 4;
+            const uint32_t w = b | (b1 << 8) | (b2 << 16) | (b3 << 24);
+            if (SP == 0) *o = w; else __builtin_nontemporal_store(w, o);
+        }
+    }
+}
+
+// T tiles per workgroup, the T descriptor blocks written together at the end
+template <int T>
+__global__ __launch_bounds__(256) void k_wbatch(const uint8_t* data, uint64_t n16, uint2* out) {
+    const uint64_t base = (uint64_t)blockIdx.x * 1024 * T;
+    uint32_t x[T];
+#pragma unroll
+    for (int tt = 0; tt < T; tt++) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = load16<true>(data + 16 * (base + 1024ull * tt + threadIdx.x + 256 * k));
+        x[tt] = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) x[tt] ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+#pragma unroll
+    for (int tt = 0; tt < T; tt++) out[base / 4 + 256 * tt + threadIdx.x] = make_uint2(x[tt], tt);
+}
+
 // persistent: grid-stride over tiles of 1024 chunks, software prefetch of the next tile
 __global__ __launch_bounds__(256) void k_rp_persist(const uint8_t* data, uint64_t ntiles, uint2* out) {
     uint4 cur[4], nxt[4];
@@ -204,6 +270,28 @@ int main(int argc, char** argv) {
         vs.push_back({"asm_sc01nt", [=]() { hipLaunchKernelGGL(k_rp_sc01nt, g, dim3(256), 0, 0, data, n16, out, 0); }});
         vs.push_back({"asm_sc01", [=]() { hipLaunchKernelGGL(k_rp_sc01, g, dim3(256), 0, 0, data, n16, out, 0); }});
         vs.push_back({"asm_plain", [=]() { hipLaunchKernelGGL(k_rp_plain, g, dim3(256), 0, 0, data, n16, out, 0); }});
+    }
+    for (int R : {2, 4, 8}) {
+        const uint64_t nunits = count / 64;
+        const uint32_t g4 = cus * (R == 8 ? 1 : (R == 4 ? 2 : 4));
+        if (R == 2) vs.push_back({"ring_R2_W4", [=]() { hipLaunchKernelGGL((k_rp_ring<2, 4>), dim3(g4), dim3(256), 0, 0, data, nunits, out); }});
+        if (R == 4) vs.push_back({"ring_R4_W4", [=]() { hipLaunchKernelGGL((k_rp_ring<4, 4>), dim3(g4), dim3(256), 0, 0, data, nunits, out); }});
+        if (R == 8) vs.push_back({"ring_R8_W4", [=]() { hipLaunchKernelGGL((k_rp_ring<8, 4>), dim3(g4), dim3(256), 0, 0, data, nunits, out); }});
+    }
+    vs.push_back({"readonly_L4_nt", [=]() { hipLaunchKernelGGL((k_ro<4>), dim3(n16 / 1024), dim3(256), 0, 0, data, n16, out); }});
+    vs.push_back({"readonly_L8_nt", [=]() { hipLaunchKernelGGL((k_ro<8>), dim3(n16 / 2048), dim3(256), 0, 0, data, n16, out); }});
+    {
+        uint8_t* o8 = reinterpret_cast<uint8_t*>(out);
+        const dim3 g(n16 / 1024);
+        vs.push_back({"w8_plain", [=]() { hipLaunchKernelGGL((k_wv<8, 0>), g, dim3(256), 0, 0, data, n16, o8); }});
+        vs.push_back({"w8_nt", [=]() { hipLaunchKernelGGL((k_wv<8, 1>), g, dim3(256), 0, 0, data, n16, o8); }});
+        vs.push_back({"w8_sc01nt", [=]() { hipLaunchKernelGGL((k_wv<8, 2>), g, dim3(256), 0, 0, data, n16, o8); }});
+        vs.push_back({"w4_plain", [=]() { hipLaunchKernelGGL((k_wv<4, 0>), g, dim3(256), 0, 0, data, n16, o8); }});
+        vs.push_back({"w4_nt", [=]() { hipLaunchKernelGGL((k_wv<4, 1>), g, dim3(256), 0, 0, data, n16, o8); }});
+        vs.push_back({"w1_plain", [=]() { hipLaunchKernelGGL((k_wv<1, 0>), g, dim3(256), 0, 0, data, n16, o8); }});
+        vs.push_back({"w1_nt", [=]() { hipLaunchKernelGGL((k_wv<1, 1>), g, dim3(256), 0, 0, data, n16, o8); }});
+        vs.push_back({"wbatch4", [=]() { hipLaunchKernelGGL(k_wbatch<4>, dim3(n16 / 4096), dim3(256), 0, 0, data, n16, out); }});
+        vs.push_back({"wbatch8", [=]() { hipLaunchKernelGGL(k_wbatch<8>, dim3(n16 / 8192), dim3(256), 0, 0, data, n16, out); }});
     }
     vs.push_back({"ldsdma", [=]() { hipLaunchKernelGGL(k_rp_ldsdma, dim3(n16 / 1024), dim3(256), 0, 0, data, n16, out); }});
     // rotation over ROT separate buffers of the same size: re-use distance
