@@ -135,8 +135,14 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
             const uint8_t* A0 = g - o;
             wlen = len < (uint32_t)WIN ? len : (uint32_t)WIN;
             const uint32_t chunks = (o + wlen + 15u) >> 4;
-            for (uint32_t k = 0; k < chunks; k++)
-                *reinterpret_cast<uint4*>(slot + 16u * k) = *reinterpret_cast<const uint4*>(A0 + 16u * k);
+            constexpr uint32_t KW = (uint32_t)WIN / 16u + 1u;  // window + alignment slack
+            uint4 v[KW];
+#pragma unroll
+            for (uint32_t k = 0; k < KW; k++)  // all loads in flight before the first LDS write
+                if (k < chunks) v[k] = *reinterpret_cast<const uint4*>(A0 + 16u * k);
+#pragma unroll
+            for (uint32_t k = 0; k < KW; k++)
+                if (k < chunks) *reinterpret_cast<uint4*>(slot + 16u * k) = v[k];
         }
     }
     // MODE 0 + RECORD: every thread stays for the coalesced copy-out

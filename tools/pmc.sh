@@ -1,16 +1,18 @@
 #!/bin/bash
 # HBM traffic per launch from PMC counters (separate passes: FETCH_SIZE and
 # WRITE_SIZE do not fit one pass on gfx950). See MI355X_MICROARCH.md §HBM.
+# Pass directories are named <workload>.<output>_<COUNTER> for tools/pmc_summary.py.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 run() { local name=$1 secs=$2; shift 2
-  timeout -k 10 "$secs" "$@" > "gpurun_out/pmc/$name.log" 2>&1; local rc=$?
-  echo "$name rc=$rc"; if [ $rc -ge 124 ]; then exit $rc; fi; }
-run list 120 rocprofv3 -L
-for wl in udp64 imix ser; do
+  timeout -s KILL "$secs" "$@" > "gpurun_out/pmc/$name.log" 2>&1; local rc=$?
+  echo "$name rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
+CONFIGS=${CONFIGS:-"udp64.desc udp64.flags udp64.record imix.desc imix.flags imix.record ser.desc"}
+for cfg in $CONFIGS; do
+  wl=${cfg%.*}; out=${cfg#*.}
   for c in FETCH_SIZE WRITE_SIZE; do
-    run ${wl}_$c 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc/${wl}_$c -o run -- python3 bench.py --workload $wl --steps 5 --warmup 1 --no-cpu-baseline
+    run ${cfg}_$c 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc/${cfg}_$c -o run -- python3 bench.py --workload $wl --out $out --steps 5 --warmup 1 --no-cpu-baseline --no-imix
   done
 done
 echo done

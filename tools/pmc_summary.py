@@ -23,7 +23,7 @@ def main():
     rows = []
     per_wl = defaultdict(lambda: {"read_bytes": 0.0, "write_bytes": 0.0, "kernels": []})
     for path in sorted(glob.glob(os.path.join(src, "*_*_SIZE", "*counter_collection.csv"))):
-        wl, counter = os.path.basename(os.path.dirname(path)).split("_", 1)
+        wl, counter = os.path.basename(os.path.dirname(path)).split("_", 1)  # <wl>[.<out>]_<COUNTER>
         vals = defaultdict(list)
         with open(path) as f:
             for r in csv.DictReader(f):
@@ -44,7 +44,8 @@ def main():
         json.dump(rows, f, indent=1)
     traffic = {}
     for wl, t in per_wl.items():
-        traffic[f"{wl}:desc"] = {
+        key = wl.replace(".", ":") if "." in wl else f"{wl}:desc"
+        traffic[key] = {
             "hbm_bytes_per_launch": int(t["read_bytes"] + t["write_bytes"]),
             "read_bytes": int(t["read_bytes"]), "write_bytes": int(t["write_bytes"]),
             "kernels": t["kernels"],
