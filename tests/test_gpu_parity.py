@@ -316,3 +316,26 @@ def test_flags_output_matches_oracle(engine, oracle, corpus):
     d8 = engine.parse(b, out_kind=abi.OUT_DESC)
     torch.cuda.synchronize()
     assert (f4.cpu().numpy().view("<u4") == d8.cpu().numpy().view(abi.DESC_DTYPE)["flags"]).all()
+
+
+def test_build_udp4_default_fields(engine, oracle):
+    """The general builder form (ports / id from the batch defaults) next to
+    the all-arrays form the udp_ping bench takes: same bytes as the oracle."""
+    import torch
+    n = 5000
+    p = engine.gen_udp4_params(n, first_index=9)
+    smac, dmac = bytes([2, 0, 0, 0, 0, 1]), bytes([2, 0, 0, 0, 0, 2])
+    host = [t.cpu().numpy() for t in p]
+    for kw, pick in (({"src_port": p[2]}, lambda i: (int(host[2][i]) & 0xFFFF, 33435, 7)),
+                     ({"dst_port": p[3], "ip_id": p[4]},
+                      lambda i: (53443, int(host[3][i]) & 0xFFFF, int(host[4][i]) & 0xFFFF)),
+                     ({}, lambda i: (53443, 33435, 7))):
+        out = engine.build_udp4(p[0], p[1], def_src_port=53443, def_dst_port=33435, def_ip_id=7,
+                                src_mac=smac, dst_mac=dmac, ttl=64, ip_flags=2, **kw)
+        torch.cuda.synchronize()
+        data = out.cpu().numpy()[: n * 42].reshape(n, 42)
+        for i in range(0, n, 31):
+            sp, dp, ident = pick(i)
+            want = oracle.build_udp4(smac, dmac, int(host[0][i]) & 0xFFFFFFFF, int(host[1][i]) & 0xFFFFFFFF,
+                                     sp, dp, ident, 64, 2, 0, b"")
+            assert bytes(data[i]) == want, (sorted(kw), i)
