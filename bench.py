@@ -110,6 +110,22 @@ def timed(step, steps, warmup, stream, device, host_clock=False):
     return elapsed, kernel_s
 
 
+def stream_ceilings(eng, batch, args, stream, device):
+    """HBM stream ceilings on the same buffer, box and timing discipline
+    (nexg_probe_stream, the parse kernels' load shape): read only, and
+    64 B read / 8 B written (the descriptor stream's shape)."""
+    import torch
+    out = torch.empty(batch.data.numel() // 8, dtype=torch.uint8, device=device)
+    nbytes = batch.data.numel() // 16384 * 16384
+    r = {}
+    for key, w8 in (("read_only_gbs", False), ("read64_write8_gbs", True)):
+        _, ks = timed(lambda: eng.probe_stream(batch.data, w8, out=out, stream=stream),
+                      args.steps, args.warmup, stream, device)
+        r[key] = round(nbytes / ks / 1e9, 1)
+    r["source"] = "nexg_probe_stream on this batch, same steps/warmup, HIP events on the launch stream"
+    return r
+
+
 def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world):
     """configs[2] beside the default configs[1] run (the metric names both
     64B and IMIX): 16M IMIX frames per GPU, same output kind, same timing
@@ -253,6 +269,9 @@ def main():
     elapsed, kernel_s = timed(step, args.steps, args.warmup, stream, device, host_clock=args.e2e)
     total_frames = dist.sum_over_ranks(F, device) * args.steps
     total_bytes = dist.sum_over_ranks(alg_bytes, device) * args.steps
+    ceilings = None
+    if args.workload == "udp64" and not args.e2e and not args.no_imix:
+        ceilings = stream_ceilings(eng, batch, args, stream, device)
     imix = None
     if args.workload == "udp64" and not args.e2e and not args.no_imix and F == 16 << 20:
         imix = imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
@@ -290,6 +309,10 @@ def main():
                                                                 args.cpu_seconds / 2, 1)
         except Exception as e:  # reported, never fatal to the GPU measurement
             res["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if ceilings is not None:
+        res["roofline"]["stream_ceilings"] = dict(
+            ceilings, frac_of_read_only=round(achieved / ceilings["read_only_gbs"], 4),
+            frac_of_read64_write8=round(achieved / ceilings["read64_write8_gbs"], 4))
     if imix is not None:
         res["imix"] = imix
     print(json.dumps(res), flush=True)

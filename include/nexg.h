@@ -241,6 +241,18 @@ int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames,
 int nexg_checksum_batch(nexg_ctx* ctx, const nexg_frames* bufs,
                         uint32_t skipword, uint16_t* out, void* stream);
 
+/* ---- calibration (not a reference entry point) ---------------------------
+ * The HBM stream ceilings the parse kernels are measured against, on the
+ * caller's own buffer and box: `bytes` (a multiple of 16384) read with the
+ * parse kernels' load shape (16-B non-temporal loads, 16-KiB tile per
+ * 256-lane workgroup). out_per_64 = 8: for every 64 B read, 8 B written
+ * (the nexg_desc stream shape): out[i] = {x, i} with x the XOR of the four
+ * 16-B chunks lane i % 256 of tile i / 256 loaded (chunks i%256 + 256k).
+ * out_per_64 = 0: read only; out[tile] = XOR of the tile's dwords (4 B per
+ * 16 KiB). bench.py reports the headline kernel against both. */
+int nexg_probe_stream(nexg_ctx* ctx, const void* data, uint64_t bytes, uint32_t out_per_64,
+                      void* out, void* stream);
+
 /* ---- serialize path (udp_ping.rs:68-109 shape) -------------------------- */
 typedef struct nexg_udp4_build {
     const uint32_t* src_ip;   /* per frame, IPv4 address as BE u32 value     */

@@ -74,6 +74,38 @@ hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStr
                                      : launch_parse_out<NEXG_OUT_RECORD>(v, a, s);
 }
 
+// calibration stream (include/nexg.h nexg_probe_stream): the parse kernels'
+// load shape with either the 8-B-per-64-B descriptor store stream or none
+template <bool W8>
+__global__ __launch_bounds__(256) void k_probe_stream(const uint8_t* data, void* out) {
+    __shared__ uint32_t s_x[4];
+    const uint32_t t = threadIdx.x;
+    const uint8_t* T = data + (uint64_t)blockIdx.x * 16384u;
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = load16<true>(T + 16u * (t + 256u * k));
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    const uint64_t i = (uint64_t)blockIdx.x * kTile + t;
+    if (W8) {
+        reinterpret_cast<uint2*>(out)[i] = make_uint2(x, (uint32_t)i);
+    } else {
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x ^= __shfl_xor(x, d, 64);
+        if ((t & 63u) == 0) s_x[t >> 6] = x;
+        __syncthreads();
+        if (t == 0) reinterpret_cast<uint32_t*>(out)[blockIdx.x] = s_x[0] ^ s_x[1] ^ s_x[2] ^ s_x[3];
+    }
+}
+
+hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, bool write8, void* out, hipStream_t s) {
+    if (tiles == 0) return hipSuccess;
+    if (write8) hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out);
+    else hipLaunchKernelGGL(k_probe_stream<false>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_checksum(const ParseArgs& a, uint32_t skipword, uint16_t* out, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const uint64_t blocks = (a.count + kTile - 1) / kTile;

@@ -339,3 +339,20 @@ def test_build_udp4_default_fields(engine, oracle):
             want = oracle.build_udp4(smac, dmac, int(host[0][i]) & 0xFFFFFFFF, int(host[1][i]) & 0xFFFFFFFF,
                                      sp, dp, ident, 64, 2, 0, b"")
             assert bytes(data[i]) == want, (sorted(kw), i)
+
+
+def test_probe_stream(engine):
+    """nexg_probe_stream (calibration): both output shapes against numpy."""
+    import torch
+    rng = np.random.default_rng(5)
+    host = rng.integers(0, 256, 3 * 16384, dtype=np.uint8)
+    data = torch.from_numpy(host).cuda()
+    w = host.view("<u4").reshape(3, 4, 256, 4)  # tile, k, lane, dword
+    lane_x = np.bitwise_xor.reduce(np.bitwise_xor.reduce(w, axis=3), axis=1)  # tile, lane
+    o8 = engine.probe_stream(data, True)
+    torch.cuda.synchronize()
+    got = o8.cpu().numpy().view("<u4").reshape(-1, 2)
+    assert (got[:, 0] == lane_x.reshape(-1)).all() and (got[:, 1] == np.arange(768)).all()
+    o0 = engine.probe_stream(data, False)
+    torch.cuda.synchronize()
+    assert (o0.cpu().numpy().view("<u4")[:3] == np.bitwise_xor.reduce(lane_x, axis=1)).all()
