@@ -123,6 +123,13 @@ def stream_ceilings(eng, batch, args, stream, device):
                       args.steps, args.warmup, stream, device)
         r[key] = round(nbytes / ks / 1e9, 1)
     r["source"] = "nexg_probe_stream on this batch, same steps/warmup, HIP events on the launch stream"
+    if args.out == "desc":  # the same parse with the 4-B flags output (NEXG_OUT_FLAGS)
+        from nex_amd import abi
+        _, ks = timed(lambda: eng.parse(batch, out_kind=abi.OUT_FLAGS, out=out, stream=stream),
+                      args.steps, args.warmup, stream, device)
+        ach = batch.total_bytes / ks / 1e9
+        r["flags_output"] = {"kernel_ms": round(ks * 1e3, 4), "achieved": round(ach, 1),
+                             "frac": round(ach / HBM_PEAK_GBS, 4)}
     return r
 
 
