@@ -143,9 +143,11 @@ def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
     out = torch.empty(F * width, dtype=torch.uint8, device=device)
     torch.cuda.synchronize(device)
     alg = batch.total_bytes
+    # a freshly generated 6-GB batch runs its first ~20 launches 5-25 % slow
+    # (profiles/r01_staging/imix_ramp.txt), so the IMIX line warms up longer
     steps = max(1, args.steps // 2)
     elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
-                              steps, max(1, args.warmup // 2), stream, device)
+                              steps, max(20, args.warmup), stream, device)
     frames = dist.sum_over_ranks(F, device) * steps
     nbytes = dist.sum_over_ranks(alg, device) * steps
     if rank != 0:

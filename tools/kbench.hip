@@ -74,6 +74,78 @@ __global__ __launch_bounds__(256) void k_lanedirect(const uint8_t* data, uint64_
 }
 
 
+// Ablation of k_parse_span's streaming skeleton on the same packed batch:
+// LEVEL 0 = stage each 16-KiB sub-tile into LDS (+ chunk sums) with the next
+// one in flight, one barrier; 1 = + the block scan and its two barriers;
+// 2 = + the head-window copy and the 4th barrier. One 8-B result per frame.
+template <int LEVEL>
+__global__ __launch_bounds__(256) void k_span_skeleton(ParseArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t sb[16384];
+    __shared__ __attribute__((aligned(16))) uint32_t sp[1028];
+    __shared__ uint32_t s_wsum[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint64_t f0 = (uint64_t)blockIdx.x * 256;
+    const uint64_t nf = a.count - f0 < 256 ? a.count - f0 : 256;
+    const uint64_t base = reinterpret_cast<uint64_t>(a.data);
+    const uint64_t lo = a.offsets[f0], hi = a.offsets[f0 + nf];
+    const uint64_t off = t < nf ? a.offsets[f0 + t] : lo;
+    const uint64_t A0 = (base + lo) & ~15ull;
+    const uint32_t span = (uint32_t)(((base + hi + 15u) & ~15ull) - A0);
+    const uint32_t hr = (uint32_t)(base + off - A0);
+    uint4 cur[4];
+    auto fetch = [&](uint32_t S) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t c = S + 16u * (t + 256u * i);
+            cur[i] = c < span ? load16<true>(reinterpret_cast<const void*>(A0 + c)) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    fetch(0);
+    uint32_t acc = 0, run = 0, w[20];
+#pragma unroll
+    for (int j = 0; j < 20; j++) w[j] = 0;
+    for (uint32_t S = 0; S < span; S += 16384) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t c = t + 256u * i;
+            *reinterpret_cast<uint4*>(sb + 16u * c) = cur[i];
+            sp[c] = chunk_le_sum(cur[i]);
+        }
+        if (S + 16384 < span) fetch(S + 16384);
+        __syncthreads();
+        if (LEVEL >= 1) {
+            uint32_t cs[4], own = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) own += (cs[i] = sp[4 * t + i]);
+            const uint32_t incl = wave_incl_scan_dpp(own);
+            if (lane == 63u) s_wsum[wv] = incl;
+            __syncthreads();
+            const uint4 ws = *reinterpret_cast<const uint4*>(s_wsum);
+            uint32_t ex = (wv > 0 ? ws.x : 0u) + (wv > 1 ? ws.y : 0u) + (wv > 2 ? ws.z : 0u) + incl - own;
+#pragma unroll
+            for (int i = 0; i < 4; i++) { sp[4 * t + i] = ex; ex += cs[i]; }
+            run += ws.x + ws.y + ws.z + ws.w;
+            __syncthreads();
+        } else {
+            acc += sp[(t * 7u) & 1023u];
+        }
+        if (LEVEL >= 2) {
+            const uint32_t dh = hr - S;
+            if (dh <= 16384u - 80u) {
+#pragma unroll
+                for (int j = 0; j < 20; j++) w[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4u * j);
+            }
+            __syncthreads();
+        } else if (LEVEL == 0) {
+            __syncthreads();
+        }
+    }
+    uint32_t x = acc ^ run;
+#pragma unroll
+    for (int j = 0; j < 20; j++) x ^= w[j];
+    if (t < nf) reinterpret_cast<uint2*>(a.out)[f0 + t] = make_uint2(x, 0);
+}
+
 struct Var {
     std::string name;
     std::function<void()> run;
@@ -164,6 +236,9 @@ int main(int argc, char** argv) {
     ivars.push_back({"imix_span_rec", [=]() {
         ParseArgs r2 = ia; r2.out = rec;
         hipLaunchKernelGGL((k_parse_span<NEXG_OUT_RECORD, 1>), grid, blk, 0, 0, r2); }, ibytes});
+    ivars.push_back({"ABL_span_stage", iparse(k_span_skeleton<0>), ibytes});
+    ivars.push_back({"ABL_span_stage_scan", iparse(k_span_skeleton<1>), ibytes});
+    ivars.push_back({"ABL_span_stage_scan_head", iparse(k_span_skeleton<2>), ibytes});
     ivars.push_back({"ABL_tails_only_u4", [=]() { hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia); }, ibytes});
     ivars.push_back({"ABL_lane80_only", [=]() { hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
     hipLaunchKernelGGL((k_parse<1, NEXG_OUT_DESC, 0, 128>), grid, blk, 0, 0, ParseArgs{idata, ho[icount], ioff, nullptr, 0, icount, 0, 0, ref});
