@@ -198,5 +198,5 @@ EXPORTED_SYMBOLS = (
     "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch", "nexg_probe_stream",
     "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_build_tcp_batch",
     "nexg_build_icmp_echo_batch", "nexg_pcap_open", "nexg_pcap_linktype", "nexg_pcap_last_error",
-    "nexg_pcap_read_batch", "nexg_pcap_read_raw", "nexg_pcap_close", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
+    "nexg_pcap_read_batch", "nexg_pcap_read_raw", "nexg_pcap_set_read_threads", "nexg_pcap_close", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
 )

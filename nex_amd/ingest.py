@@ -82,6 +82,12 @@ class PcapReader:
             for a, b in zip(offs[:-1], offs[1:]):
                 yield bytes(data[int(a):int(b)])
 
+    def set_read_threads(self, threads: int):
+        """Split read_raw's file reads over `threads` parallel preads."""
+        rc = self.lib.nexg_pcap_set_read_threads(self.h, threads)
+        if rc != abi.OK:
+            raise PcapError(f"invalid thread count {threads}")
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.nexg_pcap_close(self.h)

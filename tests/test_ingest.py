@@ -185,3 +185,29 @@ def test_malformed_captures_are_memory_safe(tmp_path, frames):
                        timeout=300, env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
                                              UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1"))
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("threads", [2, 5])
+def test_raw_shape_parallel_reads(tmp_path, frames, threads):
+    """nexg_pcap_set_read_threads: read_raw's parallel preads (>= 4-MiB
+    pieces) deliver exactly the sequential reader's frames, chunk edges and
+    carries included, on a ~22 MB classic capture and on pcapng."""
+    from nex_amd.ingest import raw_frames
+    rep = frames * (22_000_000 // sum(len(f) for f in frames) + 1)
+    for name, blob in (("big.pcap", pcapfile.classic(rep)),
+                       ("big.pcapng", pcapfile.ng_shb() + pcapfile.ng_idb(1) +
+                        b"".join(pcapfile.ng_epb(f, i) for i, f in enumerate(rep[:20000])))):
+        path = _write(tmp_path, name, blob)
+        with PcapReader(path) as r:
+            want = list(raw_frames(r, cap=9 << 20, max_frames=1 << 16))
+        for cap in (9 << 20, 17 << 20 | 5):
+            with PcapReader(path) as r:
+                r.set_read_threads(threads)
+                got = list(raw_frames(r, cap=cap, max_frames=1 << 16))
+            assert got == want, (name, cap)
+        with PcapReader(path) as r:  # the setting leaves the packed shape unchanged
+            r.set_read_threads(threads)
+            assert list(r.frames()) == want, name
+    with PcapReader(path) as r:
+        with pytest.raises(PcapError):
+            r.set_read_threads(0)

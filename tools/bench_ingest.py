@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--shape", choices=["raw", "packed"], default="packed",
                     help="raw: file bytes read straight into pinned staging, frames in place "
                          "(offsets + lengths); packed: records copied back to back (offsets only)")
+    ap.add_argument("--threads", type=int, default=1,
+                    help="raw shape: parallel preads per file chunk (nexg_pcap_set_read_threads)")
     args = ap.parse_args()
 
     import numpy as np
@@ -103,6 +105,8 @@ def main():
     def run_once():
         stats["read_s"] = 0.0
         r = PcapReader(path)
+        if args.threads > 1:
+            r.set_read_threads(args.threads)
         free = [threading.Semaphore(1) for _ in range(nbuf)]  # staging slot reusable
         ready = [threading.Semaphore(0) for _ in range(nbuf)]
         counts = [0] * nbuf
@@ -185,7 +189,9 @@ def main():
         "gib_s": round(total_bytes / best / 2**30, 3), "frames": args.frames, "bytes": total_bytes,
         "workload": args.workload, "batch_frames": B, "shape": args.shape, "seconds": round(best, 4),
         "frames_ok": ok, "pcap_write_s": round(wr, 2), "reader_busy_s": round(stats["read_s"], 4),
-        "note": "one reader thread (file read from the page cache + copy into pinned staging), "
+        "read_threads": args.threads,
+        "note": "one reader thread (file read from the page cache + copy into pinned staging; "
+                "raw shape: split over read_threads parallel preads), "
                 "H2D / parse / D2H on two streams, reader one batch ahead"}))
 
 
