@@ -20,7 +20,7 @@ if [[ $STEPS == *smoke* || $STEPS == all ]]; then
   step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ $STEPS == *pytest* || $STEPS == all ]]; then
-  step pytest_gpu 900 python -m pytest tests -q -m gpu -x
+  step pytest_gpu 900 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread
 fi
 if [[ $STEPS == *bench* || $STEPS == all ]]; then
   step bench_udp64 400 python bench.py --steps 50 --warmup 5 --cpu-seconds 5
