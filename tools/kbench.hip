@@ -146,6 +146,45 @@ __global__ __launch_bounds__(256) void k_span_skeleton(ParseArgs a) {
     if (t < nf) reinterpret_cast<uint2*>(a.out)[f0 + t] = make_uint2(x, 0);
 }
 
+// One-shot chunk skeleton: a workgroup per 16-KiB chunk of the packed byte
+// stream (all four loads per lane in flight at once), LDS staging + chunk
+// sums + block scan as in k_parse_span, 8 B written per 512 B read (near the
+// IMIX descriptor ratio). Premise check for a chunk-decomposed IMIX kernel.
+__global__ __launch_bounds__(256) void k_chunk_skeleton(const uint8_t* data, uint64_t nchunks, uint2* out) {
+    __shared__ __attribute__((aligned(16))) uint8_t sb[16384];
+    __shared__ __attribute__((aligned(16))) uint32_t sp[1028];
+    __shared__ uint32_t s_wsum[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint8_t* T = data + (uint64_t)blockIdx.x * 16384u;
+    uint4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = load16<true>(T + 16u * (t + 256u * i));
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t c = t + 256u * i;
+        *reinterpret_cast<uint4*>(sb + 16u * c) = v[i];
+        sp[c] = chunk_le_sum(v[i]);
+    }
+    __syncthreads();
+    uint32_t cs[4], own = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) own += (cs[i] = sp[4 * t + i]);
+    const uint32_t incl = wave_incl_scan_dpp(own);
+    if (lane == 63u) s_wsum[wv] = incl;
+    __syncthreads();
+    const uint4 ws = *reinterpret_cast<const uint4*>(s_wsum);
+    uint32_t ex = (wv > 0 ? ws.x : 0u) + (wv > 1 ? ws.y : 0u) + (wv > 2 ? ws.z : 0u) + incl - own;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { sp[4 * t + i] = ex; ex += cs[i]; }
+    __syncthreads();
+    if (t < 32) {  // 32 results x 8 B per 16 KiB (the caller's out holds nchunks x 32)
+        uint32_t x = sp[(t * 32u) & 1023u];
+#pragma unroll
+        for (int j = 0; j < 20; j++) x ^= *reinterpret_cast<const uint32_t*>(sb + 512u * t + 4u * j);
+        out[(uint64_t)blockIdx.x * 32 + t] = make_uint2(x, 0);
+    }
+}
+
 struct Var {
     std::string name;
     std::function<void()> run;
@@ -239,6 +278,7 @@ int main(int argc, char** argv) {
     ivars.push_back({"ABL_span_stage", iparse(k_span_skeleton<0>), ibytes});
     ivars.push_back({"ABL_span_stage_scan", iparse(k_span_skeleton<1>), ibytes});
     ivars.push_back({"ABL_span_stage_scan_head", iparse(k_span_skeleton<2>), ibytes});
+    ivars.push_back({"ABL_chunk_oneshot", [=]() { hipLaunchKernelGGL(k_chunk_skeleton, dim3((uint32_t)(ho[icount] / 16384)), blk, 0, 0, idata, ho[icount] / 16384, out); }, (double)(ho[icount] / 16384 * 16384)});
     ivars.push_back({"ABL_tails_only_u4", [=]() { hipLaunchKernelGGL((k_tail_sums<NEXG_OUT_DESC, 4>), grid, blk, 0, 0, ia); }, ibytes});
     ivars.push_back({"ABL_lane80_only", [=]() { hipLaunchKernelGGL(k_parse_lane80<NEXG_OUT_DESC>, grid, blk, 0, 0, ia); }, ibytes});
     hipLaunchKernelGGL((k_parse<1, NEXG_OUT_DESC, 0, 128>), grid, blk, 0, 0, ParseArgs{idata, ho[icount], ioff, nullptr, 0, icount, 0, 0, ref});
