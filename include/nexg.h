@@ -241,6 +241,33 @@ int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames,
 int nexg_checksum_batch(nexg_ctx* ctx, const nexg_frames* bufs,
                         uint32_t skipword, uint16_t* out, void* stream);
 
+/* ---- option lists ---------------------------------------
+ * The Vec fields of Frame's headers, decoded on the device into fixed-capacity
+ * arrays: Ipv4Header.options (ipv4.rs:442-508: EOL is kept and ends the list,
+ * NOP is kept, an option without room for its length / with length < 2 / past
+ * the header ends the walk) and TcpHeader.options (tcp.rs:767-818). Option k
+ * starts at frame byte ip_opt_off + ip_pos[k] (tcp_opt_off + tcp_pos[k]); its
+ * type/kind is that byte; EOL and NOP (IPv4: number = byte & 0x1f in {0, 1};
+ * TCP: kind in {0, 1}) are one byte long, every other option's length is the
+ * next byte and its data the length - 2 bytes after that. Counts are 0 for an
+ * absent header (nexg_record flags); they equal the record's ip_nopt /
+ * l4_nopt. An options area is at most 40 bytes, so 40 entries always suffice. */
+typedef struct nexg_options {
+    uint8_t n_ip;          /* Ipv4Header.options.len()                       */
+    uint8_t n_tcp;         /* TcpHeader.options.len()                        */
+    uint16_t ip_opt_off;   /* frame offset of the IPv4 options (l3_off + 20) */
+    uint16_t tcp_opt_off;  /* frame offset of the TCP options (l4_off + 20)  */
+    uint16_t reserved;
+    uint8_t ip_pos[40];
+    uint8_t tcp_pos[40];
+    uint8_t pad[8];
+} nexg_options;
+
+/* Option lists for a batch already parsed with NEXG_OUT_RECORD (any parse
+ * mode): records[i] must be frame i's record. Device pointers, stream-ordered. */
+int nexg_decode_options(nexg_ctx* ctx, const nexg_frames* frames, const nexg_record* records,
+                        nexg_options* out, void* stream);
+
 /* ---- calibration (not a reference entry point) ---------------------------
  * The HBM stream ceilings the parse kernels are measured against, on the
  * caller's own buffer and box: `bytes` (a multiple of 16384) read with the

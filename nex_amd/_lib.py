@@ -42,6 +42,7 @@ def load():
         "nexg_parse_batch": (I, [P, ctypes.POINTER(abi.Frames), ctypes.POINTER(abi.ParseOptionC), I, P, P]),
         "nexg_checksum_batch": (I, [P, ctypes.POINTER(abi.Frames), U32, P, P]),
         "nexg_probe_stream": (I, [P, P, U64, U32, P, P]),
+        "nexg_decode_options": (I, [P, ctypes.POINTER(abi.Frames), P, P, P]),
         "nexg_build_udp4_batch": (I, [P, ctypes.POINTER(abi.Udp4Build), P, U32, P]),
         "nexg_build_udp6_batch": (I, [P, ctypes.POINTER(abi.Udp6Build), P, U32, P]),
         "nexg_build_tcp_batch": (I, [P, ctypes.POINTER(abi.TcpBuild), P, U32, P]),

@@ -73,6 +73,9 @@ SLICE_DTYPE = np.dtype([("flags", "<u4"), ("l3_off", "<u2"), ("l3_len", "<u2"), 
                         ("payload_off", "<u2"), ("payload_len", "<u2"), ("ethertype", "<u2")])
 assert SLICE_DTYPE.itemsize == 16
 FLAGS_DTYPE = np.dtype([("flags", "<u4")])
+OPTIONS_DTYPE = np.dtype([("n_ip", "u1"), ("n_tcp", "u1"), ("ip_opt_off", "<u2"), ("tcp_opt_off", "<u2"),
+                          ("reserved", "<u2"), ("ip_pos", "u1", 40), ("tcp_pos", "u1", 40), ("pad", "u1", 8)])
+assert OPTIONS_DTYPE.itemsize == 96
 
 RECORD_DTYPE = np.dtype([
     ("flags", "<u4"), ("payload_off", "<u2"), ("payload_len", "<u2"),
@@ -195,7 +198,7 @@ class IcmpEchoBuild(ctypes.Structure):
 #: every symbol include/nexg.h declares (tests check the .so exports them)
 EXPORTED_SYMBOLS = (
     "nexg_abi_version", "nexg_strerror", "nexg_ctx_create", "nexg_ctx_destroy",
-    "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch", "nexg_probe_stream",
+    "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch", "nexg_decode_options", "nexg_probe_stream",
     "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_build_tcp_batch",
     "nexg_build_icmp_echo_batch", "nexg_pcap_open", "nexg_pcap_linktype", "nexg_pcap_last_error",
     "nexg_pcap_read_batch", "nexg_pcap_read_raw", "nexg_pcap_set_read_threads", "nexg_pcap_close", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",

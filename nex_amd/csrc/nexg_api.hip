@@ -123,6 +123,18 @@ int nexg_checksum_batch(nexg_ctx* ctx, const nexg_frames* bufs, uint32_t skipwor
                       NEXG_ELAUNCH);
 }
 
+int nexg_decode_options(nexg_ctx* ctx, const nexg_frames* frames, const nexg_record* records,
+                        nexg_options* out, void* stream) {
+    if (!ctx) return NEXG_EINVAL;
+    if (!frames_valid(frames)) return fail(ctx, NEXG_EINVAL, "invalid frame batch%s", nullptr);
+    if (frames->count && (!records || !out)) return fail(ctx, NEXG_EINVAL, "NULL records or output%s", nullptr);
+    if ((reinterpret_cast<uint64_t>(out) & 15u) != 0 || (reinterpret_cast<uint64_t>(records) & 15u) != 0)
+        return fail(ctx, NEXG_EINVAL, "misaligned records or output%s", nullptr);
+    const nexg::ParseArgs a = to_args(frames);
+    return hip_status(ctx, nexg::launch_decode_options(a, records, out, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
 int nexg_probe_stream(nexg_ctx* ctx, const void* data, uint64_t bytes, uint32_t out_per_64,
                       void* out, void* stream) {
     if (!ctx) return NEXG_EINVAL;

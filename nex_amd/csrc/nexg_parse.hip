@@ -74,6 +74,81 @@ hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStr
                                      : launch_parse_out<NEXG_OUT_RECORD>(v, a, s);
 }
 
+// nexg_decode_options: Ipv4Header.options (ipv4.rs:442-508) and
+// TcpHeader.options (tcp.rs:767-818) of each frame as positions, one lane per
+// frame, over the headers its record (a prior NEXG_OUT_RECORD parse) locates.
+// Not a hot path: byte loads, the 96-B result assembled in private memory.
+static_assert(sizeof(nexg_options) == 96, "nexg_options is 96 bytes (include/nexg.h)");
+
+__global__ __launch_bounds__(256) void k_decode_options(ParseArgs a, const nexg_record* recs,
+                                                        nexg_options* out) {
+    const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
+    if (idx >= a.count) return;
+    nexg_options o;
+    __builtin_memset(&o, 0, sizeof(o));
+    const nexg_record& r = recs[idx];
+    const uint32_t flags = r.flags;
+    uint64_t off;
+    uint32_t len;
+    if (frame_extent(a, idx, off, len) && ((flags >> NEXG_STATUS_SHIFT) & 7u) == 0) {
+        const uint8_t* g = a.data + off;
+        const uint32_t l3 = r.l3_off, ihl4 = 4u * (r.ip_ver_ihl & 0xFu);
+        if ((flags & NEXG_L_IPV4) && l3 + ihl4 <= len) {
+            const uint8_t* h = g + l3;
+            uint32_t i = 20, n = 0;
+            while (i < ihl4) {
+                const uint32_t num = h[i] & 0x1Fu;
+                if (num <= 1u) {  // EOL ends the list, NOP is one byte
+                    o.ip_pos[n++] = (uint8_t)(i - 20u);
+                    if (num == 0u) break;
+                    i += 1;
+                    continue;
+                }
+                if (i + 2 > ihl4) break;
+                const uint32_t l = h[i + 1];
+                if (l < 2 || i + l > ihl4) break;
+                o.ip_pos[n++] = (uint8_t)(i - 20u);
+                i += l;
+            }
+            o.n_ip = (uint8_t)n;
+            o.ip_opt_off = (uint16_t)(l3 + 20u);
+        }
+        const uint32_t l4 = r.l4_off, hl = 4u * (r.l4_code >> 4);
+        if ((flags & NEXG_L_TCP) && l4 + hl <= len) {
+            const uint8_t* h = g + l4;
+            uint32_t p = 20, n = 0;
+            while (p < hl) {
+                const uint32_t start = p, kind = h[p++];
+                if (kind <= 1u) {
+                    o.tcp_pos[n++] = (uint8_t)(start - 20u);
+                    if (kind == 0u) break;
+                    continue;
+                }
+                if (p >= hl) break;
+                const uint32_t l = h[p++];
+                if (l < 2 || p + (l - 2) > hl) break;
+                o.tcp_pos[n++] = (uint8_t)(start - 20u);
+                p += l - 2;
+            }
+            o.n_tcp = (uint8_t)n;
+            o.tcp_opt_off = (uint16_t)(l4 + 20u);
+        }
+    }
+    uint4 v[6];
+    __builtin_memcpy(v, &o, sizeof(o));
+    uint4* dst = reinterpret_cast<uint4*>(out + idx);
+#pragma unroll
+    for (int k = 0; k < 6; k++) dst[k] = v[k];
+}
+
+hipError_t launch_decode_options(const ParseArgs& a, const nexg_record* recs, nexg_options* out,
+                                 hipStream_t s) {
+    if (a.count == 0) return hipSuccess;
+    const uint64_t blocks = (a.count + kTile - 1) / kTile;
+    hipLaunchKernelGGL(k_decode_options, dim3((uint32_t)blocks), dim3(kTile), 0, s, a, recs, out);
+    return hipGetLastError();
+}
+
 // calibration stream (include/nexg.h nexg_probe_stream): the parse kernels'
 // load shape with either the 8-B-per-64-B descriptor store stream or none
 template <bool W8>

@@ -181,6 +181,17 @@ class Engine:
               abi.OUT_SLICE: abi.SLICE_DTYPE, abi.OUT_FLAGS: abi.FLAGS_DTYPE}[out_kind]
         return out.cpu().numpy()[: batch.count * dt.itemsize].view(dt)
 
+    def decode_options(self, batch: FrameBatch, records, stream=None):
+        """Ipv4Header.options / TcpHeader.options of every frame as positions
+        (nexg_decode_options; ipv4.rs:442-508, tcp.rs:767-818). `records` is
+        the uint8 device tensor a NEXG_OUT_RECORD parse of `batch` returned."""
+        torch = _torch()
+        out = torch.empty(max(batch.count, 1) * 96, dtype=torch.uint8, device=self.torch_device)
+        fr = batch.to_c()
+        self._check(self.lib.nexg_decode_options(self.ctx, ctypes.byref(fr), _ptr(records), _ptr(out),
+                                                 self._stream(stream)))
+        return out
+
     def probe_stream(self, data, write8: bool, out=None, stream=None):
         """Calibration stream over a uint8 device tensor (nexg_probe_stream):
         the parse kernels' load shape, read-only or with the 8-B-per-64-B

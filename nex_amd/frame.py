@@ -239,9 +239,38 @@ def _tcp_options(b, base, hl):
     return out
 
 
-def frame_from_record(rec, frame: bytes) -> Frame:
+def ipv4_options_at(b, opt_off: int, positions) -> List[Tuple[int, int, int, Optional[int], bytes]]:
+    """Ipv4Header.options from nexg_options positions (the device's walk)."""
+    out = []
+    for p in positions:
+        t = b[opt_off + int(p)]
+        num = t & 0x1F
+        if num in (0, 1):
+            out.append(((t >> 7) & 1, (t >> 5) & 3, num, None, b""))
+        else:
+            ln = b[opt_off + int(p) + 1]
+            out.append(((t >> 7) & 1, (t >> 5) & 3, num, ln, bytes(b[opt_off + int(p) + 2:opt_off + int(p) + ln])))
+    return out
+
+
+def tcp_options_at(b, opt_off: int, positions) -> List[Tuple[int, Optional[int], bytes]]:
+    """TcpHeader.options from nexg_options positions (the device's walk)."""
+    out = []
+    for p in positions:
+        kind = b[opt_off + int(p)]
+        if kind in (0, 1):
+            out.append((kind, None, b""))
+        else:
+            ln = b[opt_off + int(p) + 1]
+            out.append((kind, ln, bytes(b[opt_off + int(p) + 2:opt_off + int(p) + ln])))
+    return out
+
+
+def frame_from_record(rec, frame: bytes, options=None) -> Frame:
     """Materialise frame::Frame from a nexg_record and the frame bytes.
 
+    `options` (a nexg_options from Engine.decode_options) supplies the option
+    lists as the device decoded them; without it they are walked here.
     Raises the ParseError subclass the reference would return."""
     flags = int(rec["flags"])
     st = (flags >> abi.STATUS_SHIFT) & 7
@@ -272,7 +301,9 @@ def frame_from_record(rec, frame: bytes) -> Frame:
                             int(rec["ip_ttl"]), int(rec["ip_proto"]), int(rec["ip_csum"]),
                             ipaddress.IPv4Address(int(rec["ip_src"])),
                             ipaddress.IPv4Address(int(rec["ip_dst"])),
-                            _ipv4_options(b, l3, ihl))
+                            _ipv4_options(b, l3, ihl) if options is None else
+                            ipv4_options_at(b, int(options["ip_opt_off"]),
+                                            options["ip_pos"][:int(options["n_ip"])]))
         if flags & abi.L_IPV6:
             v6 = Ipv6Header(6, int(rec["ip_tos"]), int(rec["ip_word"]), int(rec["ip_length"]),
                             int(rec["ip_proto"]), int(rec["ip_ttl"]),
@@ -293,7 +324,9 @@ def frame_from_record(rec, frame: bytes) -> Frame:
             tcp = TcpHeader(int(rec["src_port"]), int(rec["dst_port"]), int(rec["tcp_seq"]),
                             int(rec["tcp_ack"]), oc >> 4, oc & 15, int(rec["l4_type"]),
                             int(rec["tcp_window"]), int(rec["l4_csum"]), int(rec["tcp_urg"]),
-                            _tcp_options(b, l4, int(rec["l4_length"])))
+                            _tcp_options(b, l4, int(rec["l4_length"])) if options is None else
+                            tcp_options_at(b, int(options["tcp_opt_off"]),
+                                           options["tcp_pos"][:int(options["n_tcp"])]))
         if flags & abi.L_UDP:
             udp = UdpHeader(int(rec["src_port"]), int(rec["dst_port"]), int(rec["l4_length"]),
                             int(rec["l4_csum"]))

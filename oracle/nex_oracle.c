@@ -130,6 +130,7 @@ typedef struct {
     int has_length;
     uint8_t length;
     size_t data_off, data_len; /* into the packet bytes */
+    size_t start;              /* offset of the option's type byte in the header */
 } ipv4_option;
 
 typedef struct {
@@ -168,11 +169,11 @@ static int parse_ipv4(const uint8_t* bytes, size_t len, int strict, ipv4_packet*
         uint8_t copied = (b >> 7) & 1, klass = (b >> 5) & 3, number = b & 0x1F;
         ipv4_option* o = &pk->options[pk->noptions];
         if (number == 0) { /* EOL */
-            *o = (ipv4_option){copied, klass, number, 0, 0, 0, 0};
+            *o = (ipv4_option){copied, klass, number, 0, 0, 0, 0, i};
             pk->noptions++;
             break;
         } else if (number == 1) { /* NOP */
-            *o = (ipv4_option){copied, klass, number, 0, 0, 0, 0};
+            *o = (ipv4_option){copied, klass, number, 0, 0, 0, 0, i};
             pk->noptions++;
             i += 1;
         } else {
@@ -185,7 +186,7 @@ static int parse_ipv4(const uint8_t* bytes, size_t len, int strict, ipv4_packet*
                 if (strict) return NEXG_ERR_INVALID_LENGTH;
                 break;
             }
-            *o = (ipv4_option){copied, klass, number, 1, (uint8_t)l, i + 2, l - 2};
+            *o = (ipv4_option){copied, klass, number, 1, (uint8_t)l, i + 2, l - 2, i};
             pk->noptions++;
             i += l;
         }
@@ -336,6 +337,7 @@ typedef struct {
     int has_length;
     uint8_t length;
     size_t data_off, data_len;
+    size_t start; /* offset of the option's kind byte in the header */
 } tcp_option;
 
 typedef struct {
@@ -372,11 +374,11 @@ static int parse_tcp(const uint8_t* bytes, size_t len, tcp_packet* pk) {
         offset += 1;
         tcp_option* o = &pk->options[pk->noptions];
         if (kind == 0) {
-            *o = (tcp_option){kind, 0, 0, 0, 0};
+            *o = (tcp_option){kind, 0, 0, 0, 0, offset - 1};
             pk->noptions++;
             break;
         } else if (kind == 1) {
-            *o = (tcp_option){kind, 0, 0, 0, 0};
+            *o = (tcp_option){kind, 0, 0, 0, 0, offset - 1};
             pk->noptions++;
         } else {
             if (offset >= header_len) return NEXG_ERR_MALFORMED;
@@ -385,7 +387,7 @@ static int parse_tcp(const uint8_t* bytes, size_t len, tcp_packet* pk) {
             if (l < 2) return NEXG_ERR_INVALID_LENGTH;
             size_t data_len = (size_t)l - 2;
             if (offset + data_len > header_len) return NEXG_ERR_TRUNCATED;
-            *o = (tcp_option){kind, 1, l, offset, data_len};
+            *o = (tcp_option){kind, 1, l, offset, data_len, offset - 2};
             pk->noptions++;
             offset += data_len;
         }
@@ -697,6 +699,36 @@ void nexo_record_to_desc(const nexg_record* rec, nexg_desc* d) {
     d->flags = rec->flags;
     d->payload_off = rec->payload_off;
     d->payload_len = rec->payload_len;
+}
+
+/* The option lists of the Frame nexo_parse_frame yields: Ipv4Header.options
+ * (ipv4.rs:442-508) and TcpHeader.options (tcp.rs:767-818), re-walked by the
+ * same parse_ipv4 / parse_tcp over the headers the record locates, as
+ * positions into the options areas (include/nexg.h nexg_options). */
+void nexo_decode_options(const uint8_t* fr, size_t len, uint32_t flags, uint32_t ip_offset,
+                         nexg_options* out) {
+    nexg_record rec;
+    nexo_parse_frame(fr, len, flags, ip_offset, &rec);
+    memset(out, 0, sizeof(*out));
+    if (NEXG_STATUS(rec.flags) != 0) return;
+    const int strict = (flags & NEXG_PARSE_STRICT) != 0;
+    if (rec.flags & NEXG_L_IPV4) {
+        ipv4_packet pk;
+        if (parse_ipv4(fr + rec.l3_off, len - rec.l3_off, strict, &pk) == 0) {
+            out->n_ip = (uint8_t)pk.noptions;
+            out->ip_opt_off = (uint16_t)(rec.l3_off + 20);
+            for (int k = 0; k < pk.noptions; k++) out->ip_pos[k] = (uint8_t)(pk.options[k].start - 20);
+        }
+    }
+    if (rec.flags & NEXG_L_TCP) {
+        tcp_packet pk;
+        const size_t hl = (size_t)(rec.l4_code >> 4) * 4u;
+        if (parse_tcp(fr + rec.l4_off, hl, &pk) == 0) {
+            out->n_tcp = (uint8_t)pk.noptions;
+            out->tcp_opt_off = (uint16_t)(rec.l4_off + 20);
+            for (int k = 0; k < pk.noptions; k++) out->tcp_pos[k] = (uint8_t)(pk.options[k].start - 20);
+        }
+    }
 }
 
 /* ---- batch ------------------------------------------------------------ */

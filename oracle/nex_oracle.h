@@ -54,6 +54,10 @@ uint16_t nexo_ipv6_checksum(const uint8_t* data, size_t len, size_t skipword,
 void nexo_parse_frame(const uint8_t* frame, size_t len, uint32_t flags,
                       uint32_t ip_offset, nexg_record* rec);
 void nexo_record_to_desc(const nexg_record* rec, nexg_desc* desc);
+/* Ipv4Header.options / TcpHeader.options of the same Frame as positions
+ * (include/nexg.h nexg_options; ipv4.rs:442-508, tcp.rs:767-818). */
+void nexo_decode_options(const uint8_t* frame, size_t len, uint32_t flags,
+                         uint32_t ip_offset, nexg_options* out);
 
 /* Batch form over a host-memory nexg_frames layout (pointers are HOST). */
 int nexo_parse_batch(const nexg_frames* frames, uint32_t flags,

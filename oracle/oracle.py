@@ -48,6 +48,8 @@ def lib():
         L.nexo_build_udp4.argtypes = [P, P, U32, U32, U16, U16, U16, ctypes.c_uint8, ctypes.c_uint8,
                                       ctypes.c_uint8, P, U32, P]
         L.nexo_slice_frame.restype = None
+        L.nexo_decode_options.argtypes = [P, ctypes.c_size_t, U32, U32, P]
+        L.nexo_decode_options.restype = None
         L.nexo_slice_frame.argtypes = [P, ctypes.c_size_t, U32, U32, P]
         L.nexo_slice_batch.restype = None
         L.nexo_slice_batch.argtypes = [ctypes.POINTER(abi.Frames), U32, U32, P]
@@ -123,6 +125,14 @@ def parse_packed(data: np.ndarray, offsets=None, lengths=None, stride=0, flags=0
     recs = np.zeros(count, dtype=abi.RECORD_DTYPE)
     lib().nexo_parse_batch(ctypes.byref(fr), flags, ip_offset, recs.ctypes.data, None, nthreads)
     return recs
+
+
+def decode_options(frame: bytes, flags=0, ip_offset=0):
+    """Option lists of the Frame (ipv4.rs:442-508, tcp.rs:767-818) -> one nexg_options."""
+    out = np.zeros(1, dtype=abi.OPTIONS_DTYPE)
+    b, n = _buf(frame)
+    lib().nexo_decode_options(b, n, flags, ip_offset, out.ctypes.data)
+    return out[0]
 
 
 def slice_frame(frame: bytes, flags=0, ip_offset=0):
