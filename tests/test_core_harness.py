@@ -3,6 +3,8 @@ kernels run) executed on the host via tests/native/core_harness.hip, checked
 bit-exactly against the oracle on crafted, mutated and generated frames across
 parse modes, frame alignments and LDS window sizes. This is the pre-GPU gate;
 tests/test_gpu_parity.py repeats the comparison on the device."""
+import os
+
 import numpy as np
 import pytest
 
@@ -140,3 +142,28 @@ def test_vlan_core_matches_oracle(oracle, corpus, flags, layout):
         got = harness.parse_packed(buf, offs, lens, flags=flags, use_fast=mode)
         helpers.records_equal(got, want, None, f"vlan flags={flags} mode={mode}")
     assert (want["flags"] & abi.L_VLAN).sum() >= len(helpers.vlan_frames()) - 3
+
+
+def test_parse_core_memory_safe_random_inputs(tmp_path, oracle):
+    """SURVEY.md §4 item 4 (the reference's panic_free_parsing.rs): random
+    0..2048-B inputs and mutated frames through the device parse core and the
+    oracle built with AddressSanitizer + UBSan (tests/native/parse_fuzz): each
+    frame alone in a heap block ending at its last 16-B load granule, three
+    alignments, six parse modes, four staging variants — no out-of-bounds
+    access, no UB, and every record / FrameSlice equal to the oracle's."""
+    import struct
+    import subprocess
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+    subprocess.check_call(["make", "-s", "-C", here, "parse_fuzz"])
+    rng = np.random.default_rng(2048)
+    frames = [bytes(rng.integers(0, 256, int(rng.integers(0, 2049)), dtype=np.uint8)) for _ in range(3000)]
+    base = ([bytes.fromhex(v["frame"]) for v in helpers.golden()["frames"]] + helpers.crafted_frames() +
+            [oracle.gen_frame(abi.WL_IMIX, i) for i in range(200)])
+    frames += base + helpers.mutate_frames(rng, base, 6000)
+    path = tmp_path / "frames.bin"
+    path.write_bytes(b"".join(struct.pack("<I", len(f)) + f for f in frames))
+    r = subprocess.run([os.path.join(here, "parse_fuzz"), str(path)], capture_output=True, text=True,
+                       timeout=600, env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+                                             UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1"))
+    assert r.returncode == 0, (r.stdout[-500:], r.stderr[-3000:])
+    assert "mismatches 0" in r.stdout
