@@ -356,3 +356,26 @@ def test_probe_stream(engine):
     o0 = engine.probe_stream(data, False)
     torch.cuda.synchronize()
     assert (o0.cpu().numpy().view("<u4")[:3] == np.bitwise_xor.reduce(lane_x, axis=1)).all()
+
+
+@pytest.mark.parametrize("workload", [abi.WL_UDP64, abi.WL_IMIX])
+def test_logical_shards_equal_whole(engine, workload):
+    """SURVEY.md §4 item 5 on one device: the batch regenerated as 8 index-range
+    shards (nex_amd.dist.shard, as each bench.py rank does) and parsed shard by
+    shard gives exactly the whole batch's records and frame bytes."""
+    import torch
+    from nex_amd import dist
+    total = (1 << 20) + 12345
+    whole = engine.gen_batch(workload, total)
+    want = engine.parse(whole, out_kind=abi.OUT_RECORD)
+    parts, frames = [], []
+    for r in range(8):
+        b, e = dist.shard(total, r, 8)
+        sb = engine.gen_batch(workload, e - b, first_index=b)
+        parts.append(engine.parse(sb, out_kind=abi.OUT_RECORD)[: (e - b) * 64])
+        frames.append(sb.data[: sb.total_bytes] if sb.offsets is None else
+                      sb.data[int(sb.offsets[0]): int(sb.offsets[e - b])])
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(parts), want[: total * 64])
+    wb = whole.data[: whole.total_bytes] if whole.offsets is None else whole.data[: int(whole.offsets[total])]
+    assert torch.equal(torch.cat(frames), wb)
