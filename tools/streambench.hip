@@ -75,6 +75,24 @@ __global__ __launch_bounds__(256) void k_wv(const uint8_t* data, uint64_t n16, u
     }
 }
 
+// 8 B per 64-B frame written as 16-B stores by half the lanes (through LDS)
+__global__ __launch_bounds__(256) void k_wv16(const uint8_t* data, uint64_t n16, uint8_t* out) {
+    __shared__ __attribute__((aligned(16))) uint2 s_d[256];
+    const uint64_t base = (uint64_t)blockIdx.x * 1024;
+    uint32_t x = 0;
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = load16<true>(data + 16 * (base + threadIdx.x + 256 * k));
+#pragma unroll
+    for (int k = 0; k < 4; k++) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    const uint64_t fr = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    s_d[threadIdx.x] = make_uint2(x, (uint32_t)fr);
+    __syncthreads();
+    if (threadIdx.x < 128)
+        reinterpret_cast<uint4*>(out)[(uint64_t)blockIdx.x * 128 + threadIdx.x] =
+            reinterpret_cast<const uint4*>(s_d)[threadIdx.x];
+}
+
 // T tiles per workgroup, the T descriptor blocks written together at the end
 template <int T>
 __global__ __launch_bounds__(256) void k_wbatch(const uint8_t* data, uint64_t n16, uint2* out) {
@@ -284,6 +302,7 @@ int main(int argc, char** argv) {
         uint8_t* o8 = reinterpret_cast<uint8_t*>(out);
         const dim3 g(n16 / 1024);
         vs.push_back({"w8_plain", [=]() { hipLaunchKernelGGL((k_wv<8, 0>), g, dim3(256), 0, 0, data, n16, o8); }});
+        vs.push_back({"w8_via16", [=]() { hipLaunchKernelGGL(k_wv16, g, dim3(256), 0, 0, data, n16, o8); }});
         vs.push_back({"w8_nt", [=]() { hipLaunchKernelGGL((k_wv<8, 1>), g, dim3(256), 0, 0, data, n16, o8); }});
         vs.push_back({"w8_sc01nt", [=]() { hipLaunchKernelGGL((k_wv<8, 2>), g, dim3(256), 0, 0, data, n16, o8); }});
         vs.push_back({"w4_plain", [=]() { hipLaunchKernelGGL((k_wv<4, 0>), g, dim3(256), 0, 0, data, n16, o8); }});
