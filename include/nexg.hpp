@@ -1,0 +1,451 @@
+/*
+ * nexg.hpp — C++17 host API above the C ABI (include/nexg.h), mirroring
+ * nex-packet's frame API for code that called the reference from a compiled
+ * language (the reference is Rust; cargo is absent here, so this is the host
+ * side a C++ caller links against, INTEGRATION.md gives the Rust binding).
+ *
+ * Names, field meanings and error behaviour follow the reference:
+ *   ParseMode / ParseOption / ParseError   parse.rs:34-97, frame.rs:47-50
+ *   Frame, DatalinkLayer, IpLayer, TransportLayer   frame.rs:21-60
+ *   EthernetHeader ethernet.rs:152-160, ArpHeader arp.rs:300-311,
+ *   Ipv4Header ipv4.rs:187-202 (+ Ipv4OptionPacket ipv4.rs:39-182),
+ *   Ipv6Header ipv6.rs:14-23, IcmpHeader icmp.rs:172-176,
+ *   Icmpv6Header icmpv6.rs:229-234, TcpHeader tcp.rs:482-494
+ *   (+ TcpOptionPacket tcp.rs:33-476), UdpHeader udp.rs:22-27
+ *   Engine::try_from_bufs   Frame::try_from_buf_with_mode (frame.rs:309) on a
+ *                           batch: one Result<Frame, ParseError> per frame
+ * The device does the parse and the checksums (nexg_parse_batch,
+ * NEXG_OUT_RECORD) and the option lists (nexg_decode_options); this header
+ * only reads header fields out of the frame bytes at the offsets the device
+ * reported. API misuse and HIP failures throw nexg::Error; per-frame parse
+ * failures are data (Result), as in the reference. Header-only; link
+ * libnexg.so and amdhip64.
+ */
+#ifndef NEXG_HPP
+#define NEXG_HPP
+
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <variant>
+#include <vector>
+
+#include "nexg.h"
+
+namespace nexg {
+
+/* ---- parse knobs and errors ------------------------------------------- */
+
+enum class ParseMode { Lenient, Strict };  // parse.rs:34-46
+
+struct ParseOption {  // frame.rs:47-50 (+ the NEXG_PARSE_VLAN extension, off by default)
+    bool from_ip_packet = false;
+    size_t offset = 0;
+    bool unwrap_vlan = false;
+    uint32_t flags(ParseMode mode) const {
+        return (from_ip_packet ? NEXG_PARSE_FROM_IP : 0u) | (unwrap_vlan ? NEXG_PARSE_VLAN : 0u) |
+               (mode == ParseMode::Strict ? NEXG_PARSE_STRICT : 0u);
+    }
+};
+
+enum class ParseErrorKind : uint8_t {  // parse.rs:51-97 (kinds; context strings are not carried)
+    BufferTooShort = NEXG_ERR_BUFFER_TOO_SHORT,
+    InvalidLength = NEXG_ERR_INVALID_LENGTH,
+    Malformed = NEXG_ERR_MALFORMED,
+    Truncated = NEXG_ERR_TRUNCATED,
+    BadExtent = NEXG_ERR_BAD_EXTENT,  // caller error: frame longer than 65535 bytes
+};
+
+struct ParseError {
+    ParseErrorKind kind;
+    const char* name() const {
+        switch (kind) {
+            case ParseErrorKind::BufferTooShort: return "BufferTooShort";
+            case ParseErrorKind::InvalidLength: return "InvalidLength";
+            case ParseErrorKind::Malformed: return "Malformed";
+            case ParseErrorKind::Truncated: return "Truncated";
+            default: return "BadExtent";
+        }
+    }
+};
+
+// Result<T, ParseError>, as the reference's parse functions return
+template <class T>
+class Result {
+   public:
+    Result(T v) : v_(std::move(v)) {}
+    Result(ParseError e) : v_(e) {}
+    bool is_ok() const { return v_.index() == 0; }
+    bool is_err() const { return v_.index() == 1; }
+    const T& value() const { return std::get<0>(v_); }
+    T& value() { return std::get<0>(v_); }
+    const ParseError& error() const { return std::get<1>(v_); }
+
+   private:
+    std::variant<T, ParseError> v_;
+};
+
+struct Error : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+/* ---- addresses and headers -------------------------------------------- */
+
+using MacAddr = std::array<uint8_t, 6>;
+
+struct Ipv4Addr {
+    std::array<uint8_t, 4> octets{};
+    std::string to_string() const {
+        char b[16];
+        snprintf(b, sizeof(b), "%u.%u.%u.%u", octets[0], octets[1], octets[2], octets[3]);
+        return b;
+    }
+    bool operator==(const Ipv4Addr& o) const { return octets == o.octets; }
+};
+
+struct Ipv6Addr {
+    std::array<uint8_t, 16> octets{};
+    bool operator==(const Ipv6Addr& o) const { return octets == o.octets; }
+};
+
+struct EthernetHeader {  // ethernet.rs:152-160
+    MacAddr destination{}, source{};
+    uint16_t ethertype = 0;  // EtherType::value()
+};
+
+struct ArpHeader {  // arp.rs:300-311
+    uint16_t hardware_type = 0, protocol_type = 0;
+    uint8_t hw_addr_len = 0, proto_addr_len = 0;
+    uint16_t operation = 0;
+    MacAddr sender_hw_addr{};
+    Ipv4Addr sender_proto_addr;
+    MacAddr target_hw_addr{};
+    Ipv4Addr target_proto_addr;
+};
+
+struct Ipv4OptionHeader {  // ipv4.rs:39-182
+    uint8_t copied = 0, class_ = 0, number = 0;  // number = Ipv4OptionType::value()
+    std::optional<uint8_t> length;
+};
+struct Ipv4OptionPacket {
+    Ipv4OptionHeader header;
+    std::vector<uint8_t> data;
+};
+
+struct Ipv4Header {  // ipv4.rs:187-202
+    uint8_t version = 4, header_length = 0, dscp = 0, ecn = 0;
+    uint16_t total_length = 0, identification = 0;
+    uint8_t flags = 0;
+    uint16_t fragment_offset = 0;
+    uint8_t ttl = 0;
+    uint8_t next_level_protocol = 0;  // IpNextProtocol::value() (143..=252 -> 255, Q8)
+    uint16_t checksum = 0;
+    Ipv4Addr source, destination;
+    std::vector<Ipv4OptionPacket> options;
+};
+
+struct Ipv6Header {  // ipv6.rs:14-23
+    uint8_t version = 6, traffic_class = 0;
+    uint32_t flow_label = 0;
+    uint16_t payload_length = 0;
+    uint8_t next_header = 0;  // raw byte 6 (Q10)
+    uint8_t hop_limit = 0;
+    Ipv6Addr source, destination;
+};
+
+struct IcmpHeader {  // icmp.rs:172-176
+    uint8_t icmp_type = 0, icmp_code = 0;
+    uint16_t checksum = 0;
+};
+struct Icmpv6Header {  // icmpv6.rs:229-234
+    uint8_t icmpv6_type = 0, icmpv6_code = 0;
+    uint16_t checksum = 0;
+};
+
+struct TcpOptionPacket {  // tcp.rs:33-476
+    uint8_t kind = 0;
+    std::optional<uint8_t> length;
+    std::vector<uint8_t> data;
+};
+
+struct TcpHeader {  // tcp.rs:482-494
+    uint16_t source = 0, destination = 0;
+    uint32_t sequence = 0, acknowledgement = 0;
+    uint8_t data_offset = 0, reserved = 0, flags = 0;
+    uint16_t window = 0, checksum = 0, urgent_ptr = 0;
+    std::vector<TcpOptionPacket> options;
+};
+
+struct UdpHeader {  // udp.rs:22-27
+    uint16_t source = 0, destination = 0, length = 0, checksum = 0;
+};
+
+struct DatalinkLayer {
+    std::optional<EthernetHeader> ethernet;
+    std::optional<ArpHeader> arp;
+};
+struct IpLayer {
+    std::optional<Ipv4Header> ipv4;
+    std::optional<Ipv6Header> ipv6;
+    std::optional<IcmpHeader> icmp;
+    std::optional<Icmpv6Header> icmpv6;
+};
+struct TransportLayer {
+    std::optional<TcpHeader> tcp;
+    std::optional<UdpHeader> udp;
+};
+
+// What the engine adds to the Frame path: the packet-API verification
+// checksums (DESIGN.md §1 "Verify semantics")
+struct Checksums {
+    bool ip_checked = false, ip_ok = false, ip_panic = false, l4_checked = false, l4_ok = false;
+    uint16_t ip_computed = 0, l4_computed = 0;
+};
+
+struct Frame {  // frame.rs:54-60
+    std::optional<DatalinkLayer> datalink;
+    std::optional<IpLayer> ip;
+    std::optional<TransportLayer> transport;
+    std::vector<uint8_t> payload;
+    size_t packet_len = 0;
+    Checksums checksums;
+};
+
+/* ---- materialisation from a device record ------------------------------ */
+
+namespace detail {
+inline uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
+inline Ipv4Addr v4(uint32_t be_value) {
+    return Ipv4Addr{{(uint8_t)(be_value >> 24), (uint8_t)(be_value >> 16), (uint8_t)(be_value >> 8),
+                     (uint8_t)be_value}};
+}
+inline MacAddr mac(const uint8_t* p) {
+    MacAddr m;
+    memcpy(m.data(), p, 6);
+    return m;
+}
+inline Ipv4OptionPacket ipv4_option_at(const uint8_t* p) {
+    Ipv4OptionPacket o;
+    o.header.copied = (p[0] >> 7) & 1;
+    o.header.class_ = (p[0] >> 5) & 3;
+    o.header.number = p[0] & 0x1F;
+    if (o.header.number > 1) {
+        o.header.length = p[1];
+        o.data.assign(p + 2, p + p[1]);
+    }
+    return o;
+}
+inline TcpOptionPacket tcp_option_at(const uint8_t* p) {
+    TcpOptionPacket o;
+    o.kind = p[0];
+    if (o.kind > 1) {
+        o.length = p[1];
+        o.data.assign(p + 2, p + p[1]);
+    }
+    return o;
+}
+}  // namespace detail
+
+// Frame from one NEXG_OUT_RECORD record, the frame bytes and (for the option
+// lists) the frame's nexg_options. Mirrors nex_amd/frame.py::frame_from_record.
+inline Result<Frame> frame_from_record(const nexg_record& r, const uint8_t* b, size_t len,
+                                       const nexg_options& opts) {
+    using namespace detail;
+    const uint32_t f = r.flags;
+    if (NEXG_STATUS(f)) return ParseError{(ParseErrorKind)NEXG_STATUS(f)};
+    (void)len;
+    Frame fr;
+    const uint32_t l3 = r.l3_off;
+    if (f & NEXG_L_ETHERNET) {
+        DatalinkLayer dl;
+        EthernetHeader eth;
+        eth.ethertype = r.ethertype;
+        // a real Ethernet header unless from_ip_packet fabricated one (frame.rs:396-400)
+        if ((f & NEXG_L_VLAN) || (l3 == 14 && be16(b + 12) == r.ethertype)) {
+            eth.destination = mac(b);
+            eth.source = mac(b + 6);
+        }
+        dl.ethernet = eth;
+        if (f & NEXG_L_ARP) {
+            ArpHeader a;
+            const uint8_t* p = b + l3;
+            a.hardware_type = be16(p);
+            a.protocol_type = be16(p + 2);
+            a.hw_addr_len = p[4];
+            a.proto_addr_len = p[5];
+            a.operation = be16(p + 6);
+            a.sender_hw_addr = mac(p + 8);
+            memcpy(a.sender_proto_addr.octets.data(), p + 14, 4);
+            a.target_hw_addr = mac(p + 18);
+            memcpy(a.target_proto_addr.octets.data(), p + 24, 4);
+            dl.arp = a;
+        }
+        fr.datalink = dl;
+    }
+    if (f & NEXG_L_IP) {
+        IpLayer ip;
+        if (f & NEXG_L_IPV4) {
+            Ipv4Header h;
+            h.header_length = r.ip_ver_ihl & 15;
+            h.dscp = r.ip_tos >> 2;
+            h.ecn = r.ip_tos & 3;
+            h.total_length = r.ip_length;
+            h.identification = (uint16_t)(r.ip_word >> 16);
+            h.flags = (r.ip_word >> 13) & 7;
+            h.fragment_offset = r.ip_word & 0x1FFF;
+            h.ttl = r.ip_ttl;
+            h.next_level_protocol = r.ip_proto;
+            h.checksum = r.ip_csum;
+            h.source = v4(r.ip_src);
+            h.destination = v4(r.ip_dst);
+            for (int k = 0; k < opts.n_ip; k++) h.options.push_back(ipv4_option_at(b + opts.ip_opt_off + opts.ip_pos[k]));
+            ip.ipv4 = std::move(h);
+        }
+        if (f & NEXG_L_IPV6) {
+            Ipv6Header h;
+            h.traffic_class = r.ip_tos;
+            h.flow_label = r.ip_word;
+            h.payload_length = r.ip_length;
+            h.next_header = r.ip_proto;
+            h.hop_limit = r.ip_ttl;
+            memcpy(h.source.octets.data(), b + l3 + 8, 16);
+            memcpy(h.destination.octets.data(), b + l3 + 24, 16);
+            ip.ipv6 = h;
+        }
+        if (f & NEXG_L_ICMP) ip.icmp = IcmpHeader{r.l4_type, r.l4_code, r.l4_csum};
+        if (f & NEXG_L_ICMPV6) ip.icmpv6 = Icmpv6Header{r.l4_type, r.l4_code, r.l4_csum};
+        fr.ip = std::move(ip);
+    }
+    if (f & NEXG_L_TRANSPORT) {
+        TransportLayer tp;
+        if (f & NEXG_L_TCP) {
+            TcpHeader h;
+            h.source = r.src_port;
+            h.destination = r.dst_port;
+            h.sequence = r.tcp_seq;
+            h.acknowledgement = r.tcp_ack;
+            h.data_offset = r.l4_code >> 4;
+            h.reserved = r.l4_code & 15;
+            h.flags = r.l4_type;
+            h.window = r.tcp_window;
+            h.checksum = r.l4_csum;
+            h.urgent_ptr = r.tcp_urg;
+            for (int k = 0; k < opts.n_tcp; k++) h.options.push_back(tcp_option_at(b + opts.tcp_opt_off + opts.tcp_pos[k]));
+            tp.tcp = std::move(h);
+        }
+        if (f & NEXG_L_UDP) tp.udp = UdpHeader{r.src_port, r.dst_port, r.l4_length, r.l4_csum};
+        fr.transport = std::move(tp);
+    }
+    fr.payload.assign(b + r.payload_off, b + r.payload_off + r.payload_len);
+    fr.packet_len = r.packet_len;
+    fr.checksums = Checksums{(f & NEXG_C_IP_CHECKED) != 0, (f & NEXG_C_IP_OK) != 0, (f & NEXG_C_IP_PANIC) != 0,
+                             (f & NEXG_C_L4_CHECKED) != 0, (f & NEXG_C_L4_OK) != 0, r.ip_csum_calc,
+                             r.l4_csum_calc};
+    return fr;
+}
+
+/* ---- the engine --------------------------------------------------------- */
+
+class Engine {  // one nexg context on one gfx950 device, one stream
+   public:
+    explicit Engine(int device = 0) {
+        check_hip(hipSetDevice(device), "hipSetDevice");
+        check(nexg_ctx_create(device, &ctx_), "nexg_ctx_create");
+        check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+    }
+    ~Engine() {
+        if (stream_) (void)hipStreamDestroy(stream_);
+        if (ctx_) nexg_ctx_destroy(ctx_);
+    }
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+
+    nexg_ctx* ctx() const { return ctx_; }
+    hipStream_t stream() const { return stream_; }
+
+    // Device-resident batch (frames / out are device pointers), stream-ordered
+    void parse(const nexg_frames& frames, ParseOption option, ParseMode mode, int out_kind, void* out) {
+        const nexg_parse_option o{option.flags(mode), (uint32_t)option.offset};
+        check(nexg_parse_batch(ctx_, &frames, &o, out_kind, out, stream_), "nexg_parse_batch");
+    }
+
+    // Frame::try_from_buf_with_mode (frame.rs:309) on every host frame: the
+    // batch is packed, copied to the device, parsed (NEXG_OUT_RECORD), its
+    // option lists decoded, and each Frame materialised from its record.
+    std::vector<Result<Frame>> try_from_bufs(const std::vector<std::vector<uint8_t>>& frames,
+                                             ParseOption option = {}, ParseMode mode = ParseMode::Lenient) {
+        const uint64_t n = frames.size();
+        std::vector<Result<Frame>> out;
+        if (n == 0) return out;
+        std::vector<uint64_t> offs(n);
+        std::vector<uint32_t> lens(n);
+        uint64_t pos = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            offs[i] = pos;
+            lens[i] = (uint32_t)frames[i].size();
+            pos += (frames[i].size() + 3) & ~(uint64_t)3;
+        }
+        std::vector<uint8_t> data(pos ? pos : 16, 0);
+        for (uint64_t i = 0; i < n; i++)
+            if (!frames[i].empty()) memcpy(data.data() + offs[i], frames[i].data(), frames[i].size());
+        DeviceBuf d_data(data.size()), d_offs(n * 8), d_lens(n * 4), d_recs(n * 64), d_opts(n * 96);
+        check_hip(hipMemcpyAsync(d_data.p, data.data(), data.size(), hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_offs.p, offs.data(), n * 8, hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_lens.p, lens.data(), n * 4, hipMemcpyHostToDevice, stream_), "H2D");
+        nexg_frames fb{};
+        fb.data = static_cast<const uint8_t*>(d_data.p);
+        fb.data_bytes = data.size();
+        fb.offsets = static_cast<const uint64_t*>(d_offs.p);
+        fb.lengths = static_cast<const uint32_t*>(d_lens.p);
+        fb.count = n;
+        parse(fb, option, mode, NEXG_OUT_RECORD, d_recs.p);
+        check(nexg_decode_options(ctx_, &fb, static_cast<const nexg_record*>(d_recs.p),
+                                  static_cast<nexg_options*>(d_opts.p), stream_),
+              "nexg_decode_options");
+        std::vector<nexg_record> recs(n);
+        std::vector<nexg_options> opts(n);
+        check_hip(hipMemcpyAsync(recs.data(), d_recs.p, n * 64, hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipMemcpyAsync(opts.data(), d_opts.p, n * 96, hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+        out.reserve(n);
+        for (uint64_t i = 0; i < n; i++)
+            out.push_back(frame_from_record(recs[i], frames[i].data(), frames[i].size(), opts[i]));
+        return out;
+    }
+
+    Result<Frame> try_from_buf(const std::vector<uint8_t>& frame, ParseOption option = {},
+                               ParseMode mode = ParseMode::Lenient) {
+        return std::move(try_from_bufs({frame}, option, mode)[0]);
+    }
+
+   private:
+    struct DeviceBuf {
+        void* p = nullptr;
+        explicit DeviceBuf(size_t n) {
+            if (hipMalloc(&p, n ? n : 16) != hipSuccess) throw Error("hipMalloc failed");
+        }
+        ~DeviceBuf() { (void)hipFree(p); }
+        DeviceBuf(const DeviceBuf&) = delete;
+        DeviceBuf& operator=(const DeviceBuf&) = delete;
+    };
+    void check(int rc, const char* what) {
+        if (rc != NEXG_OK)
+            throw Error(std::string(what) + " failed: " + (ctx_ ? nexg_ctx_last_error(ctx_) : "no context"));
+    }
+    static void check_hip(hipError_t e, const char* what) {
+        if (e != hipSuccess) throw Error(std::string(what) + ": " + hipGetErrorString(e));
+    }
+    nexg_ctx* ctx_ = nullptr;
+    hipStream_t stream_ = nullptr;
+};
+
+}  // namespace nexg
+
+#endif  // NEXG_HPP

@@ -1,0 +1,187 @@
+// TEST INFRASTRUCTURE: the C++ host API (include/nexg.hpp) checked with the
+// reference's own unit-test assertions, written as the reference writes them
+// (frame.rs:665-784, ipv4.rs:944-1204, ipv6.rs:706-741, tcp.rs:1276-1314,
+// udp.rs:511-527, icmp.rs:708-725, icmpv6.rs:606-631). Frames come from
+// tests/golden/reference_vectors.json via a text fixture (name flags
+// ip_offset hex per line) the pytest writes.
+//   --gpu <fixture>: Frames from nexg::Engine::try_from_bufs (the device path)
+//   --cpu <fixture>: Frames materialised by nexg::frame_from_record from the
+//                    oracle's records (checks the C++ materialisation without
+//                    a GPU; the oracle is test infrastructure)
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <fstream>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/nexg.hpp"
+#include "../../oracle/nex_oracle.h"
+
+using namespace nexg;
+
+static int failures = 0, checks = 0;
+#define CHECK(c)                                                                  \
+    do {                                                                          \
+        checks++;                                                                 \
+        if (!(c)) { failures++; fprintf(stderr, "%s:%d: CHECK(%s) failed\n", __FILE__, __LINE__, #c); } \
+    } while (0)
+
+struct Fixture {
+    uint32_t flags = 0, ip_offset = 0;
+    std::vector<uint8_t> bytes;
+};
+
+static std::vector<uint8_t> hex(const std::string& s) {
+    std::vector<uint8_t> b;
+    for (size_t i = 0; i + 1 < s.size(); i += 2) b.push_back((uint8_t)strtoul(s.substr(i, 2).c_str(), nullptr, 16));
+    return b;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) return 2;
+    const bool gpu = std::string(argv[1]) == "--gpu";
+    std::map<std::string, Fixture> fx;
+    std::ifstream in(argv[2]);
+    std::string line;
+    while (std::getline(in, line)) {
+        std::istringstream ss(line);
+        std::string name, h;
+        Fixture f;
+        ss >> name >> f.flags >> f.ip_offset >> h;
+        f.bytes = hex(h);
+        fx[name] = f;
+    }
+    std::vector<std::string> names;
+    std::vector<std::vector<uint8_t>> frames;
+    for (auto& kv : fx) {
+        names.push_back(kv.first);
+        frames.push_back(kv.second.bytes);
+    }
+    // Frame::try_from_buf_with_mode per fixture, in its own ParseOption/ParseMode
+    std::map<std::string, Result<Frame>> got;
+    std::unique_ptr<Engine> eng;
+    if (gpu) eng.reset(new Engine(0));
+    for (size_t i = 0; i < names.size(); i++) {
+        const Fixture& f = fx[names[i]];
+        ParseOption opt;
+        opt.from_ip_packet = (f.flags & NEXG_PARSE_FROM_IP) != 0;
+        opt.offset = f.ip_offset;
+        const ParseMode mode = (f.flags & NEXG_PARSE_STRICT) ? ParseMode::Strict : ParseMode::Lenient;
+        if (gpu) {
+            got.emplace(names[i], eng->try_from_buf(f.bytes, opt, mode));
+        } else {
+            nexg_record r;
+            nexg_options o;
+            nexo_parse_frame(f.bytes.data(), f.bytes.size(), f.flags, f.ip_offset, &r);
+            nexo_decode_options(f.bytes.data(), f.bytes.size(), f.flags, f.ip_offset, &o);
+            got.emplace(names[i], frame_from_record(r, f.bytes.data(), f.bytes.size(), o));
+        }
+    }
+    auto frame = [&](const char* n) -> const Frame& {
+        const auto& r = got.at(n);
+        if (r.is_err()) { fprintf(stderr, "%s: unexpected %s\n", n, r.error().name()); exit(1); }
+        return r.value();
+    };
+    auto bytes = [](const char* s) { return std::vector<uint8_t>(s, s + strlen(s)); };
+
+    {  // frame.rs:665-680 unknown EtherType keeps the payload
+        const Frame& f = frame("unknown_ethertype_keeps_payload");
+        CHECK(f.datalink && f.datalink->ethernet && f.datalink->ethernet->ethertype == 0x88b5);
+        CHECK(!f.ip && !f.transport);
+        CHECK(f.payload == (std::vector<uint8_t>{0xde, 0xad, 0xbe, 0xef}));
+    }
+    {  // frame.rs:681-712 IPv4/UDP frame
+        const Frame& f = frame("ipv4_udp_frame");
+        CHECK(f.ip && f.ip->ipv4 && f.ip->ipv4->version == 4);
+        CHECK(f.transport && f.transport->udp && f.transport->udp->destination == 53);
+        CHECK(f.payload == (std::vector<uint8_t>{1, 2, 3, 4}));
+    }
+    {  // frame.rs:713-734 from_ip_packet: dummy Ethernet header
+        const Frame& f = frame("dummy_ethernet_ipv4");
+        CHECK(f.datalink && f.datalink->ethernet && f.datalink->ethernet->ethertype == 0x0800);
+        CHECK(f.datalink->ethernet->source == (MacAddr{}) && f.datalink->ethernet->destination == (MacAddr{}));
+    }
+    {  // ipv4.rs:944-1020 options: NOP, RecordRoute(len 4, data 12 34), EOL
+        const Frame& f = frame("ipv4_with_options");
+        const auto& h = *f.ip->ipv4;
+        CHECK(h.header_length == 7 && h.total_length == 32);
+        CHECK(h.options.size() == 3);
+        CHECK(h.options[0].header.number == 1 && !h.options[0].header.length);
+        CHECK(h.options[1].header.number == 7 && h.options[1].header.length == 4);
+        CHECK(h.options[1].data == (std::vector<uint8_t>{0x12, 0x34}));
+        CHECK(h.options[2].header.number == 0);
+        CHECK(f.payload == (std::vector<uint8_t>{0xde, 0xad, 0xbe, 0xef}));
+    }
+    {  // ipv4.rs:944-970 round trip fields
+        const Frame& f = frame("ipv4_round_trip");
+        const auto& h = *f.ip->ipv4;
+        CHECK(h.source.to_string() == "192.168.0.1" && h.destination.to_string() == "192.168.0.199");
+        CHECK(h.checksum == 0xb1e6 && h.total_length == 28);
+        CHECK(f.checksums.ip_checked && !f.checksums.ip_ok);  // the fixture's field does not verify
+    }
+    {  // ipv4.rs:1176-1204 strict truncation is an error, lenient is not; zero total length
+        const auto& s = got.at("ipv4_strict_truncation");
+        CHECK(s.is_err() && s.error().kind == ParseErrorKind::Truncated);
+        CHECK(frame("ipv4_lenient_truncation").ip->ipv4->total_length == 24);
+        const Frame& z = frame("ipv4_zero_total_length");
+        CHECK(z.ip->ipv4->total_length == 24);
+        CHECK(z.payload == (std::vector<uint8_t>{0xde, 0xad, 0xbe, 0xef}));
+    }
+    {  // ipv6.rs:706-741 traffic class, flow label, payload
+        const Frame& f = frame("ipv6_from_bytes");
+        CHECK(f.ip->ipv6 && f.ip->ipv6->traffic_class == 0x0A && f.ip->ipv6->flow_label == 0x12345);
+        CHECK(f.payload == bytes("Hello!!\n"));
+    }
+    {  // tcp.rs:1276-1314 options NOP, NOP, Timestamp; header 32; payload "test"
+        const Frame& f = frame("tcp_basic_parse");
+        const auto& t = *f.transport->tcp;
+        CHECK(t.source == 49511 && t.destination == 9000);
+        CHECK(t.sequence == 2419577528u && t.acknowledgement == 2487988854u);
+        CHECK(t.data_offset == 8 && t.window == 4015 && t.checksum == 0xc031);
+        CHECK(t.options.size() == 3 && t.options[0].kind == 1 && t.options[1].kind == 1);
+        CHECK(t.options[2].kind == 8 && t.options[2].length == 10);
+        CHECK(t.options[2].data == (std::vector<uint8_t>{0x2c, 0x57, 0xcd, 0xa5, 0x02, 0xa0, 0x41, 0x92}));
+        CHECK(f.payload == bytes("test"));
+    }
+    {  // udp.rs:511-527
+        const Frame& f = frame("udp_basic_parse");
+        const auto& u = *f.transport->udp;
+        CHECK(u.source == 0x1234 && u.destination == 0xabcd && u.length == 12 && u.checksum == 0x55aa);
+        CHECK(f.payload == bytes("data"));
+    }
+    {  // icmp.rs:708-725 echo request, id 1234, seq 42
+        const Frame& f = frame("icmp_echo_request");
+        CHECK(f.ip->icmp && f.ip->icmp->icmp_type == 8 && f.ip->icmp->checksum == 0x3abc);
+        CHECK(!f.transport);
+        CHECK(f.payload.size() >= 4 && f.payload[0] == 0x04 && f.payload[1] == 0xd2 && f.payload[3] == 42);
+    }
+    {  // icmpv6.rs:606-631 checksum KAT
+        const Frame& f = frame("icmpv6_echo_request_lo");
+        CHECK(f.ip->icmpv6 && f.ip->icmpv6->icmpv6_type == 128);
+        CHECK(f.checksums.l4_checked && f.checksums.l4_computed == 0x1d2e);
+    }
+    {  // frame.rs:760-784 IPv6 + hop-by-hop: Frame dispatches on the raw next header (Q10)
+        const Frame& f = frame("frame_slice_ipv6_hbh_udp");
+        CHECK(f.ip->ipv6 && f.ip->ipv6->next_header == 0 && !f.transport);
+        CHECK(f.payload == (std::vector<uint8_t>{0x04, 0xd2, 0x00, 0x35, 0x00, 0x0b, 0x00, 0x00, 'd', 'n', 's'}));
+    }
+    // every fixture: Frame fields == the record the oracle writes (device == oracle in --gpu)
+    for (const auto& n : names) {
+        const Fixture& fxt = fx[n];
+        nexg_record r;
+        nexo_parse_frame(fxt.bytes.data(), fxt.bytes.size(), fxt.flags, fxt.ip_offset, &r);
+        const auto& g = got.at(n);
+        CHECK(g.is_err() == (NEXG_STATUS(r.flags) != 0));
+        if (g.is_ok()) {
+            CHECK(g.value().packet_len == r.packet_len);
+            CHECK(g.value().payload.size() == r.payload_len);
+            CHECK(g.value().checksums.l4_computed == r.l4_csum_calc && g.value().checksums.ip_computed == r.ip_csum_calc);
+        }
+    }
+    printf("%s: %d checks, %d failures, %zu fixtures\n", gpu ? "gpu" : "cpu", checks, failures, names.size());
+    return failures ? 1 : 0;
+}
