@@ -280,7 +280,7 @@ def frame_from_record(rec, frame: bytes, options=None) -> Frame:
     l3 = int(rec["l3_off"])
     eth = None
     if flags & abi.L_ETHERNET:
-        if l3 == 14 and int(rec["ethertype"]) == _be16(b, 12):
+        if (flags & abi.L_VLAN) or (l3 == 14 and int(rec["ethertype"]) == _be16(b, 12)):
             eth = EthernetHeader(bytes(b[0:6]), bytes(b[6:12]), int(rec["ethertype"]))
         else:  # from_ip_packet: dummy Ethernet (frame.rs:396-400)
             eth = EthernetHeader(b"\0" * 6, b"\0" * 6, int(rec["ethertype"]))

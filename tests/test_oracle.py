@@ -442,6 +442,10 @@ def test_vlan_extension_oracle(oracle):
             if n == "packet_len":
                 w = len(f)
             assert int(got[n]) == w, (n, f.hex())
+        if not abi.status_of(int(got["flags"])):  # the Ethernet MACs stay the frame's own
+            from nex_amd.frame import frame_from_record
+            eth = frame_from_record(got, f).datalink.ethernet
+            assert eth.destination == f[0:6] and eth.source == f[6:12] and eth.ethertype == et
     # untagged frames are unchanged by the flag
     for f in helpers.crafted_frames():
         if len(f) >= 14 and f[12:14] in (b"\x81\x00", b"\x88\xa8", b"\x91\x00"):
