@@ -14,6 +14,10 @@
  *   (+ TcpOptionPacket tcp.rs:33-476), UdpHeader udp.rs:22-27
  *   Engine::try_from_bufs   Frame::try_from_buf_with_mode (frame.rs:309) on a
  *                           batch: one Result<Frame, ParseError> per frame
+ *   Engine::frame_slices    FrameSlice::try_from_buf (frame.rs:86) on a batch
+ *   Engine::build_udp_ping  UdpPacketBuilder -> Ipv4PacketBuilder ->
+ *                           EthernetPacketBuilder (udp_ping.rs:68-109) per
+ *                           tuple, Result<frames, BuildError>
  * The device does the parse and the checksums (nexg_parse_batch,
  * NEXG_OUT_RECORD) and the option lists (nexg_decode_options); this header
  * only reads header fields out of the frame bytes at the offsets the device
@@ -76,20 +80,23 @@ struct ParseError {
     }
 };
 
-// Result<T, ParseError>, as the reference's parse functions return
-template <class T>
+enum class BuildError { LengthOverflow, AddressFamilyMismatch };  // builder/error.rs:6-53
+
+// Result<T, E>, as the reference's parse (ParseError) and build (BuildError)
+// functions return
+template <class T, class E = ParseError>
 class Result {
    public:
     Result(T v) : v_(std::move(v)) {}
-    Result(ParseError e) : v_(e) {}
+    Result(E e) : v_(e) {}
     bool is_ok() const { return v_.index() == 0; }
     bool is_err() const { return v_.index() == 1; }
     const T& value() const { return std::get<0>(v_); }
     T& value() { return std::get<0>(v_); }
-    const ParseError& error() const { return std::get<1>(v_); }
+    const E& error() const { return std::get<1>(v_); }
 
    private:
-    std::variant<T, ParseError> v_;
+    std::variant<T, E> v_;
 };
 
 struct Error : std::runtime_error {
@@ -216,6 +223,46 @@ struct Frame {  // frame.rs:54-60
     std::vector<uint8_t> payload;
     size_t packet_len = 0;
     Checksums checksums;
+};
+
+// FrameSlice (frame.rs:62-83): layer boundaries borrowed from the input frame
+struct Bytes {
+    const uint8_t* data = nullptr;
+    size_t len = 0;
+    std::vector<uint8_t> to_vec() const { return std::vector<uint8_t>(data, data + len); }
+};
+struct FrameSlice {
+    Bytes packet;
+    std::optional<Bytes> datalink, network, transport;
+    Bytes payload;
+    std::optional<uint16_t> ethertype;
+    std::optional<uint8_t> ip_protocol;
+};
+
+inline Result<FrameSlice> frame_slice_from(const nexg_slice& s, const uint8_t* b, size_t len) {
+    if (NEXG_STATUS(s.flags)) return ParseError{(ParseErrorKind)NEXG_STATUS(s.flags)};
+    FrameSlice fs;
+    fs.packet = Bytes{b, len};
+    if (s.flags & NEXG_S_DATALINK) fs.datalink = Bytes{b, 14};
+    if (s.flags & NEXG_S_NETWORK) fs.network = Bytes{b + s.l3_off, s.l3_len};
+    if (s.flags & NEXG_S_TRANSPORT) fs.transport = Bytes{b + s.l3_off + s.l3_len, s.l4_len};
+    fs.payload = Bytes{b + s.payload_off, s.payload_len};
+    if (s.flags & NEXG_S_ETHERTYPE) fs.ethertype = s.ethertype;
+    if (s.flags & NEXG_S_IP_PROTOCOL) fs.ip_protocol = (uint8_t)(s.flags >> NEXG_S_PROTO_SHIFT);
+    return fs;
+}
+
+// The udp_ping frame shape (examples/udp_ping.rs:68-109): UdpPacketBuilder ->
+// Ipv4PacketBuilder -> EthernetPacketBuilder, one frame per tuple
+struct UdpPingTuple {
+    Ipv4Addr source, destination;
+    uint16_t src_port = 0, dst_port = 0, ip_id = 0;
+};
+struct UdpPingShape {
+    MacAddr src_mac{}, dst_mac{};
+    uint8_t ttl = 64;       // Ipv4PacketBuilder default (builder/ipv4.rs:37)
+    uint8_t ip_flags = 2;   // udp_ping sets DontFragment
+    std::vector<uint8_t> payload;
 };
 
 /* ---- materialisation from a device record ------------------------------ */
@@ -384,29 +431,10 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         const uint64_t n = frames.size();
         std::vector<Result<Frame>> out;
         if (n == 0) return out;
-        std::vector<uint64_t> offs(n);
-        std::vector<uint32_t> lens(n);
-        uint64_t pos = 0;
-        for (uint64_t i = 0; i < n; i++) {
-            offs[i] = pos;
-            lens[i] = (uint32_t)frames[i].size();
-            pos += (frames[i].size() + 3) & ~(uint64_t)3;
-        }
-        std::vector<uint8_t> data(pos ? pos : 16, 0);
-        for (uint64_t i = 0; i < n; i++)
-            if (!frames[i].empty()) memcpy(data.data() + offs[i], frames[i].data(), frames[i].size());
-        DeviceBuf d_data(data.size()), d_offs(n * 8), d_lens(n * 4), d_recs(n * 64), d_opts(n * 96);
-        check_hip(hipMemcpyAsync(d_data.p, data.data(), data.size(), hipMemcpyHostToDevice, stream_), "H2D");
-        check_hip(hipMemcpyAsync(d_offs.p, offs.data(), n * 8, hipMemcpyHostToDevice, stream_), "H2D");
-        check_hip(hipMemcpyAsync(d_lens.p, lens.data(), n * 4, hipMemcpyHostToDevice, stream_), "H2D");
-        nexg_frames fb{};
-        fb.data = static_cast<const uint8_t*>(d_data.p);
-        fb.data_bytes = data.size();
-        fb.offsets = static_cast<const uint64_t*>(d_offs.p);
-        fb.lengths = static_cast<const uint32_t*>(d_lens.p);
-        fb.count = n;
-        parse(fb, option, mode, NEXG_OUT_RECORD, d_recs.p);
-        check(nexg_decode_options(ctx_, &fb, static_cast<const nexg_record*>(d_recs.p),
+        HostBatch hb(frames, stream_);
+        DeviceBuf d_recs(n * 64), d_opts(n * 96);
+        parse(hb.fb, option, mode, NEXG_OUT_RECORD, d_recs.p);
+        check(nexg_decode_options(ctx_, &hb.fb, static_cast<const nexg_record*>(d_recs.p),
                                   static_cast<nexg_options*>(d_opts.p), stream_),
               "nexg_decode_options");
         std::vector<nexg_record> recs(n);
@@ -420,9 +448,75 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         return out;
     }
 
-    Result<Frame> try_from_buf(const std::vector<uint8_t>& frame, ParseOption option = {},
-                               ParseMode mode = ParseMode::Lenient) {
-        return std::move(try_from_bufs({frame}, option, mode)[0]);
+    // FrameSlice::try_from_buf (frame.rs:86) on every host frame; the slices
+    // borrow `frames`, which must outlive them
+    std::vector<Result<FrameSlice>> frame_slices(const std::vector<std::vector<uint8_t>>& frames,
+                                                 ParseOption option = {}) {
+        const uint64_t n = frames.size();
+        std::vector<Result<FrameSlice>> out;
+        if (n == 0) return out;
+        HostBatch hb(frames, stream_);
+        DeviceBuf d_sl(n * 16);
+        parse(hb.fb, option, ParseMode::Lenient, NEXG_OUT_SLICE, d_sl.p);
+        std::vector<nexg_slice> sl(n);
+        check_hip(hipMemcpyAsync(sl.data(), d_sl.p, n * 16, hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+        out.reserve(n);
+        for (uint64_t i = 0; i < n; i++) out.push_back(frame_slice_from(sl[i], frames[i].data(), frames[i].size()));
+        return out;
+    }
+
+    // udp_ping's build (udp_ping.rs:68-109) for every tuple: 42 + payload bytes
+    // each; BuildError::LengthOverflow when the UDP / IPv4 length would pass
+    // 65535 (builder/udp.rs:83, builder/ipv4.rs:153)
+    Result<std::vector<std::vector<uint8_t>>, BuildError> build_udp_ping(const std::vector<UdpPingTuple>& t,
+                                                                         const UdpPingShape& shape) {
+        if (28ull + shape.payload.size() > 65535ull) return BuildError::LengthOverflow;
+        const uint64_t n = t.size();
+        const uint32_t L = 42u + (uint32_t)shape.payload.size();
+        std::vector<std::vector<uint8_t>> frames;
+        if (n == 0) return frames;
+        std::vector<uint32_t> src(n), dst(n);
+        std::vector<uint16_t> sp(n), dp(n), id(n);
+        for (uint64_t i = 0; i < n; i++) {
+            const auto& a = t[i].source.octets;
+            const auto& b = t[i].destination.octets;
+            src[i] = (uint32_t)a[0] << 24 | (uint32_t)a[1] << 16 | (uint32_t)a[2] << 8 | a[3];
+            dst[i] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+            sp[i] = t[i].src_port;
+            dp[i] = t[i].dst_port;
+            id[i] = t[i].ip_id;
+        }
+        DeviceBuf d_src(n * 4), d_dst(n * 4), d_sp(n * 2), d_dp(n * 2), d_id(n * 2), d_pl(shape.payload.size()),
+            d_out((uint64_t)n * L);
+        check_hip(hipMemcpyAsync(d_src.p, src.data(), n * 4, hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_dst.p, dst.data(), n * 4, hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_sp.p, sp.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_dp.p, dp.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_id.p, id.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
+        if (!shape.payload.empty())
+            check_hip(hipMemcpyAsync(d_pl.p, shape.payload.data(), shape.payload.size(), hipMemcpyHostToDevice,
+                                     stream_), "H2D");
+        nexg_udp4_build p{};
+        p.src_ip = static_cast<const uint32_t*>(d_src.p);
+        p.dst_ip = static_cast<const uint32_t*>(d_dst.p);
+        p.src_port = static_cast<const uint16_t*>(d_sp.p);
+        p.dst_port = static_cast<const uint16_t*>(d_dp.p);
+        p.ip_id = static_cast<const uint16_t*>(d_id.p);
+        p.payload = shape.payload.empty() ? nullptr : static_cast<const uint8_t*>(d_pl.p);
+        p.payload_len = (uint32_t)shape.payload.size();
+        memcpy(p.def_src_mac, shape.src_mac.data(), 6);
+        memcpy(p.def_dst_mac, shape.dst_mac.data(), 6);
+        p.ttl = shape.ttl;
+        p.ip_flags = shape.ip_flags;
+        p.count = n;
+        check(nexg_build_udp4_batch(ctx_, &p, static_cast<uint8_t*>(d_out.p), L, stream_), "nexg_build_udp4_batch");
+        std::vector<uint8_t> host((uint64_t)n * L);
+        check_hip(hipMemcpyAsync(host.data(), d_out.p, host.size(), hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+        frames.reserve(n);
+        for (uint64_t i = 0; i < n; i++) frames.emplace_back(host.begin() + i * L, host.begin() + (i + 1) * L);
+        return frames;
     }
 
    private:
@@ -435,6 +529,46 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         DeviceBuf(const DeviceBuf&) = delete;
         DeviceBuf& operator=(const DeviceBuf&) = delete;
     };
+    // host frames packed (4-B aligned starts) with offsets + lengths, on the device
+    struct HostBatch {
+        std::vector<uint8_t> data;
+        std::vector<uint64_t> offs;
+        std::vector<uint32_t> lens;
+        DeviceBuf d_data, d_offs, d_lens;
+        nexg_frames fb{};
+        static size_t packed_size(const std::vector<std::vector<uint8_t>>& frames) {
+            size_t pos = 0;
+            for (const auto& f : frames) pos += (f.size() + 3) & ~(size_t)3;
+            return pos ? pos : 16;
+        }
+        HostBatch(const std::vector<std::vector<uint8_t>>& frames, hipStream_t s)
+            : data(packed_size(frames), 0), offs(frames.size()), lens(frames.size()),
+              d_data(data.size()), d_offs(frames.size() * 8), d_lens(frames.size() * 4) {
+            uint64_t pos = 0;
+            for (size_t i = 0; i < frames.size(); i++) {
+                offs[i] = pos;
+                lens[i] = (uint32_t)frames[i].size();
+                if (!frames[i].empty()) memcpy(data.data() + pos, frames[i].data(), frames[i].size());
+                pos += (frames[i].size() + 3) & ~(uint64_t)3;
+            }
+            check_hip(hipMemcpyAsync(d_data.p, data.data(), data.size(), hipMemcpyHostToDevice, s), "H2D");
+            check_hip(hipMemcpyAsync(d_offs.p, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, s), "H2D");
+            check_hip(hipMemcpyAsync(d_lens.p, lens.data(), lens.size() * 4, hipMemcpyHostToDevice, s), "H2D");
+            fb.data = static_cast<const uint8_t*>(d_data.p);
+            fb.data_bytes = data.size();
+            fb.offsets = static_cast<const uint64_t*>(d_offs.p);
+            fb.lengths = static_cast<const uint32_t*>(d_lens.p);
+            fb.count = frames.size();
+        }
+    };
+
+   public:
+    Result<Frame> try_from_buf(const std::vector<uint8_t>& frame, ParseOption option = {},
+                               ParseMode mode = ParseMode::Lenient) {
+        return std::move(try_from_bufs({frame}, option, mode)[0]);
+    }
+
+   private:
     void check(int rc, const char* what) {
         if (rc != NEXG_OK)
             throw Error(std::string(what) + " failed: " + (ctx_ ? nexg_ctx_last_error(ctx_) : "no context"));

@@ -169,6 +169,52 @@ int main(int argc, char** argv) {
         CHECK(f.ip->ipv6 && f.ip->ipv6->next_header == 0 && !f.transport);
         CHECK(f.payload == (std::vector<uint8_t>{0x04, 0xd2, 0x00, 0x35, 0x00, 0x0b, 0x00, 0x00, 'd', 'n', 's'}));
     }
+    {  // frame.rs:747-784 FrameSlice boundaries (IPv4/TCP; IPv6 + hop-by-hop + UDP)
+        std::vector<std::vector<uint8_t>> sf = {fx["frame_slice_ipv4_tcp"].bytes, fx["frame_slice_ipv6_hbh_udp"].bytes};
+        std::vector<Result<FrameSlice>> sl;
+        if (gpu) {
+            sl = eng->frame_slices(sf);
+        } else {
+            for (auto& b : sf) {
+                nexg_slice s;
+                nexo_slice_frame(b.data(), b.size(), 0, 0, &s);
+                sl.push_back(frame_slice_from(s, b.data(), b.size()));
+            }
+        }
+        CHECK(sl[0].is_ok() && sl[1].is_ok());
+        const FrameSlice& a = sl[0].value();
+        CHECK(a.datalink && a.datalink->data == sf[0].data() && a.datalink->len == 14);
+        CHECK(a.network && a.network->data == sf[0].data() + 14 && a.network->len == 20);
+        CHECK(a.transport && a.transport->data == sf[0].data() + 34 && a.transport->len == 20);
+        CHECK(a.payload.to_vec() == bytes("data"));
+        const FrameSlice& b6 = sl[1].value();
+        CHECK(b6.network && b6.network->len == 48 && b6.transport && b6.transport->len == 8);
+        CHECK(b6.payload.to_vec() == bytes("dns"));
+    }
+    if (gpu) {  // examples/udp_ping.rs:68-109 (192.168.1.100 -> 1.1.1.1, 53443 -> 33435, DF, TTL 64)
+        UdpPingTuple t;
+        t.source = Ipv4Addr{{192, 168, 1, 100}};
+        t.destination = Ipv4Addr{{1, 1, 1, 1}};
+        t.src_port = 53443;
+        t.dst_port = 33435;
+        UdpPingShape shape;
+        shape.src_mac = MacAddr{2, 0, 0, 0, 0, 1};
+        shape.dst_mac = MacAddr{2, 0, 0, 0, 0, 2};
+        auto built = eng->build_udp_ping({t, t}, shape);
+        CHECK(built.is_ok() && built.value().size() == 2 && built.value()[0].size() == 42);
+        std::vector<uint8_t> want(42);
+        nexo_build_udp4(shape.src_mac.data(), shape.dst_mac.data(), 0xC0A80164u, 0x01010101u, 53443, 33435, 0, 64, 2, 0,
+                        nullptr, 0, want.data());
+        CHECK(built.value()[0] == want);
+        auto parsed = eng->try_from_bufs(built.value());  // builder.rs -> Frame round trip
+        CHECK(parsed[0].is_ok() && parsed[0].value().checksums.ip_ok && parsed[0].value().checksums.l4_ok);
+        CHECK(parsed[0].value().ip->ipv4->total_length == 28 && parsed[0].value().transport->udp->length == 8);
+        CHECK(parsed[0].value().ip->ipv4->flags == 2 && parsed[0].value().ip->ipv4->ttl == 64);
+        UdpPingShape big = shape;  // builder/udp.rs:83 LengthOverflow
+        big.payload.assign(65535 - 28 + 1, 0);
+        auto over = eng->build_udp_ping({t}, big);
+        CHECK(over.is_err() && over.error() == BuildError::LengthOverflow);
+    }
     // every fixture: Frame fields == the record the oracle writes (device == oracle in --gpu)
     for (const auto& n : names) {
         const Fixture& fxt = fx[n];
