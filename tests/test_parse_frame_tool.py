@@ -65,3 +65,26 @@ def test_parse_capture_on_gpu(engine, oracle, tmp_path):
     assert got == want
     assert len(list(parse_capture(str(path), engine=engine, batch_frames=64, limit=70))) == \
         len(list(display_records(oracle.parse_frames(frames[:70]), frames[:70], 1, str(path))))
+
+
+@pytest.mark.gpu
+def test_cpp_parse_frame_matches_python(engine, oracle, tmp_path):
+    """tools/parse_frame (C++ host API) prints exactly what nex_amd.parse_frame
+    prints for the same capture (both: capture -> GPU batches -> display_frame)."""
+    import os
+    import subprocess
+    from nex_amd.parse_frame import parse_capture
+    from tests import pcapfile
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "parse_frame")
+    assert os.path.exists(exe), "build tools/parse_frame first (make -C tools parse_frame)"
+    frames = ([bytes.fromhex(v["frame"]) for v in helpers.golden()["frames"] if v["parse_flags"] == 0] +
+              helpers.crafted_frames() + [oracle.gen_frame(abi.WL_IMIX, i) for i in range(500)])
+    path = tmp_path / "cap.pcap"
+    path.write_bytes(pcapfile.classic(frames))
+    want = list(parse_capture(str(path), engine=engine, batch_frames=256))
+    r = subprocess.run([exe, str(path), "256"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = r.stdout.splitlines()
+    assert len(got) == len(want)
+    bad = [(i, g, w) for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, bad[:5]
