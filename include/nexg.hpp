@@ -307,7 +307,7 @@ inline Result<Frame> frame_from_record(const nexg_record& r, const uint8_t* b, s
     using namespace detail;
     const uint32_t f = r.flags;
     if (NEXG_STATUS(f)) return ParseError{(ParseErrorKind)NEXG_STATUS(f)};
-    (void)len;
+    if (r.payload_off + (size_t)r.payload_len > len || r.l3_off > len) throw Error("record does not fit its frame");
     Frame fr;
     const uint32_t l3 = r.l3_off;
     if (f & NEXG_L_ETHERNET) {
@@ -578,6 +578,45 @@ class Engine {  // one nexg context on one gfx950 device, one stream
     }
     nexg_ctx* ctx_ = nullptr;
     hipStream_t stream_ = nullptr;
+};
+
+/* ---- capture-file source (nexg_pcap_*; pcap::from_file, pcap.rs:95-109) -- */
+
+class PcapReader {  // classic pcap / pcapng, a batch of records per call
+   public:
+    explicit PcapReader(const std::string& path) {
+        if (nexg_pcap_open(path.c_str(), &p_) != NEXG_OK) throw Error("cannot open " + path + " as pcap/pcapng");
+    }
+    ~PcapReader() {
+        if (p_) nexg_pcap_close(p_);
+    }
+    PcapReader(const PcapReader&) = delete;
+    PcapReader& operator=(const PcapReader&) = delete;
+
+    int linktype() const { return nexg_pcap_linktype(p_); }  // 1 Ethernet, 101 raw IP
+    // ParseOption a capture of this link type needs (raw IP: from_ip_packet, offset 0)
+    ParseOption parse_option() const {
+        ParseOption o;
+        o.from_ip_packet = linktype() == 101;
+        return o;
+    }
+    // up to max_frames records (fewer at the end of the file, none after it);
+    // throws on a malformed file after the complete records before the damage
+    std::vector<std::vector<uint8_t>> next_batch(uint64_t max_frames, uint64_t data_cap = 64u << 20) {
+        buf_.resize(data_cap);
+        offs_.resize(max_frames + 1);
+        uint64_t n = 0;
+        if (nexg_pcap_read_batch(p_, buf_.data(), buf_.size(), offs_.data(), max_frames, nullptr, &n) != NEXG_OK)
+            throw Error(std::string("capture read failed: ") + nexg_pcap_last_error(p_));
+        std::vector<std::vector<uint8_t>> frames(n);
+        for (uint64_t i = 0; i < n; i++) frames[i].assign(buf_.begin() + offs_[i], buf_.begin() + offs_[i + 1]);
+        return frames;
+    }
+
+   private:
+    nexg_pcap* p_ = nullptr;
+    std::vector<uint8_t> buf_;
+    std::vector<uint64_t> offs_;
 };
 
 }  // namespace nexg

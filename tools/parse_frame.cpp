@@ -112,35 +112,25 @@ int main(int argc, char** argv) {
         return 2;
     }
     const uint64_t batch = argc > 2 ? strtoull(argv[2], nullptr, 0) : 65536;
-    nexg_pcap* cap = nullptr;
-    if (nexg_pcap_open(argv[1], &cap) != NEXG_OK) {
-        fprintf(stderr, "cannot open %s\n", argv[1]);
+    try {
+        nexg::PcapReader cap(argv[1]);
+        const nexg::ParseOption opt = cap.parse_option();
+        nexg::Engine eng(0);
+        uint64_t no = 1;
+        for (;;) {
+            const auto frames = cap.next_batch(batch, batch * 2048);
+            if (frames.empty()) break;
+            const auto res = eng.try_from_bufs(frames, opt);
+            for (size_t i = 0; i < frames.size(); i++, no++) {
+                printf("---- Interface: %s, No.: %llu, Total Length: %zu bytes ----\n", argv[1],
+                       (unsigned long long)no, frames[i].size());
+                if (res[i].is_err()) printf("Failed to parse packet as Frame\n");
+                else display_frame(res[i].value());
+            }
+        }
+    } catch (const nexg::Error& e) {
+        fprintf(stderr, "%s\n", e.what());
         return 1;
     }
-    nexg::ParseOption opt;
-    if (nexg_pcap_linktype(cap) == 101) opt.from_ip_packet = true;  // LINKTYPE_RAW: IP at offset 0
-    nexg::Engine eng(0);
-    std::vector<uint8_t> data(batch * 2048);
-    std::vector<uint64_t> offs(batch + 1);
-    uint64_t no = 1;
-    for (;;) {
-        uint64_t n = 0;
-        if (nexg_pcap_read_batch(cap, data.data(), data.size(), offs.data(), batch, nullptr, &n) != NEXG_OK) {
-            fprintf(stderr, "%s\n", nexg_pcap_last_error(cap));
-            nexg_pcap_close(cap);
-            return 1;
-        }
-        if (n == 0) break;
-        std::vector<std::vector<uint8_t>> frames(n);
-        for (uint64_t i = 0; i < n; i++) frames[i].assign(data.begin() + offs[i], data.begin() + offs[i + 1]);
-        const auto res = eng.try_from_bufs(frames, opt);
-        for (uint64_t i = 0; i < n; i++, no++) {
-            printf("---- Interface: %s, No.: %llu, Total Length: %zu bytes ----\n", argv[1],
-                   (unsigned long long)no, frames[i].size());
-            if (res[i].is_err()) printf("Failed to parse packet as Frame\n");
-            else display_frame(res[i].value());
-        }
-    }
-    nexg_pcap_close(cap);
     return 0;
 }
