@@ -93,6 +93,20 @@ __global__ __launch_bounds__(256) void k_wv16(const uint8_t* data, uint64_t n16,
             reinterpret_cast<const uint4*>(s_d)[threadIdx.x];
 }
 
+// descriptor stream into a small wrapping output window (wmask + 1 entries):
+// are writes that stay cache-resident cheaper than writes that reach HBM?
+__global__ __launch_bounds__(256) void k_wwin(const uint8_t* data, uint64_t n16, uint2* out, uint64_t wmask) {
+    const uint64_t base = (uint64_t)blockIdx.x * 1024;
+    uint32_t x = 0;
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = load16<true>(data + 16 * (base + threadIdx.x + 256 * k));
+#pragma unroll
+    for (int k = 0; k < 4; k++) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    const uint64_t fr = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    out[fr & wmask] = make_uint2(x, (uint32_t)fr);
+}
+
 // T tiles per workgroup, the T descriptor blocks written together at the end
 template <int T>
 __global__ __launch_bounds__(256) void k_wbatch(const uint8_t* data, uint64_t n16, uint2* out) {
@@ -302,6 +316,10 @@ int main(int argc, char** argv) {
         uint8_t* o8 = reinterpret_cast<uint8_t*>(out);
         const dim3 g(n16 / 1024);
         vs.push_back({"w8_plain", [=]() { hipLaunchKernelGGL((k_wv<8, 0>), g, dim3(256), 0, 0, data, n16, o8); }});
+        for (int lg : {16, 19, 22, 24}) {  // 512 KiB, 4 MiB, 32 MiB, 128 MiB windows
+            const uint64_t m = (1ull << lg) - 1;
+            vs.push_back({"w8_win" + std::to_string(8ull << lg >> 20) + "MiB", [=]() { hipLaunchKernelGGL(k_wwin, g, dim3(256), 0, 0, data, n16, out, m); }});
+        }
         vs.push_back({"w8_via16", [=]() { hipLaunchKernelGGL(k_wv16, g, dim3(256), 0, 0, data, n16, o8); }});
         vs.push_back({"w8_nt", [=]() { hipLaunchKernelGGL((k_wv<8, 1>), g, dim3(256), 0, 0, data, n16, o8); }});
         vs.push_back({"w8_sc01nt", [=]() { hipLaunchKernelGGL((k_wv<8, 2>), g, dim3(256), 0, 0, data, n16, o8); }});
