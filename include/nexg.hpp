@@ -408,6 +408,7 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
     }
     ~Engine() {
+        for (auto& b : scratch_) (void)hipFree(b.p);
         if (stream_) (void)hipStreamDestroy(stream_);
         if (ctx_) nexg_ctx_destroy(ctx_);
     }
@@ -431,16 +432,17 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         const uint64_t n = frames.size();
         std::vector<Result<Frame>> out;
         if (n == 0) return out;
-        HostBatch hb(frames, stream_);
-        DeviceBuf d_recs(n * 64), d_opts(n * 96);
-        parse(hb.fb, option, mode, NEXG_OUT_RECORD, d_recs.p);
-        check(nexg_decode_options(ctx_, &hb.fb, static_cast<const nexg_record*>(d_recs.p),
-                                  static_cast<nexg_options*>(d_opts.p), stream_),
+        HostBatch hb(*this, frames);
+        void* d_recs = scratch(3, n * 64);
+        void* d_opts = scratch(4, n * 96);
+        parse(hb.fb, option, mode, NEXG_OUT_RECORD, d_recs);
+        check(nexg_decode_options(ctx_, &hb.fb, static_cast<const nexg_record*>(d_recs),
+                                  static_cast<nexg_options*>(d_opts), stream_),
               "nexg_decode_options");
         std::vector<nexg_record> recs(n);
         std::vector<nexg_options> opts(n);
-        check_hip(hipMemcpyAsync(recs.data(), d_recs.p, n * 64, hipMemcpyDeviceToHost, stream_), "D2H");
-        check_hip(hipMemcpyAsync(opts.data(), d_opts.p, n * 96, hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipMemcpyAsync(recs.data(), d_recs, n * 64, hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipMemcpyAsync(opts.data(), d_opts, n * 96, hipMemcpyDeviceToHost, stream_), "D2H");
         check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
         out.reserve(n);
         for (uint64_t i = 0; i < n; i++)
@@ -455,11 +457,11 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         const uint64_t n = frames.size();
         std::vector<Result<FrameSlice>> out;
         if (n == 0) return out;
-        HostBatch hb(frames, stream_);
-        DeviceBuf d_sl(n * 16);
-        parse(hb.fb, option, ParseMode::Lenient, NEXG_OUT_SLICE, d_sl.p);
+        HostBatch hb(*this, frames);
+        void* d_sl = scratch(3, n * 16);
+        parse(hb.fb, option, ParseMode::Lenient, NEXG_OUT_SLICE, d_sl);
         std::vector<nexg_slice> sl(n);
-        check_hip(hipMemcpyAsync(sl.data(), d_sl.p, n * 16, hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipMemcpyAsync(sl.data(), d_sl, n * 16, hipMemcpyDeviceToHost, stream_), "D2H");
         check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
         out.reserve(n);
         for (uint64_t i = 0; i < n; i++) out.push_back(frame_slice_from(sl[i], frames[i].data(), frames[i].size()));
@@ -487,32 +489,37 @@ class Engine {  // one nexg context on one gfx950 device, one stream
             dp[i] = t[i].dst_port;
             id[i] = t[i].ip_id;
         }
-        DeviceBuf d_src(n * 4), d_dst(n * 4), d_sp(n * 2), d_dp(n * 2), d_id(n * 2), d_pl(shape.payload.size()),
-            d_out((uint64_t)n * L);
-        check_hip(hipMemcpyAsync(d_src.p, src.data(), n * 4, hipMemcpyHostToDevice, stream_), "H2D");
-        check_hip(hipMemcpyAsync(d_dst.p, dst.data(), n * 4, hipMemcpyHostToDevice, stream_), "H2D");
-        check_hip(hipMemcpyAsync(d_sp.p, sp.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
-        check_hip(hipMemcpyAsync(d_dp.p, dp.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
-        check_hip(hipMemcpyAsync(d_id.p, id.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
+        void* d_src = scratch(5, n * 4);
+        void* d_dst = scratch(6, n * 4);
+        void* d_sp = scratch(7, n * 2);
+        void* d_dp = scratch(8, n * 2);
+        void* d_id = scratch(9, n * 2);
+        void* d_pl = scratch(10, shape.payload.size());
+        void* d_out = scratch(11, (uint64_t)n * L);
+        check_hip(hipMemcpyAsync(d_src, src.data(), n * 4, hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_dst, dst.data(), n * 4, hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_sp, sp.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_dp, dp.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_id, id.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
         if (!shape.payload.empty())
-            check_hip(hipMemcpyAsync(d_pl.p, shape.payload.data(), shape.payload.size(), hipMemcpyHostToDevice,
+            check_hip(hipMemcpyAsync(d_pl, shape.payload.data(), shape.payload.size(), hipMemcpyHostToDevice,
                                      stream_), "H2D");
         nexg_udp4_build p{};
-        p.src_ip = static_cast<const uint32_t*>(d_src.p);
-        p.dst_ip = static_cast<const uint32_t*>(d_dst.p);
-        p.src_port = static_cast<const uint16_t*>(d_sp.p);
-        p.dst_port = static_cast<const uint16_t*>(d_dp.p);
-        p.ip_id = static_cast<const uint16_t*>(d_id.p);
-        p.payload = shape.payload.empty() ? nullptr : static_cast<const uint8_t*>(d_pl.p);
+        p.src_ip = static_cast<const uint32_t*>(d_src);
+        p.dst_ip = static_cast<const uint32_t*>(d_dst);
+        p.src_port = static_cast<const uint16_t*>(d_sp);
+        p.dst_port = static_cast<const uint16_t*>(d_dp);
+        p.ip_id = static_cast<const uint16_t*>(d_id);
+        p.payload = shape.payload.empty() ? nullptr : static_cast<const uint8_t*>(d_pl);
         p.payload_len = (uint32_t)shape.payload.size();
         memcpy(p.def_src_mac, shape.src_mac.data(), 6);
         memcpy(p.def_dst_mac, shape.dst_mac.data(), 6);
         p.ttl = shape.ttl;
         p.ip_flags = shape.ip_flags;
         p.count = n;
-        check(nexg_build_udp4_batch(ctx_, &p, static_cast<uint8_t*>(d_out.p), L, stream_), "nexg_build_udp4_batch");
+        check(nexg_build_udp4_batch(ctx_, &p, static_cast<uint8_t*>(d_out), L, stream_), "nexg_build_udp4_batch");
         std::vector<uint8_t> host((uint64_t)n * L);
-        check_hip(hipMemcpyAsync(host.data(), d_out.p, host.size(), hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipMemcpyAsync(host.data(), d_out, host.size(), hipMemcpyDeviceToHost, stream_), "D2H");
         check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
         frames.reserve(n);
         for (uint64_t i = 0; i < n; i++) frames.emplace_back(host.begin() + i * L, host.begin() + (i + 1) * L);
@@ -520,44 +527,52 @@ class Engine {  // one nexg context on one gfx950 device, one stream
     }
 
    private:
-    struct DeviceBuf {
+    // grow-only device scratch, one buffer per slot: every call ends with a
+    // stream sync, so the next call may reuse them (no hipMalloc per batch)
+    struct Scratch {
         void* p = nullptr;
-        explicit DeviceBuf(size_t n) {
-            if (hipMalloc(&p, n ? n : 16) != hipSuccess) throw Error("hipMalloc failed");
-        }
-        ~DeviceBuf() { (void)hipFree(p); }
-        DeviceBuf(const DeviceBuf&) = delete;
-        DeviceBuf& operator=(const DeviceBuf&) = delete;
+        size_t size = 0;
     };
+    std::vector<Scratch> scratch_;
+    void* scratch(size_t slot, size_t n) {
+        if (slot >= scratch_.size()) scratch_.resize(slot + 1);
+        Scratch& b = scratch_[slot];
+        if (b.size < n || !b.p) {
+            if (b.p) (void)hipFree(b.p);
+            b.p = nullptr;
+            b.size = 0;
+            check_hip(hipMalloc(&b.p, n ? n : 16), "hipMalloc");
+            b.size = n ? n : 16;
+        }
+        return b.p;
+    }
     // host frames packed (4-B aligned starts) with offsets + lengths, on the device
     struct HostBatch {
         std::vector<uint8_t> data;
         std::vector<uint64_t> offs;
         std::vector<uint32_t> lens;
-        DeviceBuf d_data, d_offs, d_lens;
         nexg_frames fb{};
-        static size_t packed_size(const std::vector<std::vector<uint8_t>>& frames) {
-            size_t pos = 0;
-            for (const auto& f : frames) pos += (f.size() + 3) & ~(size_t)3;
-            return pos ? pos : 16;
-        }
-        HostBatch(const std::vector<std::vector<uint8_t>>& frames, hipStream_t s)
-            : data(packed_size(frames), 0), offs(frames.size()), lens(frames.size()),
-              d_data(data.size()), d_offs(frames.size() * 8), d_lens(frames.size() * 4) {
+        HostBatch(Engine& e, const std::vector<std::vector<uint8_t>>& frames)
+            : offs(frames.size()), lens(frames.size()) {
             uint64_t pos = 0;
             for (size_t i = 0; i < frames.size(); i++) {
                 offs[i] = pos;
                 lens[i] = (uint32_t)frames[i].size();
-                if (!frames[i].empty()) memcpy(data.data() + pos, frames[i].data(), frames[i].size());
                 pos += (frames[i].size() + 3) & ~(uint64_t)3;
             }
-            check_hip(hipMemcpyAsync(d_data.p, data.data(), data.size(), hipMemcpyHostToDevice, s), "H2D");
-            check_hip(hipMemcpyAsync(d_offs.p, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, s), "H2D");
-            check_hip(hipMemcpyAsync(d_lens.p, lens.data(), lens.size() * 4, hipMemcpyHostToDevice, s), "H2D");
-            fb.data = static_cast<const uint8_t*>(d_data.p);
+            data.assign(pos ? pos : 16, 0);
+            for (size_t i = 0; i < frames.size(); i++)
+                if (!frames[i].empty()) memcpy(data.data() + offs[i], frames[i].data(), frames[i].size());
+            void* d_data = e.scratch(0, data.size());
+            void* d_offs = e.scratch(1, offs.size() * 8);
+            void* d_lens = e.scratch(2, lens.size() * 4);
+            check_hip(hipMemcpyAsync(d_data, data.data(), data.size(), hipMemcpyHostToDevice, e.stream_), "H2D");
+            check_hip(hipMemcpyAsync(d_offs, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, e.stream_), "H2D");
+            check_hip(hipMemcpyAsync(d_lens, lens.data(), lens.size() * 4, hipMemcpyHostToDevice, e.stream_), "H2D");
+            fb.data = static_cast<const uint8_t*>(d_data);
             fb.data_bytes = data.size();
-            fb.offsets = static_cast<const uint64_t*>(d_offs.p);
-            fb.lengths = static_cast<const uint32_t*>(d_lens.p);
+            fb.offsets = static_cast<const uint64_t*>(d_offs);
+            fb.lengths = static_cast<const uint32_t*>(d_lens);
             fb.count = frames.size();
         }
     };
