@@ -12,7 +12,8 @@ channel, pcap.rs:95-109), are moved to the GPU a batch at a time and parsed by
 
 Enum names follow the reference's `Debug` output for the common values
 (EtherType::new, ethernet.rs:56-80; IpNextProtocol, ip.rs:308-456); other
-values print as `Unknown(0x....)` / `IpNextProtocol(n)` — display only, the
+EtherTypes print as the derived Debug does (`Unknown(<decimal>)`); IP protocol
+numbers outside the table print as `IpNextProtocol(n)` — display only, the
 parsed values are exact.
 """
 import argparse
@@ -30,7 +31,7 @@ ETHERTYPE_NAMES = {0x0800: "Ipv4", 0x0806: "Arp", 0x0842: "WakeOnLan", 0x22F3: "
                    0x8819: "CobraNet", 0x8847: "Mpls", 0x8848: "MplsMcast",
                    0x8863: "PppoeDiscovery", 0x8864: "PppoeSession", 0x8100: "Vlan",
                    0x88A8: "PBridge", 0x88CC: "Lldp", 0x88F7: "Ptp", 0x8902: "Cfm",
-                   0x9100: "QinQ"}
+                   0x9100: "QinQ", 0x8899: "Rldp"}
 IPPROTO_NAMES = {0: "Hopopt", 1: "Icmp", 2: "Igmp", 4: "Ipv4", 6: "Tcp", 17: "Udp",
                  41: "Ipv6", 43: "Ipv6Route", 44: "Ipv6Frag", 47: "Gre", 50: "Esp", 51: "Ah",
                  58: "Icmpv6", 59: "Ipv6NoNxt", 60: "Ipv6Opts", 132: "Sctp", 255: "Reserved"}
@@ -42,7 +43,14 @@ def _mac(b: bytes) -> str:
 
 
 def ethertype_debug(v: int) -> str:
-    return ETHERTYPE_NAMES.get(v, f"Unknown(0x{v:04x})")
+    """EtherType's derived Debug: the variant name, or Unknown(<decimal u16>)."""
+    return ETHERTYPE_NAMES.get(v, f"Unknown({v})")
+
+
+def ipv6_display(a) -> str:
+    """std::net::Ipv6Addr's Display: IPv4-mapped addresses in dotted form,
+    otherwise RFC 5952 (what ipaddress prints)."""
+    return f"::ffff:{a.ipv4_mapped}" if a.ipv4_mapped is not None else str(a)
 
 
 def ipproto_debug(v: int) -> str:
@@ -68,7 +76,7 @@ def display_frame(frame: Frame) -> List[str]:
             out.append(f"  IPv4: {ip.ipv4.source} -> {ip.ipv4.destination} "
                        f"(protocol: {ipproto_debug(ip.ipv4.next_level_protocol)})")
         if ip.ipv6 is not None:
-            out.append(f"  IPv6: {ip.ipv6.source} -> {ip.ipv6.destination} "
+            out.append(f"  IPv6: {ipv6_display(ip.ipv6.source)} -> {ipv6_display(ip.ipv6.destination)} "
                        f"(next header: {ipproto_debug(ip.ipv6.next_header)})")
         if ip.icmp is not None:
             out.append("  ICMP: present")

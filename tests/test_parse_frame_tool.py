@@ -37,7 +37,7 @@ def test_display_other_layers(oracle):
     assert "  ICMPv6: present" in lines
     fr = _golden("unknown_ethertype_keeps_payload")  # frame.rs:665-680
     lines = display_frame(frame_from_record(oracle.parse_frame(fr), fr))
-    assert lines[1].endswith("(Unknown(0x88b5))") and lines[-1] == "  Payload: 4 bytes"
+    assert lines[1].endswith("(Unknown(34997))") and lines[-1] == "  Payload: 4 bytes"  # 0x88b5
     fr = _golden("tcp_basic_parse")  # tcp.rs:1276-1314
     lines = display_frame(frame_from_record(oracle.parse_frame(fr), fr))
     assert "  TCP: 49511 -> 9000" in lines
@@ -77,11 +77,15 @@ def test_cpp_parse_frame_matches_python(engine, oracle, tmp_path):
     from tests import pcapfile
     exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "parse_frame")
     assert os.path.exists(exe), "build tools/parse_frame first (make -C tools parse_frame)"
+    mapped = (bytes(12) + b"\x86\xdd" + bytes([0x60, 0, 0, 0, 0, 8, 17, 64]) +
+              bytes(10) + b"\xff\xff" + bytes([1, 2, 3, 4]) + bytes(15) + b"\x01" +
+              bytes([0x12, 0x34, 0, 53, 0, 8, 0, 0]))  # IPv6/UDP from ::ffff:1.2.3.4 to ::1
     frames = ([bytes.fromhex(v["frame"]) for v in helpers.golden()["frames"] if v["parse_flags"] == 0] +
-              helpers.crafted_frames() + [oracle.gen_frame(abi.WL_IMIX, i) for i in range(500)])
+              helpers.crafted_frames() + [oracle.gen_frame(abi.WL_IMIX, i) for i in range(500)] + [mapped])
     path = tmp_path / "cap.pcap"
     path.write_bytes(pcapfile.classic(frames))
     want = list(parse_capture(str(path), engine=engine, batch_frames=256))
+    assert "  IPv6: ::ffff:1.2.3.4 -> ::1 (next header: Udp)" in want
     r = subprocess.run([exe, str(path), "256"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     got = r.stdout.splitlines()

@@ -22,11 +22,16 @@ std::string mac(const nexg::MacAddr& m) {
     return b;
 }
 
-// std::net::Ipv6Addr's Display (RFC 5952: longest run of >= 2 zero groups as ::,
-// IPv4-mapped / compatible forms as the Python ipaddress module prints them)
+// std::net::Ipv6Addr's Display: IPv4-mapped addresses as ::ffff:a.b.c.d,
+// otherwise RFC 5952 (longest run of >= 2 zero groups as ::, the first on ties)
 std::string ipv6(const nexg::Ipv6Addr& a) {
     uint16_t g[8];
     for (int i = 0; i < 8; i++) g[i] = (uint16_t)(a.octets[2 * i] << 8 | a.octets[2 * i + 1]);
+    if (!g[0] && !g[1] && !g[2] && !g[3] && !g[4] && g[5] == 0xffff) {
+        char b[32];
+        snprintf(b, sizeof(b), "::ffff:%u.%u.%u.%u", a.octets[12], a.octets[13], a.octets[14], a.octets[15]);
+        return b;
+    }
     int best = -1, blen = 0;
     for (int i = 0; i < 8;) {
         if (g[i] != 0) { i++; continue; }
@@ -51,7 +56,7 @@ const std::map<uint16_t, const char*> kEtherTypes = {
     {0x8035, "Rarp"}, {0x809B, "AppleTalk"}, {0x80F3, "Aarp"}, {0x8137, "Ipx"}, {0x8204, "Qnx"},
     {0x86DD, "Ipv6"}, {0x8808, "FlowControl"}, {0x8819, "CobraNet"}, {0x8847, "Mpls"}, {0x8848, "MplsMcast"},
     {0x8863, "PppoeDiscovery"}, {0x8864, "PppoeSession"}, {0x8100, "Vlan"}, {0x88A8, "PBridge"},
-    {0x88CC, "Lldp"}, {0x88F7, "Ptp"}, {0x8902, "Cfm"}, {0x9100, "QinQ"}};
+    {0x88CC, "Lldp"}, {0x88F7, "Ptp"}, {0x8902, "Cfm"}, {0x9100, "QinQ"}, {0x8899, "Rldp"}};
 const std::map<uint8_t, const char*> kProtocols = {
     {0, "Hopopt"}, {1, "Icmp"}, {2, "Igmp"}, {4, "Ipv4"}, {6, "Tcp"}, {17, "Udp"}, {41, "Ipv6"},
     {43, "Ipv6Route"}, {44, "Ipv6Frag"}, {47, "Gre"}, {50, "Esp"}, {51, "Ah"}, {58, "Icmpv6"},
@@ -60,9 +65,7 @@ const std::map<uint8_t, const char*> kProtocols = {
 std::string ethertype(uint16_t v) {
     auto it = kEtherTypes.find(v);
     if (it != kEtherTypes.end()) return it->second;
-    char b[24];
-    snprintf(b, sizeof(b), "Unknown(0x%04x)", v);
-    return b;
+    return "Unknown(" + std::to_string(v) + ")";  // EtherType's derived Debug
 }
 std::string protocol(uint8_t v) {
     auto it = kProtocols.find(v);
