@@ -108,6 +108,7 @@ int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_
     a.opt_flags = option ? option->flags : 0u;
     a.ip_offset = option ? option->ip_offset : 0u;
     a.out = out;
+    a.tile_order = nexg::tile_order_for(a);
     const nexg::ParseVariant v = nexg::choose_parse_variant(a);
     return hip_status(ctx, nexg::launch_parse(v, a, out_kind, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);

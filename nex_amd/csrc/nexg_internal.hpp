@@ -19,6 +19,7 @@ struct ParseArgs {
     uint32_t opt_flags;
     uint32_t ip_offset;
     void* out;
+    uint32_t tile_order = 0;  // fixed-stride tiles: 0 in grid order, 1 XCD-contiguous
 };
 
 // Kernel variants of the parse path.
@@ -31,6 +32,7 @@ enum class ParseVariant {
 };
 
 hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStream_t s);
+uint32_t tile_order_for(const ParseArgs& a);
 ParseVariant choose_parse_variant(const ParseArgs& a);
 
 hipError_t launch_checksum(const ParseArgs& a, uint32_t skipword, uint16_t* out, hipStream_t s);

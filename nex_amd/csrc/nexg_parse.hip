@@ -12,9 +12,28 @@
 //       of chunk sums (k_parse_span).
 //   TwoPass : explicit lengths (frames anywhere, in any order): quarter-wave
 //       tail sums past byte 80, then one lane per frame on an 80-B head.
+#include <stdlib.h>
+#include <string.h>
+
 #include "parse_kernels.hpp"
 
 namespace nexg {
+
+// Tile order of the fixed-stride tile kernels: NEXG_TILE_ORDER=linear|xcd
+// overrides (measurement); otherwise XCD-contiguous from 3 GiB up. Measured
+// (profiles/r01_staging/tile_order.txt): grid order is 3 % faster at 1 GiB,
+// equal at 2 GiB; XCD order 6 % faster at 4 GiB and 10 % at 16 GiB. The span
+// kernel (packed batches) keeps grid order: XCD order was 3 % slower at 6 GB.
+uint32_t tile_order_for(const ParseArgs& a) {
+    static const int forced = [] {
+        const char* e = getenv("NEXG_TILE_ORDER");
+        if (!e) return -1;
+        return strcmp(e, "xcd") == 0 ? 1 : (strcmp(e, "linear") == 0 ? 0 : -1);
+    }();
+    if (forced >= 0) return (uint32_t)forced;
+    constexpr uint64_t kXcdOrderBytes = 3ull << 30;
+    return !a.offsets && a.count * (uint64_t)a.stride >= kXcdOrderBytes ? 1u : 0u;
+}
 
 ParseVariant choose_parse_variant(const ParseArgs& a) {
     const bool aligned = (reinterpret_cast<uint64_t>(a.data) & 15u) == 0;

@@ -67,6 +67,16 @@ __device__ __forceinline__ void stage_record(uint8_t* slot, const nexg_record& r
     for (int k = 0; k < 4; k++) reinterpret_cast<uint4*>(slot)[k] = v[k];
 }
 
+// Tile handled by this workgroup. order 1: workgroups are dispatched to the 8
+// XCDs round-robin (blockIdx % 8), so tile = (b % 8) * (nb / 8) + b / 8 gives
+// each XCD one contiguous eighth of the batch (its own pages and L2 lines);
+// the nb % 8 tail keeps grid order. A bijection on [0, nb) either way.
+__device__ __forceinline__ uint64_t tile_index(uint32_t order) {
+    const uint32_t b = blockIdx.x, q = gridDim.x >> 3;
+    if (!order || b >= (q << 3)) return b;
+    return (uint64_t)(b & 7u) * q + (b >> 3);
+}
+
 // MODE 0: fixed stride tile staging (STRIDE = 0 -> runtime stride).
 // MODE 1: per-lane window staging.
 template <int MODE, int OUT, int STRIDE, int WIN, bool FAST = true, bool NT = false>
@@ -74,7 +84,7 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
     constexpr uint32_t PITCH = WIN + 16;
     __shared__ __attribute__((aligned(16))) uint8_t smem[kTile * PITCH];
     const uint32_t tid = threadIdx.x;
-    const uint64_t first = (uint64_t)blockIdx.x * kTile;
+    const uint64_t first = (MODE == 0 ? tile_index(a.tile_order) : (uint64_t)blockIdx.x) * kTile;
     const uint64_t left = a.count - first;
     const uint32_t nf = left < kTile ? (uint32_t)left : kTile;
     const uint64_t idx = first + tid;
@@ -463,7 +473,7 @@ __global__ __launch_bounds__(256) void k_parse_span(ParseArgs a) {
     __shared__ uint32_t s_wsum[NB][4];
     __shared__ uint64_t s_span[2];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    const uint64_t f0 = (uint64_t)blockIdx.x * kTile;
+    const uint64_t f0 = (uint64_t)blockIdx.x * kTile;  // grid order: XCD order measured slower here
     const uint64_t idx = f0 + t;
     const uint32_t nf = a.count - f0 < kTile ? (uint32_t)(a.count - f0) : kTile;
     const uint64_t base = reinterpret_cast<uint64_t>(a.data);

@@ -98,9 +98,11 @@ def test_generators_match_oracle(engine, oracle):
         assert got == want
 
 
-@pytest.mark.parametrize("workload,count", [(abi.WL_UDP64, 16 << 20), (abi.WL_IMIX, 16 << 20)])
+@pytest.mark.parametrize("workload,count", [(abi.WL_UDP64, 16 << 20), (abi.WL_IMIX, 16 << 20),
+                                            (abi.WL_UDP64, 52 << 20)])
 def test_full_size_sampled(engine, oracle, workload, count):
-    """BASELINE.json full sizes: sample 65536 frames bit-exact + properties."""
+    """BASELINE.json full sizes: sample 65536 frames bit-exact + properties.
+    52M x 64 B (3.25 GiB) takes the XCD-contiguous tile order."""
     import torch
     b = engine.gen_batch(workload, count)
     desc = engine.parse(b, out_kind=abi.OUT_DESC)
