@@ -130,6 +130,31 @@ add("frame_slice_ipv6_hbh_udp", "frame.rs:764-784 (Frame path: HBH -> no transpo
     slice_expect={"cite": "frame.rs:764-784", "network_len": 48, "transport_len": 8,
                   "payload_bytes": b"dns".hex(), "ip_protocol": 17})
 
+# ---- ethernet.rs:458-539, ipv6.rs:672-704, icmpv6.rs:2531-2549 (per-protocol
+# tests; the asserted bytes as Frames, the asserted values as expectations) ---
+add("ethernet_parse_basic", "ethernet.rs:458-476",
+    bytes([0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff, 0x11, 0x22, 0x33, 0x44, 0x55, 0x66, 0x08, 0x00,
+           0xde, 0xad, 0xbe, 0xef]),
+    {"layers": ["eth", "ip"], "ethertype": 0x0800, "eth_dst": "aabbccddeeff", "eth_src": "112233445566"},
+    note="EtherType Ipv4 with a 4-B payload: IPv4 fails -> ip Some(all None), payload empty (Q4)")
+add("ethernet_too_short", "ethernet.rs:510-528 (BufferTooShort, actual 4)", bytes([0, 1, 2, 3]),
+    {"status": 1})
+add("ethernet_unknown_ethertype_dead", "ethernet.rs:530-539 (EtherType::Unknown(0xdead))",
+    bytes([0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff, 0x11, 0x22, 0x33, 0x44, 0x55, 0x66, 0xde, 0xad,
+           0x00, 0x11, 0x22, 0x33]),
+    {"layers": ["eth"], "ethertype": 0xdead, "payload": "00112233"})
+add("ipv6_basic_header_fields", "ipv6.rs:672-704 (tc 0xaa, flow 0x12345, Udp, hop 64, ::1 -> ::)",
+    eth(ipv6_hdr(b"", 17, src=LO6, dst=bytes(16), tc_flow=(0x6a, 0xa1, 0x23, 0x45)), 0x86DD),
+    {"layers": ["eth", "ip", "ipv6", "transport"], "ip_tos": 0xaa, "ip_word": 0x12345, "ip_length": 0,
+     "ip_proto": 17, "ip_ttl": 64},
+    note="UDP over 0 bytes fails -> transport Some(None,None)")
+ECHO6 = bytes([0x80, 0x00, 0xbe, 0xef, 0x12, 0x34, 0x56, 0x78]) + b"ping!"
+add("icmpv6_echo_request_parse", "icmpv6.rs:2531-2549 (type EchoRequest, code 0, checksum 0xbeef, "
+    "id 0x1234, seq 0x5678, payload 'ping!')", eth(ipv6_hdr(ECHO6, 58), 0x86DD),
+    {"layers": ["eth", "ip", "ipv6", "icmpv6"], "l4_type": 128, "l4_code": 0, "l4_csum": 0xbeef,
+     "payload": (bytes([0x12, 0x34, 0x56, 0x78]) + b"ping!").hex()},
+    note="Frame.payload of ICMPv6 = bytes after the 4-B header (Q15): identifier, sequence, data")
+
 # ---- ipv4.rs:944-1204 ------------------------------------------------------
 IPV4_RT = bytes([0x45, 0x00, 0x00, 0x1c, 0x1c, 0x46, 0x40, 0x00, 0x40, 0x06, 0xb1, 0xe6,
                  0xc0, 0xa8, 0x00, 0x01, 0xc0, 0xa8, 0x00, 0xc7,

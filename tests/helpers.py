@@ -47,6 +47,9 @@ def check_expect(rec, frame: bytes, exp: dict, name=""):
             assert int(rec["ip_ver_ihl"]) & 15 == v, name
         elif k in ("ip_src", "ip_dst"):
             assert str(ipaddress.IPv4Address(int(rec[k]))) == v, name
+        elif k in ("eth_dst", "eth_src"):
+            e = fr.datalink.ethernet
+            assert (e.destination if k == "eth_dst" else e.source).hex() == v, name
         elif k == "ip_csum_consistent":
             assert int(rec["ip_csum_calc"]) != 0 or int(rec["ip_csum"]) == 0, name
         else:

@@ -88,6 +88,28 @@ int main(int argc, char** argv) {
     };
     auto bytes = [](const char* s) { return std::vector<uint8_t>(s, s + strlen(s)); };
 
+    {  // ethernet.rs:458-476, 510-539
+        const Frame& f = frame("ethernet_parse_basic");
+        CHECK(f.datalink->ethernet->destination == (MacAddr{0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff}));
+        CHECK(f.datalink->ethernet->source == (MacAddr{0x11, 0x22, 0x33, 0x44, 0x55, 0x66}));
+        CHECK(f.datalink->ethernet->ethertype == 0x0800);
+        const auto& s = got.at("ethernet_too_short");
+        CHECK(s.is_err() && s.error().kind == ParseErrorKind::BufferTooShort);
+        const Frame& u = frame("ethernet_unknown_ethertype_dead");
+        CHECK(u.datalink->ethernet->ethertype == 0xdead && !u.ip);
+    }
+    {  // ipv6.rs:672-704 header fields; icmpv6.rs:2531-2549 echo request
+        const Frame& f = frame("ipv6_basic_header_fields");
+        const auto& h = *f.ip->ipv6;
+        CHECK(h.version == 6 && h.traffic_class == 0xaa && h.flow_label == 0x12345);
+        CHECK(h.payload_length == 0 && h.next_header == 17 && h.hop_limit == 64);
+        CHECK(h.source.octets[15] == 1 && h.destination == Ipv6Addr{});
+        const Frame& e = frame("icmpv6_echo_request_parse");
+        CHECK(e.ip->icmpv6 && e.ip->icmpv6->icmpv6_type == 128 && e.ip->icmpv6->icmpv6_code == 0);
+        CHECK(e.ip->icmpv6->checksum == 0xbeef);
+        CHECK(e.payload.size() == 9 && e.payload[0] == 0x12 && e.payload[1] == 0x34 && e.payload[2] == 0x56 &&
+              e.payload[3] == 0x78 && e.payload[4] == 'p');
+    }
     {  // frame.rs:665-680 unknown EtherType keeps the payload
         const Frame& f = frame("unknown_ethertype_keeps_payload");
         CHECK(f.datalink && f.datalink->ethernet && f.datalink->ethernet->ethertype == 0x88b5);
