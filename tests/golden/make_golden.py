@@ -206,6 +206,23 @@ def ipv4_hdr(payload, proto, src=(10, 0, 0, 1), dst=(10, 0, 0, 2), ident=0):
                   *src, *dst]) + bytes(payload)
 
 
+# icmp.rs:728-815: EchoReply / DestinationUnreachable / TimeExceeded messages
+# as the tests assemble them (checksum field left 0: the tests only assert the
+# fields and payloads below), carried as IPv4 protocol 1 in a Frame
+for name, cite, msg, typ, code, pl in (
+        ("icmp_echo_reply_roundtrip", "icmp.rs:728-757 (id 5678, seq 99, payload 'pong')",
+         bytes([0, 0, 0, 0, 0x16, 0x2e, 0x00, 0x63]) + b"pong", 0, 0,
+         bytes([0x16, 0x2e, 0x00, 0x63]) + b"pong"),
+        ("icmp_destination_unreachable", "icmp.rs:759-787 (code 3, next_hop_mtu 1500, payload 'bad ip')",
+         bytes([3, 3, 0, 0, 0, 0, 0x05, 0xdc]) + b"bad ip", 3, 3, bytes([0, 0, 0x05, 0xdc]) + b"bad ip"),
+        ("icmp_time_exceeded", "icmp.rs:789-815 (unused 0xdeadbeef, payload 'timeout')",
+         bytes([11, 0, 0, 0, 0xde, 0xad, 0xbe, 0xef]) + b"timeout", 11, 0,
+         bytes([0xde, 0xad, 0xbe, 0xef]) + b"timeout")):
+    add(name, cite, eth(ipv4_hdr(msg, 1)),
+        {"layers": ["eth", "ip", "ipv4", "icmp"], "l4_type": typ, "l4_code": code, "payload": pl.hex()},
+        note="Frame.payload of ICMP = bytes after the 4-B header (Q15)")
+
+
 TCP_P = bytes([0xc1, 0x67, 0x23, 0x28, 0x90, 0x37, 0xd2, 0xb8, 0x94, 0x4b, 0xb2, 0x76, 0x80, 0x18,
                0x0f, 0xaf, 0xc0, 0x31, 0x00, 0x00, 0x01, 0x01, 0x08, 0x0a, 0x2c, 0x57, 0xcd, 0xa5,
                0x02, 0xa0, 0x41, 0x92]) + b"test"

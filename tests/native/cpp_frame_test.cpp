@@ -181,6 +181,16 @@ int main(int argc, char** argv) {
         CHECK(!f.transport);
         CHECK(f.payload.size() >= 4 && f.payload[0] == 0x04 && f.payload[1] == 0xd2 && f.payload[3] == 42);
     }
+    {  // icmp.rs:728-815 echo reply / destination unreachable / time exceeded
+        const Frame& r = frame("icmp_echo_reply_roundtrip");
+        CHECK(r.ip->icmp && r.ip->icmp->icmp_type == 0 && r.payload.size() == 8);
+        CHECK(detail::be16(r.payload.data()) == 5678 && detail::be16(r.payload.data() + 2) == 99);
+        const Frame& u = frame("icmp_destination_unreachable");
+        CHECK(u.ip->icmp->icmp_type == 3 && u.ip->icmp->icmp_code == 3);
+        CHECK(detail::be16(u.payload.data() + 2) == 1500);  // next_hop_mtu
+        const Frame& x = frame("icmp_time_exceeded");
+        CHECK(x.ip->icmp->icmp_type == 11 && x.payload.size() == 11 && x.payload[0] == 0xde);
+    }
     {  // icmpv6.rs:606-631 checksum KAT
         const Frame& f = frame("icmpv6_echo_request_lo");
         CHECK(f.ip->icmpv6 && f.ip->icmpv6->icmpv6_type == 128);
