@@ -18,6 +18,8 @@
  *   Engine::build_udp_ping  UdpPacketBuilder -> Ipv4PacketBuilder ->
  *                           EthernetPacketBuilder (udp_ping.rs:68-109) per
  *                           tuple, Result<frames, BuildError>
+ *   Engine::build_tcp_ping / build_icmp_ping   tcp_ping.rs:111-163 /
+ *                           icmp_ping.rs:67-102 (IPv4 or IPv6 per batch)
  * The device does the parse and the checksums (nexg_parse_batch,
  * NEXG_OUT_RECORD) and the option lists (nexg_decode_options); this header
  * only reads header fields out of the frame bytes at the offsets the device
@@ -262,6 +264,53 @@ struct UdpPingShape {
     MacAddr src_mac{}, dst_mac{};
     uint8_t ttl = 64;       // Ipv4PacketBuilder default (builder/ipv4.rs:37)
     uint8_t ip_flags = 2;   // udp_ping sets DontFragment
+    std::vector<uint8_t> payload;
+};
+
+// An IPv4 or IPv6 address for the builders (std::net::IpAddr)
+struct IpAddr {
+    uint8_t family = 4;                // 4 or 6
+    std::array<uint8_t, 16> octets{};  // IPv4 in the first 4 bytes
+    static IpAddr from(const Ipv4Addr& a) {
+        IpAddr r;
+        memcpy(r.octets.data(), a.octets.data(), 4);
+        return r;
+    }
+    static IpAddr from(const Ipv6Addr& a) {
+        IpAddr r;
+        r.family = 6;
+        r.octets = a.octets;
+        return r;
+    }
+};
+
+// tcp_ping's frame (examples/tcp_ping.rs:111-163): TcpPacketBuilder ->
+// Ipv4/Ipv6PacketBuilder -> EthernetPacketBuilder
+struct TcpPingTuple {
+    IpAddr source, destination;
+    uint16_t src_port = 0, dst_port = 0, ip_id = 0;
+    uint32_t sequence = 0, acknowledgement = 0;
+};
+struct TcpPingShape {
+    MacAddr src_mac{}, dst_mac{};
+    uint8_t ttl = 64, ip_flags = 2, tos = 0;
+    uint32_t flow_label = 0;
+    uint8_t flags = 0x02;  // SYN
+    uint16_t window = 0xffff, urgent_ptr = 0;
+    std::vector<uint8_t> options;  // encoded TcpOptionPacket bytes (padded to 4 B on the wire)
+    std::vector<uint8_t> payload;
+};
+
+// icmp_ping's frame (examples/icmp_ping.rs:67-102): an echo request
+// (IcmpPacketBuilder / Icmpv6PacketBuilder with echo_fields)
+struct IcmpPingTuple {
+    IpAddr source, destination;
+    uint16_t identifier = 0, sequence = 0, ip_id = 0;
+};
+struct IcmpPingShape {
+    MacAddr src_mac{}, dst_mac{};
+    uint8_t ttl = 64, ip_flags = 2, tos = 0;
+    uint32_t flow_label = 0;
     std::vector<uint8_t> payload;
 };
 
@@ -526,7 +575,119 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         return frames;
     }
 
+    // tcp_ping's build for every tuple (one address family per batch:
+    // BuildError::AddressFamilyMismatch otherwise, builder/error.rs)
+    Result<std::vector<std::vector<uint8_t>>, BuildError> build_tcp_ping(const std::vector<TcpPingTuple>& t,
+                                                                         const TcpPingShape& shape) {
+        std::vector<std::vector<uint8_t>> frames;
+        if (t.empty()) return frames;
+        if (shape.options.size() > 40) return BuildError::LengthOverflow;
+        const uint8_t fam = t[0].source.family;
+        for (const auto& x : t)
+            if (x.source.family != fam || x.destination.family != fam) return BuildError::AddressFamilyMismatch;
+        const uint64_t n = t.size();
+        const uint32_t L = 14u + (fam == 4 ? 20u : 40u) + 20u + (((uint32_t)shape.options.size() + 3u) & ~3u) +
+                           (uint32_t)shape.payload.size();
+        nexg_tcp_build p{};
+        fill_ip(p.ip, t, shape.src_mac, shape.dst_mac, fam, shape.ttl, shape.ip_flags, shape.tos, shape.flow_label, 5);
+        std::vector<uint16_t> sp(n), dp(n);
+        std::vector<uint32_t> seq(n), ack(n);
+        for (uint64_t i = 0; i < n; i++) {
+            sp[i] = t[i].src_port;
+            dp[i] = t[i].dst_port;
+            seq[i] = t[i].sequence;
+            ack[i] = t[i].acknowledgement;
+        }
+        p.src_port = static_cast<const uint16_t*>(upload(10, sp.data(), n * 2));
+        p.dst_port = static_cast<const uint16_t*>(upload(11, dp.data(), n * 2));
+        p.seq = static_cast<const uint32_t*>(upload(12, seq.data(), n * 4));
+        p.ack = static_cast<const uint32_t*>(upload(13, ack.data(), n * 4));
+        p.payload = shape.payload.empty() ? nullptr
+                                          : static_cast<const uint8_t*>(upload(14, shape.payload.data(), shape.payload.size()));
+        p.payload_len = (uint32_t)shape.payload.size();
+        p.window = shape.window;
+        p.urgent_ptr = shape.urgent_ptr;
+        p.flags = shape.flags;
+        p.options_len = (uint8_t)shape.options.size();
+        if (!shape.options.empty()) memcpy(p.options, shape.options.data(), shape.options.size());
+        p.count = n;
+        void* d_out = scratch(15, n * L);
+        const int rc = nexg_build_tcp_batch(ctx_, &p, static_cast<uint8_t*>(d_out), L, stream_);
+        if (rc == NEXG_ERANGE) return BuildError::LengthOverflow;
+        check(rc, "nexg_build_tcp_batch");
+        return download_frames(d_out, n, L);
+    }
+
+    // icmp_ping's echo request for every tuple (EchoRequest 8 / ICMPv6 128, code 0)
+    Result<std::vector<std::vector<uint8_t>>, BuildError> build_icmp_ping(const std::vector<IcmpPingTuple>& t,
+                                                                          const IcmpPingShape& shape) {
+        std::vector<std::vector<uint8_t>> frames;
+        if (t.empty()) return frames;
+        const uint8_t fam = t[0].source.family;
+        for (const auto& x : t)
+            if (x.source.family != fam || x.destination.family != fam) return BuildError::AddressFamilyMismatch;
+        const uint64_t n = t.size();
+        const uint32_t L = 14u + (fam == 4 ? 20u : 40u) + 8u + (uint32_t)shape.payload.size();
+        nexg_icmp_echo_build p{};
+        fill_ip(p.ip, t, shape.src_mac, shape.dst_mac, fam, shape.ttl, shape.ip_flags, shape.tos, shape.flow_label, 5);
+        std::vector<uint16_t> id(n), sq(n);
+        for (uint64_t i = 0; i < n; i++) {
+            id[i] = t[i].identifier;
+            sq[i] = t[i].sequence;
+        }
+        p.identifier = static_cast<const uint16_t*>(upload(10, id.data(), n * 2));
+        p.sequence = static_cast<const uint16_t*>(upload(11, sq.data(), n * 2));
+        p.payload = shape.payload.empty() ? nullptr
+                                          : static_cast<const uint8_t*>(upload(14, shape.payload.data(), shape.payload.size()));
+        p.payload_len = (uint32_t)shape.payload.size();
+        p.icmp_type = fam == 4 ? 8 : 128;
+        p.icmp_code = 0;
+        p.count = n;
+        void* d_out = scratch(15, n * L);
+        const int rc = nexg_build_icmp_echo_batch(ctx_, &p, static_cast<uint8_t*>(d_out), L, stream_);
+        if (rc == NEXG_ERANGE) return BuildError::LengthOverflow;
+        check(rc, "nexg_build_icmp_echo_batch");
+        return download_frames(d_out, n, L);
+    }
+
    private:
+    void* upload(size_t slot, const void* src, size_t n) {
+        void* d = scratch(slot, n);
+        if (n) check_hip(hipMemcpyAsync(d, src, n, hipMemcpyHostToDevice, stream_), "H2D");
+        return d;
+    }
+    std::vector<std::vector<uint8_t>> download_frames(const void* d_out, uint64_t n, uint32_t L) {
+        std::vector<uint8_t> host(n * L);
+        check_hip(hipMemcpyAsync(host.data(), d_out, host.size(), hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+        std::vector<std::vector<uint8_t>> frames;
+        frames.reserve(n);
+        for (uint64_t i = 0; i < n; i++) frames.emplace_back(host.begin() + i * L, host.begin() + (i + 1) * L);
+        return frames;
+    }
+    // per-tuple addresses / ids into nexg_ip_build (scratch slots first .. first+2)
+    template <class Tuple>
+    void fill_ip(nexg_ip_build& ip, const std::vector<Tuple>& t, const MacAddr& smac, const MacAddr& dmac,
+                 uint8_t fam, uint8_t ttl, uint8_t ip_flags, uint8_t tos, uint32_t flow_label, size_t first) {
+        const size_t w = fam == 4 ? 4 : 16;
+        std::vector<uint8_t> src(t.size() * w), dst(t.size() * w);
+        std::vector<uint16_t> id(t.size());
+        for (size_t i = 0; i < t.size(); i++) {
+            memcpy(src.data() + i * w, t[i].source.octets.data(), w);
+            memcpy(dst.data() + i * w, t[i].destination.octets.data(), w);
+            id[i] = t[i].ip_id;
+        }
+        ip.src_ip = static_cast<const uint8_t*>(upload(first, src.data(), src.size()));
+        ip.dst_ip = static_cast<const uint8_t*>(upload(first + 1, dst.data(), dst.size()));
+        ip.ip_id = fam == 4 ? static_cast<const uint16_t*>(upload(first + 2, id.data(), id.size() * 2)) : nullptr;
+        ip.family = fam;
+        ip.flow_label = flow_label;
+        memcpy(ip.def_src_mac, smac.data(), 6);
+        memcpy(ip.def_dst_mac, dmac.data(), 6);
+        ip.ttl = ttl;
+        ip.ip_flags = ip_flags;
+        ip.tos = tos;
+    }
     // grow-only device scratch, one buffer per slot: every call ends with a
     // stream sync, so the next call may reuse them (no hipMalloc per batch)
     struct Scratch {

@@ -247,6 +247,68 @@ int main(int argc, char** argv) {
         auto over = eng->build_udp_ping({t}, big);
         CHECK(over.is_err() && over.error() == BuildError::LengthOverflow);
     }
+    if (gpu) {  // tcp_ping / icmp_ping builds (builder/tcp.rs:175-228, examples/tcp_ping.rs:111-123,
+                // examples/icmp_ping.rs:67-80) against the oracle's builders, IPv4 and IPv6
+        for (int fam : {4, 6}) {
+            TcpPingTuple t;
+            if (fam == 4) {
+                t.source = IpAddr::from(Ipv4Addr{{192, 168, 1, 100}});
+                t.destination = IpAddr::from(Ipv4Addr{{192, 168, 1, 1}});
+            } else {
+                Ipv6Addr a, b;
+                a.octets[15] = 1;
+                b.octets[15] = 2;
+                t.source = IpAddr::from(a);
+                t.destination = IpAddr::from(b);
+            }
+            t.src_port = 1234;
+            t.dst_port = 80;
+            t.sequence = 1;
+            t.acknowledgement = 2;
+            TcpPingShape sh;
+            sh.window = 1024;
+            sh.options = {0x02, 0x04, 0x05, 0xb4, 0x04, 0x02, 0x01, 0x01, 0x03, 0x03, 0x07};  // mss, sack_perm, nop, nop, wscale
+            sh.payload = {'a', 'b', 'c'};
+            auto b = eng->build_tcp_ping({t, t}, sh);
+            CHECK(b.is_ok() && b.value().size() == 2);
+            nexo_ip_spec spec{};
+            spec.family = fam;
+            memcpy(spec.src, t.source.octets.data(), 16);
+            memcpy(spec.dst, t.destination.octets.data(), 16);
+            spec.ttl = 64;
+            spec.ip_flags = 2;
+            std::vector<uint8_t> want(14 + (fam == 4 ? 20 : 40) + 20 + 12 + 3);
+            nexo_build_tcp(&spec, 1234, 80, 1, 2, 0x02, 1024, 0, sh.options.data(), (uint32_t)sh.options.size(),
+                           sh.payload.data(), 3, want.data());
+            CHECK(b.value()[0] == want);
+            auto f = eng->try_from_bufs(b.value());
+            // 11 option bytes + 1 zero pad: the walk reads the pad as EOL (tcp.rs:767-818)
+            CHECK(f[0].is_ok() && f[0].value().checksums.l4_ok && f[0].value().transport->tcp->options.size() == 6);
+            CHECK(f[0].value().transport->tcp->options[5].kind == 0 && f[0].value().transport->tcp->data_offset == 8);
+            IcmpPingTuple it;
+            it.source = t.source;
+            it.destination = t.destination;
+            it.identifier = 0x1234;
+            it.sequence = 1;
+            IcmpPingShape ish;
+            ish.payload = {'h', 'e', 'l', 'l', 'o'};
+            auto e = eng->build_icmp_ping({it}, ish);
+            std::vector<uint8_t> wante(14 + (fam == 4 ? 20 : 40) + 8 + 5);
+            nexo_build_icmp_echo(&spec, fam == 4 ? 8 : 128, 0, 0x1234, 1, ish.payload.data(), 5, wante.data());
+            CHECK(e.is_ok() && e.value()[0] == wante);
+            auto fe = eng->try_from_bufs(e.value());
+            CHECK(fe[0].is_ok() && fe[0].value().checksums.l4_ok);
+        }
+        TcpPingTuple a, b6;
+        a.source = a.destination = IpAddr::from(Ipv4Addr{{10, 0, 0, 1}});
+        b6.source = b6.destination = IpAddr::from(Ipv6Addr{});
+        auto mix = eng->build_tcp_ping({a, b6}, TcpPingShape{});
+        CHECK(mix.is_err() && mix.error() == BuildError::AddressFamilyMismatch);
+        TcpPingShape big;
+        big.options.assign(50, 0x01);  // builder/tcp.rs:211-228: options past 40 B
+        auto over = eng->build_tcp_ping({a}, big);
+        CHECK(over.is_err() && over.error() == BuildError::LengthOverflow);
+    }
     // every fixture: Frame fields == the record the oracle writes (device == oracle in --gpu)
     for (const auto& n : names) {
         const Fixture& fxt = fx[n];
