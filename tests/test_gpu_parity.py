@@ -381,3 +381,33 @@ def test_logical_shards_equal_whole(engine, workload):
     assert torch.equal(torch.cat(parts), want[: total * 64])
     wb = whole.data[: whole.total_bytes] if whole.offsets is None else whole.data[: int(whole.offsets[total])]
     assert torch.equal(torch.cat(frames), wb)
+
+
+@pytest.mark.parametrize("flags,ip_offset", [(0, 0), (abi.PARSE_STRICT, 0), (abi.PARSE_FROM_IP, 14),
+                                             (abi.PARSE_FROM_IP | abi.PARSE_STRICT, 14),
+                                             (abi.PARSE_VLAN, 0)])
+def test_large_mutation_sweep(engine, oracle, flags, ip_offset):
+    """400k fuzz-style mutations of every fixture family (golden, crafted,
+    VLAN, FrameSlice edge cases, IMIX) per parse mode, in the packed
+    (SpanTile) and explicit-length (TwoPass) layouts: every record field
+    bit-exact against the oracle."""
+    import torch
+    rng = np.random.default_rng(1000 + flags)
+    base = ([bytes.fromhex(v["frame"]) for v in helpers.golden()["frames"]] + helpers.crafted_frames() +
+            helpers.vlan_frames() + helpers.slice_frames() +
+            [oracle.gen_frame(abi.WL_IMIX, i) for i in range(400)])
+    frames = helpers.mutate_frames(rng, base, 400_000)
+    want = oracle.parse_packed(*_packed_host(frames), flags=flags, ip_offset=ip_offset, nthreads=16)
+    mode = ParseMode.Strict if flags & abi.PARSE_STRICT else ParseMode.Lenient
+    opt = ParseOption(bool(flags & abi.PARSE_FROM_IP), ip_offset, bool(flags & abi.PARSE_VLAN))
+    for batch in (FrameBatch.from_packed(frames), FrameBatch.from_frames(frames, pad_to=2)):
+        got = engine.parse_to_numpy(batch, opt, mode, abi.OUT_RECORD)
+        helpers.records_equal(got, want, frames, f"mutation sweep flags={flags}")
+    torch.cuda.synchronize()
+
+
+def _packed_host(frames):
+    offs = np.zeros(len(frames) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(f) for f in frames])
+    data = np.frombuffer(b"".join(frames) + bytes(16), np.uint8)
+    return data, offs, None
