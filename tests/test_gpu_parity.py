@@ -411,3 +411,27 @@ def _packed_host(frames):
     offs[1:] = np.cumsum([len(f) for f in frames])
     data = np.frombuffer(b"".join(frames) + bytes(16), np.uint8)
     return data, offs, None
+
+
+@pytest.mark.parametrize("flags,ip_offset", [(0, 0), (abi.PARSE_FROM_IP, 14)])
+def test_large_mutation_sweep_slices_and_options(engine, oracle, flags, ip_offset):
+    """The same 400k-mutation corpus through FrameSlice (NEXG_OUT_SLICE) and
+    the device option lists (nexg_decode_options), against the oracle."""
+    import torch
+    rng = np.random.default_rng(2000 + flags)
+    base = ([bytes.fromhex(v["frame"]) for v in helpers.golden()["frames"]] + helpers.crafted_frames() +
+            helpers.slice_frames() + [oracle.gen_frame(abi.WL_IMIX, i) for i in range(400)])
+    frames = helpers.mutate_frames(rng, base, 400_000)
+    data, offs, _ = _packed_host(frames)
+    want_s = oracle.slice_packed(data, offs, flags=flags, ip_offset=ip_offset)
+    opt = ParseOption(bool(flags & abi.PARSE_FROM_IP), ip_offset)
+    batch = FrameBatch.from_packed(frames)
+    got_s = engine.parse_to_numpy(batch, opt, ParseMode.Lenient, abi.OUT_SLICE)
+    helpers.records_equal(got_s, want_s, frames, f"slice sweep flags={flags}")
+    recs = engine.parse(batch, opt, ParseMode.Lenient, abi.OUT_RECORD)
+    got_o = engine.decode_options(batch, recs)
+    torch.cuda.synchronize()
+    got_o = got_o.cpu().numpy()[: len(frames) * 96].view(abi.OPTIONS_DTYPE)
+    sel = rng.choice(len(frames), 40_000, replace=False)  # the oracle's option walk is per frame
+    want_o = np.array([oracle.decode_options(frames[i], flags, ip_offset) for i in sel], abi.OPTIONS_DTYPE)
+    helpers.records_equal(got_o[sel], want_o, [frames[i] for i in sel], f"options sweep flags={flags}")
