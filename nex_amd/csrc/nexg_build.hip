@@ -69,11 +69,14 @@ __device__ __forceinline__ void lds_put_halfwords(uint8_t* smem, uint32_t d0, co
 __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }
 
 // tile copy-out shared by the builders: nf frames of `stride` bytes staged
-// contiguously in LDS leave as 16-B stores (+ byte tail of a partial tile)
+// contiguously in LDS leave as 16-B non-temporal stores (+ byte tail of a
+// partial tile). Non-temporal: the udp_ping build of 16M frames takes 0.132
+// instead of 0.165 ms with identical HBM traffic (PMC).
 __device__ __forceinline__ void build_copy_out(const uint8_t* smem, uint8_t* T, uint32_t bytes) {
     const uint32_t tid = threadIdx.x;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     for (uint32_t c = tid; c < bytes / 16u; c += kBuildTile)
-        reinterpret_cast<uint4*>(T)[c] = reinterpret_cast<const uint4*>(smem)[c];
+        __builtin_nontemporal_store(reinterpret_cast<const v4u*>(smem)[c], reinterpret_cast<v4u*>(T) + c);
     const uint32_t tail = bytes & ~15u;
     if (tid < bytes - tail) T[tail + tid] = smem[tail + tid];
 }

@@ -75,6 +75,42 @@ __global__ __launch_bounds__(256) void k_wv(const uint8_t* data, uint64_t n16, u
     }
 }
 
+// 64 B read + 64 B written per frame (the record output's shape), store policy
+template <bool NTS>
+__global__ __launch_bounds__(256) void k_rec(const uint8_t* data, uint64_t n16, uint8_t* out) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const uint64_t base = (uint64_t)blockIdx.x * 1024;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t c = base + threadIdx.x + 256 * k;
+        uint4 v = load16<true>(data + 16 * c);
+        v.x ^= 0x9e3779b9u;
+        v4u w = {v.x, v.y, v.z, v.w};
+        if (NTS) __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(out) + c);
+        else reinterpret_cast<v4u*>(out)[c] = w;
+    }
+}
+
+// 8 B per frame as 16-B non-temporal stores by half the lanes (through LDS)
+__global__ __launch_bounds__(256) void k_wv16nt(const uint8_t* data, uint64_t n16, uint8_t* out) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint2 s_d[256];
+    const uint64_t base = (uint64_t)blockIdx.x * 1024;
+    uint32_t x = 0;
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = load16<true>(data + 16 * (base + threadIdx.x + 256 * k));
+#pragma unroll
+    for (int k = 0; k < 4; k++) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    s_d[threadIdx.x] = make_uint2(x, (uint32_t)(blockIdx.x * 256 + threadIdx.x));
+    __syncthreads();
+    if (threadIdx.x < 128) {
+        const uint4 d = reinterpret_cast<const uint4*>(s_d)[threadIdx.x];
+        v4u w = {d.x, d.y, d.z, d.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(out) + (uint64_t)blockIdx.x * 128 + threadIdx.x);
+    }
+}
+
 // 8 B per 64-B frame written as 16-B stores by half the lanes (through LDS)
 __global__ __launch_bounds__(256) void k_wv16(const uint8_t* data, uint64_t n16, uint8_t* out) {
     __shared__ __attribute__((aligned(16))) uint2 s_d[256];
@@ -276,6 +312,8 @@ int main(int argc, char** argv) {
     uint2* out;
     CK(hipMalloc(&data, bytes));
     CK(hipMalloc(&out, count * 8));
+    uint8_t* rec;
+    CK(hipMalloc(&rec, count * 64));
     CK(hipMemset(data, 1, bytes));
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -320,6 +358,9 @@ int main(int argc, char** argv) {
             const uint64_t m = (1ull << lg) - 1;
             vs.push_back({"w8_win" + std::to_string(8ull << lg >> 20) + "MiB", [=]() { hipLaunchKernelGGL(k_wwin, g, dim3(256), 0, 0, data, n16, out, m); }});
         }
+        vs.push_back({"w8_via16_nt", [=]() { hipLaunchKernelGGL(k_wv16nt, g, dim3(256), 0, 0, data, n16, o8); }});
+        vs.push_back({"rec64_plain", [=]() { hipLaunchKernelGGL(k_rec<false>, g, dim3(256), 0, 0, data, n16, reinterpret_cast<uint8_t*>(rec)); }});
+        vs.push_back({"rec64_nt", [=]() { hipLaunchKernelGGL(k_rec<true>, g, dim3(256), 0, 0, data, n16, reinterpret_cast<uint8_t*>(rec)); }});
         vs.push_back({"w8_via16", [=]() { hipLaunchKernelGGL(k_wv16, g, dim3(256), 0, 0, data, n16, o8); }});
         vs.push_back({"w8_nt", [=]() { hipLaunchKernelGGL((k_wv<8, 1>), g, dim3(256), 0, 0, data, n16, o8); }});
         vs.push_back({"w8_sc01nt", [=]() { hipLaunchKernelGGL((k_wv<8, 2>), g, dim3(256), 0, 0, data, n16, o8); }});
