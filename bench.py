@@ -123,13 +123,14 @@ def stream_ceilings(eng, batch, args, stream, device):
                       args.steps, args.warmup, stream, device)
         r[key] = round(nbytes / ks / 1e9, 1)
     r["source"] = "nexg_probe_stream on this batch, same steps/warmup, HIP events on the launch stream"
-    if args.out == "desc":  # the same parse with the 4-B flags output (NEXG_OUT_FLAGS)
+    if args.out == "desc":  # the same parse with the 4-B flags / 2-B verdict outputs
         from nex_amd import abi
-        _, ks = timed(lambda: eng.parse(batch, out_kind=abi.OUT_FLAGS, out=out, stream=stream),
-                      args.steps, args.warmup, stream, device)
-        ach = batch.total_bytes / ks / 1e9
-        r["flags_output"] = {"kernel_ms": round(ks * 1e3, 4), "achieved": round(ach, 1),
-                             "frac": round(ach / HBM_PEAK_GBS, 4)}
+        for key, kind in (("flags_output", abi.OUT_FLAGS), ("verdict_output", abi.OUT_VERDICT)):
+            _, ks = timed(lambda: eng.parse(batch, out_kind=kind, out=out, stream=stream),
+                          args.steps, args.warmup, stream, device)
+            ach = batch.total_bytes / ks / 1e9
+            r[key] = {"kernel_ms": round(ks * 1e3, 4), "achieved": round(ach, 1),
+                      "frac": round(ach / HBM_PEAK_GBS, 4)}
     return r
 
 
@@ -176,7 +177,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["udp64", "imix", "ser"], default="udp64")
     ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
-    ap.add_argument("--out", choices=["desc", "record", "flags"], default="desc")
+    ap.add_argument("--out", choices=["desc", "record", "flags", "verdict"], default="desc")
     ap.add_argument("--no-imix", action="store_true",
                     help="skip the configs[2] IMIX line reported beside the default UDP64 run")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -201,8 +202,8 @@ def main():
     F = args.frames
     first = rank * F
     stream = torch.cuda.current_stream(device)
-    out_kind = {"desc": abi.OUT_DESC, "record": abi.OUT_RECORD, "flags": abi.OUT_FLAGS}[args.out]
-    width = {"desc": 8, "record": 64, "flags": 4}[args.out]
+    out_kind = {"desc": abi.OUT_DESC, "record": abi.OUT_RECORD, "flags": abi.OUT_FLAGS, "verdict": abi.OUT_VERDICT}[args.out]
+    width = {"desc": 8, "record": 64, "flags": 4, "verdict": 2}[args.out]
 
     if args.workload in ("udp64", "imix"):
         wl = abi.WL_UDP64 if args.workload == "udp64" else abi.WL_IMIX

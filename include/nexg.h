@@ -168,6 +168,19 @@ typedef struct nexg_record {
  * 8-B descriptor stream costs ~18 % of the read rate at 64-B frames; 4 B
  * halves that. */
 #define NEXG_OUT_FLAGS 4
+/* Verdict per frame (out_kind NEXG_OUT_VERDICT), 2 bytes, lossless for the
+ * flags word: a parsed frame stores flags & 0xFFFF (layer and checksum bits;
+ * bits 16..23 are never set), a frame with a nonzero status (no layers) stores
+ * NEXG_VERDICT_ERR | status << 3. NEXG_L_ARP together with NEXG_L_IP marks it:
+ * a Frame never holds both datalink.arp and ip (frame.rs:596-607). Output
+ * alignment 2 B. Explicit-length batches (TwoPass layout) run the lane-window
+ * kernel for this output. */
+#define NEXG_OUT_VERDICT 5
+#define NEXG_VERDICT_ERR (NEXG_L_ARP | NEXG_L_IP)
+#define NEXG_VERDICT_FLAGS(v)                                                        \
+    ((((v) & NEXG_VERDICT_ERR) == NEXG_VERDICT_ERR) ? ((((uint32_t)(v) >> 3) & 0x7u) \
+                                                       << NEXG_STATUS_SHIFT)         \
+                                                    : (uint32_t)(v))
 
 /* FrameSlice::try_from_buf (frame.rs:84-287) per frame, out_kind
  * NEXG_OUT_SLICE, 16 bytes: layer boundaries only, no checksums. FrameSlice

@@ -41,11 +41,13 @@ C_L4_CHECKED = 1 << 13
 C_L4_OK = 1 << 14
 L_VLAN = 1 << 15
 STATUS_SHIFT = 24
+VERDICT_ERR = L_ARP | L_IP  # NEXG_VERDICT_ERR: never both in a parsed Frame
 
 OUT_DESC = 1
 OUT_RECORD = 2
 OUT_SLICE = 3
 OUT_FLAGS = 4  # nexg_desc.flags only (include/nexg.h)
+OUT_VERDICT = 5  # lossless 2-B form of the flags word (include/nexg.h)
 
 # FrameSlice presence bits (nexg_slice.flags)
 S_DATALINK = 1 << 0
@@ -73,6 +75,14 @@ SLICE_DTYPE = np.dtype([("flags", "<u4"), ("l3_off", "<u2"), ("l3_len", "<u2"), 
                         ("payload_off", "<u2"), ("payload_len", "<u2"), ("ethertype", "<u2")])
 assert SLICE_DTYPE.itemsize == 16
 FLAGS_DTYPE = np.dtype([("flags", "<u4")])
+VERDICT_DTYPE = np.dtype([("verdict", "<u2")])
+
+
+def verdict_to_flags(v):
+    """NEXG_VERDICT_FLAGS (include/nexg.h): the flags words of 2-B verdicts."""
+    v = np.asarray(v).astype(np.uint32)
+    err = (v & VERDICT_ERR) == VERDICT_ERR
+    return np.where(err, ((v >> 3) & 7) << STATUS_SHIFT, v).astype(np.uint32)
 OPTIONS_DTYPE = np.dtype([("n_ip", "u1"), ("n_tcp", "u1"), ("ip_opt_off", "<u2"), ("tcp_opt_off", "<u2"),
                           ("reserved", "<u2"), ("ip_pos", "u1", 40), ("tcp_pos", "u1", 40), ("pad", "u1", 8)])
 assert OPTIONS_DTYPE.itemsize == 96

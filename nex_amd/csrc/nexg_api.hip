@@ -99,10 +99,12 @@ int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_
     if (!ctx) return NEXG_EINVAL;
     if (!frames_valid(frames)) return fail(ctx, NEXG_EINVAL, "invalid frame batch%s", nullptr);
     if (out_kind != NEXG_OUT_DESC && out_kind != NEXG_OUT_RECORD && out_kind != NEXG_OUT_SLICE &&
-        out_kind != NEXG_OUT_FLAGS)
+        out_kind != NEXG_OUT_FLAGS && out_kind != NEXG_OUT_VERDICT)
         return fail(ctx, NEXG_EINVAL, "invalid out_kind%s", nullptr);
     if (frames->count && !out) return fail(ctx, NEXG_EINVAL, "NULL output%s", nullptr);
-    if ((reinterpret_cast<uint64_t>(out) & (out_kind == NEXG_OUT_FLAGS ? 3u : out_kind == NEXG_OUT_DESC ? 7u : 15u)) != 0)
+    const uint64_t align_mask = out_kind == NEXG_OUT_VERDICT ? 1u : out_kind == NEXG_OUT_FLAGS ? 3u
+                                : out_kind == NEXG_OUT_DESC  ? 7u : 15u;
+    if ((reinterpret_cast<uint64_t>(out) & align_mask) != 0)
         return fail(ctx, NEXG_EINVAL, "misaligned output%s", nullptr);
     nexg::ParseArgs a = to_args(frames);
     a.opt_flags = option ? option->flags : 0u;

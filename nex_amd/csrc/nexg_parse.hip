@@ -89,6 +89,9 @@ hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStr
     if (a.count == 0) return hipSuccess;
     if (out_kind == NEXG_OUT_SLICE) return launch_slice(v, a, s);
     if (out_kind == NEXG_OUT_FLAGS) return launch_parse_out<NEXG_OUT_FLAGS>(v, a, s);
+    if (out_kind == NEXG_OUT_VERDICT)  // no 4-B hand-off slot for the TwoPass tail sums
+        return launch_parse_out<NEXG_OUT_VERDICT>(v == ParseVariant::TwoPass ? ParseVariant::LaneWindow : v,
+                                                  a, s);
     return out_kind == NEXG_OUT_DESC ? launch_parse_out<NEXG_OUT_DESC>(v, a, s)
                                      : launch_parse_out<NEXG_OUT_RECORD>(v, a, s);
 }

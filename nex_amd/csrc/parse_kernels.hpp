@@ -37,6 +37,10 @@ template <int OUT>
 __device__ __forceinline__ void store_result(void* out, uint64_t idx, const nexg_record& r) {
     if (OUT == NEXG_OUT_FLAGS) {  // non-temporal: +2.6 % on the 4-B stream (streambench w4_nt)
         __builtin_nontemporal_store(r.flags, reinterpret_cast<uint32_t*>(out) + idx);
+    } else if (OUT == NEXG_OUT_VERDICT) {  // include/nexg.h: lossless 2-B form of the flags
+        const uint32_t st = (r.flags >> NEXG_STATUS_SHIFT) & 7u;
+        const uint16_t v = (uint16_t)(st ? (NEXG_VERDICT_ERR | (st << 3)) : (r.flags & 0xFFFFu));
+        __builtin_nontemporal_store(v, reinterpret_cast<uint16_t*>(out) + idx);
     } else if (OUT == NEXG_OUT_DESC) {
         uint2 d = make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
         reinterpret_cast<uint2*>(out)[idx] = d;

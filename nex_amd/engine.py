@@ -162,9 +162,11 @@ class Engine:
 
         Returns a uint8 device tensor holding nexg_desc[count] (8 B each),
         nexg_record[count] (64 B), nexg_slice[count] (16 B) or, with
-        out_kind=OUT_FLAGS, the nexg_desc.flags word alone (4 B)."""
+        out_kind=OUT_FLAGS, the nexg_desc.flags word alone (4 B), or with
+        OUT_VERDICT its lossless 2-B form (abi.verdict_to_flags)."""
         torch = _torch()
-        width = {abi.OUT_DESC: 8, abi.OUT_RECORD: 64, abi.OUT_SLICE: 16, abi.OUT_FLAGS: 4}[out_kind]
+        width = {abi.OUT_DESC: 8, abi.OUT_RECORD: 64, abi.OUT_SLICE: 16, abi.OUT_FLAGS: 4,
+                 abi.OUT_VERDICT: 2}[out_kind]
         if out is None:
             out = torch.empty(max(batch.count, 1) * width, dtype=torch.uint8, device=self.torch_device)
         fr = batch.to_c()
@@ -178,7 +180,8 @@ class Engine:
         out = self.parse(batch, option, mode, out_kind)
         _torch().cuda.synchronize(self.torch_device)
         dt = {abi.OUT_DESC: abi.DESC_DTYPE, abi.OUT_RECORD: abi.RECORD_DTYPE,
-              abi.OUT_SLICE: abi.SLICE_DTYPE, abi.OUT_FLAGS: abi.FLAGS_DTYPE}[out_kind]
+              abi.OUT_SLICE: abi.SLICE_DTYPE, abi.OUT_FLAGS: abi.FLAGS_DTYPE,
+              abi.OUT_VERDICT: abi.VERDICT_DTYPE}[out_kind]
         return out.cpu().numpy()[: batch.count * dt.itemsize].view(dt)
 
     def decode_options(self, batch: FrameBatch, records, stream=None):

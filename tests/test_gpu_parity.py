@@ -320,6 +320,36 @@ def test_flags_output_matches_oracle(engine, oracle, corpus):
     assert (f4.cpu().numpy().view("<u4") == d8.cpu().numpy().view(abi.DESC_DTYPE)["flags"]).all()
 
 
+def test_verdict_output_matches_oracle(engine, oracle, corpus):
+    """NEXG_OUT_VERDICT (2 B) decodes to the oracle's flags word exactly, in
+    every layout (packed, explicit lengths -> lane window, strides 64 / 128)
+    and in strict / from-IP modes, where error statuses are common."""
+    import torch
+    for mode, opt in ((ParseMode.Lenient, ParseOption()), (ParseMode.Strict, ParseOption()),
+                      (ParseMode.Lenient, ParseOption(True, 14))):
+        want = oracle.parse_frames(corpus, opt.flags(mode), opt.offset)["flags"].astype(np.uint32)
+        for batch in (FrameBatch.from_packed(corpus, shift=4), FrameBatch.from_frames(corpus, pad_to=4)):
+            got = engine.parse_to_numpy(batch, opt, mode, out_kind=abi.OUT_VERDICT)
+            assert got.dtype == abi.VERDICT_DTYPE and len(got) == len(corpus)
+            bad = np.nonzero(abi.verdict_to_flags(got["verdict"]) != want)[0]
+            assert len(bad) == 0, (mode, opt, batch.count, bad[:8])
+        assert (want >> abi.STATUS_SHIFT).any()
+    for stride in (64, 128):
+        sel = [f for f in corpus if len(f) <= stride][:20000]
+        arr = np.zeros((len(sel), stride), np.uint8)
+        for i, f in enumerate(sel):
+            arr[i, :len(f)] = np.frombuffer(f, np.uint8)
+        full = [bytes(arr[i]) for i in range(len(sel))]
+        got = engine.parse_to_numpy(FrameBatch.from_strided(arr), out_kind=abi.OUT_VERDICT)
+        assert (abi.verdict_to_flags(got["verdict"]) == oracle.parse_frames(full)["flags"]).all(), stride
+    b = engine.gen_batch(abi.WL_UDP64, 1 << 20)
+    v2 = engine.parse(b, out_kind=abi.OUT_VERDICT)
+    d8 = engine.parse(b, out_kind=abi.OUT_DESC)
+    torch.cuda.synchronize()
+    assert (abi.verdict_to_flags(v2.cpu().numpy().view("<u2")) ==
+            d8.cpu().numpy().view(abi.DESC_DTYPE)["flags"]).all()
+
+
 def test_build_udp4_default_fields(engine, oracle):
     """The general builder form (ports / id from the batch defaults) next to
     the all-arrays form the udp_ping bench takes: same bytes as the oracle."""
