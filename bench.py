@@ -22,6 +22,14 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+#: --out name -> nexg out_kind (include/nexg.h NEXG_OUT_*)
+OUT_KINDS = {"desc": 1, "record": 2, "flags": 4, "verdict": 5, "sparse": 6}
+OUT_NOTE = {
+    "sparse": "lossless sparse descriptors (NEXG_OUT_SPARSE: 1-B shape code per frame + 8-B "
+              "exceptions; expands to nexg_desc bit-exactly)",
+    "desc": "8-B nexg_desc per frame", "record": "64-B nexg_record per frame",
+    "flags": "4-B flags word per frame (no payload location)",
+    "verdict": "2-B lossless flags per frame (no payload location)"}
 METRIC = "Mpkt/s + GiB/s device-resident parse+cksum, 64B & IMIX, 1/2/4/8 MI355X"
 
 
@@ -115,7 +123,7 @@ def stream_ceilings(eng, batch, args, stream, device):
     (nexg_probe_stream, the parse kernels' load shape): read only, and
     64 B read / 8 B written (the descriptor stream's shape)."""
     import torch
-    out = torch.empty(batch.data.numel() // 8, dtype=torch.uint8, device=device)
+    out = torch.empty(max(batch.data.numel() // 8, batch.count * 8 + 16), dtype=torch.uint8, device=device)
     nbytes = batch.data.numel() // 16384 * 16384
     r = {}
     for key, w8 in (("read_only_gbs", False), ("read64_write8_gbs", True)):
@@ -123,9 +131,12 @@ def stream_ceilings(eng, batch, args, stream, device):
                       args.steps, args.warmup, stream, device)
         r[key] = round(nbytes / ks / 1e9, 1)
     r["source"] = "nexg_probe_stream on this batch, same steps/warmup, HIP events on the launch stream"
-    if args.out == "desc":  # the same parse with the 4-B flags / 2-B verdict outputs
+    if args.out in ("sparse", "desc"):  # the same parse with the other output kinds
         from nex_amd import abi
-        for key, kind in (("flags_output", abi.OUT_FLAGS), ("verdict_output", abi.OUT_VERDICT)):
+        for key, kind in (("desc_output", abi.OUT_DESC), ("flags_output", abi.OUT_FLAGS),
+                          ("verdict_output", abi.OUT_VERDICT), ("sparse_output", abi.OUT_SPARSE)):
+            if OUT_KINDS[args.out] == kind:
+                continue
             _, ks = timed(lambda: eng.parse(batch, out_kind=kind, out=out, stream=stream),
                           args.steps, args.warmup, stream, device)
             ach = batch.total_bytes / ks / 1e9
@@ -140,8 +151,9 @@ def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
     discipline. Returns the object rank 0 adds to the JSON line."""
     import torch
     from nex_amd import abi, dist
+    from nex_amd.engine import Engine
     batch = eng.gen_batch(abi.WL_IMIX, F, first_index=first)
-    out = torch.empty(F * width, dtype=torch.uint8, device=device)
+    out = torch.empty(Engine.out_bytes(out_kind, F), dtype=torch.uint8, device=device)
     torch.cuda.synchronize(device)
     alg = batch.total_bytes
     # a freshly generated 6-GB batch runs its first ~20 launches 5-25 % slow
@@ -155,7 +167,7 @@ def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
         return None
     ach = alg / kernel_s / 1e9
     r = {"workload": f"configs[2]: {F} IMIX frames per GPU (64/576/1500 at 7:4:1, "
-                     "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table",
+                     "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table; " + OUT_NOTE[args.out],
          "value": round(frames / elapsed / 1e6, 2), "unit": "Mpkt/s", "steps": steps,
          "ms_per_step": round(elapsed / steps * 1e3, 4),
          "gib_s": round(nbytes / elapsed / 2**30, 2), "bytes_per_gpu": alg,
@@ -177,7 +189,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["udp64", "imix", "ser"], default="udp64")
     ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
-    ap.add_argument("--out", choices=["desc", "record", "flags", "verdict"], default="desc")
+    ap.add_argument("--out", choices=list(OUT_KINDS), default="sparse",
+                    help="output kind (default: lossless sparse descriptors, NEXG_OUT_SPARSE)")
     ap.add_argument("--no-imix", action="store_true",
                     help="skip the configs[2] IMIX line reported beside the default UDP64 run")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -202,26 +215,26 @@ def main():
     F = args.frames
     first = rank * F
     stream = torch.cuda.current_stream(device)
-    out_kind = {"desc": abi.OUT_DESC, "record": abi.OUT_RECORD, "flags": abi.OUT_FLAGS, "verdict": abi.OUT_VERDICT}[args.out]
-    width = {"desc": 8, "record": 64, "flags": 4, "verdict": 2}[args.out]
+    out_kind = OUT_KINDS[args.out]
+    width = {"desc": 8, "record": 64, "flags": 4, "verdict": 2, "sparse": 1}[args.out]
 
     if args.workload in ("udp64", "imix"):
         wl = abi.WL_UDP64 if args.workload == "udp64" else abi.WL_IMIX
         batch = eng.gen_batch(wl, F, first_index=first)
         torch.cuda.synchronize(device)
         alg_bytes = batch.total_bytes  # Σ frame_len: every byte is read (L4 checksum)
-        out = torch.empty(F * width, dtype=torch.uint8, device=device)
+        out = torch.empty(Engine.out_bytes(out_kind, F), dtype=torch.uint8, device=device)
 
         def step():
             eng.parse(batch, out_kind=out_kind, out=out, stream=stream)
         if args.workload == "udp64":
             cfg = {"workload": "configs[1]: 16M x 64-B Eth/IPv4/UDP frames per GPU, fixed 64-B "
                                "stride, device-resident; Frame parse (L2/L3/L4) + IPv4 header and "
-                               f"UDP checksum verify -> {width}-B {args.out} per frame" if F == 16 << 20
-                               else f"{F} x 64-B Eth/IPv4/UDP frames per GPU"}
+                               "UDP checksum verify -> " + OUT_NOTE[args.out] if F == 16 << 20
+                               else f"{F} x 64-B Eth/IPv4/UDP frames per GPU; " + OUT_NOTE[args.out]}
         else:
             cfg = {"workload": f"configs[2]: {F} IMIX frames per GPU (64/576/1500 at 7:4:1, "
-                               "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table"}
+                               "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table; " + OUT_NOTE[args.out]}
     else:
         p = eng.gen_udp4_params(F, first_index=first)
         out = torch.empty(F * 42, dtype=torch.uint8, device=device)
@@ -244,12 +257,11 @@ def main():
         # copy stream: H2D chunk i; compute stream: parse chunk i; D2H descs
         host = torch.empty(batch.data.numel(), dtype=torch.uint8, pin_memory=True)
         host.copy_(batch.data)
-        host_out = torch.empty(out.numel(), dtype=torch.uint8, pin_memory=True)
         cs, ps = torch.cuda.Stream(device), torch.cuda.Stream(device)
         C = args.e2e_chunk
         from nex_amd.engine import FrameBatch
         offs_host = None if batch.offsets is None else batch.offsets.cpu()
-        chunks = []
+        chunks, o0 = [], 0
         for c0 in range(0, F, C):
             c1 = min(F, c0 + C)
             if batch.offsets is None:
@@ -259,19 +271,23 @@ def main():
                 b0, b1 = int(offs_host[c0]), int(offs_host[c1])
                 sub = FrameBatch(data=batch.data[b0:b1], count=c1 - c0,
                                  offsets=batch.offsets[c0:c1 + 1] - b0)
-            chunks.append((c0, c1, b0, b1, sub))
+            # each chunk's whole output (sparse: codes + exception slots) goes back
+            ob = (Engine.out_bytes(out_kind, c1 - c0) + 255) // 256 * 256
+            chunks.append((b0, b1, o0, o0 + ob, sub))
+            o0 += ob
+        out = torch.empty(o0, dtype=torch.uint8, device=device)
+        host_out = torch.empty(o0, dtype=torch.uint8, pin_memory=True)
 
         def step():
-            ev_prev = None
-            for (c0, c1, b0, b1, sub) in chunks:
+            for (b0, b1, p0, p1, sub) in chunks:
                 with torch.cuda.stream(cs):
                     batch.data[b0:b1].copy_(host[b0:b1], non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record(cs)
                 ps.wait_event(ev)
-                eng.parse(sub, out_kind=out_kind, out=out[c0 * width:c1 * width], stream=ps)
+                eng.parse(sub, out_kind=out_kind, out=out[p0:p1], stream=ps)
                 with torch.cuda.stream(ps):
-                    host_out[c0 * width:c1 * width].copy_(out[c0 * width:c1 * width], non_blocking=True)
+                    host_out[p0:p1].copy_(out[p0:p1], non_blocking=True)
             ps.synchronize()
         cfg["workload"] += "; END-TO-END: frames in pinned host memory, chunked H2D/parse/D2H"
         cfg["e2e_chunk_frames"] = C

@@ -182,6 +182,87 @@ typedef struct nexg_record {
                                                        << NEXG_STATUS_SHIFT)         \
                                                     : (uint32_t)(v))
 
+/* Sparse descriptors (out_kind NEXG_OUT_SPARSE): lossless for nexg_desc at
+ * 1 B per frame whenever the frame has one of the canonical shapes below
+ * (every frame of the synthetic 64-B and IMIX workloads does), plus the full
+ * 8-B descriptor for every other frame. `out` (16-B aligned) holds
+ *   codes : uint8_t[count]                 at out
+ *   exc   : nexg_desc[count] (capacity)    at out + NEXG_SPARSE_EXC_OFFSET(count)
+ * The k-th exception (code 0) of the 64-frame group g = i / 64, counted in
+ * frame order, is stored at exc[64 * g + k]; nothing else of exc is written.
+ * Code byte: bits 0..3 shape, bit 4 NEXG_C_IP_OK, bit 5 NEXG_C_L4_OK, bits
+ * 6..7 number of VLAN tags unwrapped (NEXG_PARSE_VLAN). With L = l3 offset
+ * = (FROM_IP ? ip_offset : 14) + 4 * tags, h = L + NEXG_SHAPE_HDR(shape):
+ *   flags       = NEXG_SHAPE_FLAGS(shape) | ok bits | (tags ? NEXG_L_VLAN : 0)
+ *   payload_len = len - h, payload_off = payload_len ? h : 0
+ * for shapes 1..9; shape 10 (IP layer present but all None, Q4/Q12) has an
+ * empty payload; shapes 11..15 are error statuses 1..4, 7 (no layers, empty
+ * payload). The device encoder stores a code only when this decodes to the
+ * frame's exact descriptor, so the output is lossless by construction;
+ * nexg_sparse_expand (below) or nexg_sparse_decode restores nexg_desc. */
+#define NEXG_OUT_SPARSE 6
+#define NEXG_SPARSE_EXC_OFFSET(count) ((((uint64_t)(count)) + 15u) & ~(uint64_t)15u)
+#define NEXG_SPARSE_BYTES(count) (NEXG_SPARSE_EXC_OFFSET(count) + 8u * (uint64_t)(count))
+#define NEXG_SPARSE_IP_OK 0x10u
+#define NEXG_SPARSE_L4_OK 0x20u
+#define NEXG_SPARSE_TAG_SHIFT 6
+enum {
+    NEXG_SHAPE_EXCEPTION = 0,
+    NEXG_SHAPE_V4_UDP = 1,   /* IPv4 IHL 5 + UDP, datagram to the frame end   */
+    NEXG_SHAPE_V4_TCP = 2,   /* IPv4 IHL 5 + TCP data offset 5                */
+    NEXG_SHAPE_V4_ICMP = 3,  /* IPv4 IHL 5 + ICMP                             */
+    NEXG_SHAPE_V6_UDP = 4,   /* IPv6 without extensions + UDP                 */
+    NEXG_SHAPE_V6_TCP = 5,   /* IPv6 + TCP data offset 5                      */
+    NEXG_SHAPE_V6_ICMP = 6,  /* IPv6 + ICMPv6                                 */
+    NEXG_SHAPE_ETH_ONLY = 7, /* EtherType not IPv4/IPv6/ARP (Q3)              */
+    NEXG_SHAPE_V4_OTHER = 8, /* IPv4 IHL 5, no L4 layer (Q9, Q15)             */
+    NEXG_SHAPE_V6_OTHER = 9, /* IPv6 without extensions, no L4 layer          */
+    NEXG_SHAPE_IP_NONE = 10, /* ip = Some(all None), payload empty (Q4, Q12)  */
+    NEXG_SHAPE_ERR_FIRST = 11 /* 11..14 = status 1..4, 15 = NEXG_ERR_BAD_EXTENT */
+};
+#define NEXG_SHAPE_V4_ (NEXG_L_ETHERNET | NEXG_L_IP | NEXG_L_IPV4 | NEXG_C_IP_CHECKED)
+#define NEXG_SHAPE_V6_ (NEXG_L_ETHERNET | NEXG_L_IP | NEXG_L_IPV6)
+#define NEXG_SHAPE_FLAGS(s)                                                                     \
+    ((s) == 1 ? NEXG_SHAPE_V4_ | NEXG_L_TRANSPORT | NEXG_L_UDP | NEXG_C_L4_CHECKED            \
+   : (s) == 2 ? NEXG_SHAPE_V4_ | NEXG_L_TRANSPORT | NEXG_L_TCP | NEXG_C_L4_CHECKED            \
+   : (s) == 3 ? NEXG_SHAPE_V4_ | NEXG_L_ICMP | NEXG_C_L4_CHECKED                              \
+   : (s) == 4 ? NEXG_SHAPE_V6_ | NEXG_L_TRANSPORT | NEXG_L_UDP | NEXG_C_L4_CHECKED            \
+   : (s) == 5 ? NEXG_SHAPE_V6_ | NEXG_L_TRANSPORT | NEXG_L_TCP | NEXG_C_L4_CHECKED            \
+   : (s) == 6 ? NEXG_SHAPE_V6_ | NEXG_L_ICMPV6 | NEXG_C_L4_CHECKED                            \
+   : (s) == 7 ? NEXG_L_ETHERNET                                                               \
+   : (s) == 8 ? NEXG_SHAPE_V4_                                                                \
+   : (s) == 9 ? NEXG_SHAPE_V6_                                                                \
+   : (s) == 10 ? NEXG_L_ETHERNET | NEXG_L_IP                                                  \
+   : (s) >= 11 && (s) <= 14 ? (uint32_t)((s) - 10) << NEXG_STATUS_SHIFT                       \
+   : (s) == 15 ? (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT : 0u)
+/* bytes from the l3 offset to the payload: IP header + L4 header */
+#define NEXG_SHAPE_HDR(s)                                                                       \
+    ((s) == 1 ? 28u : (s) == 2 ? 40u : (s) == 3 ? 24u : (s) == 4 ? 48u : (s) == 5 ? 60u       \
+   : (s) == 6 ? 44u : (s) == 8 ? 20u : (s) == 9 ? 40u : 0u)
+
+/* nexg_desc of a frame from its sparse code (host side; the device encoder
+ * uses the same table). len = the frame's length, flags/ip_offset = the
+ * batch's parse option. Returns 0 for an exception code (look the descriptor
+ * up in exc), 1 otherwise. */
+static inline int nexg_sparse_decode(uint8_t code, uint32_t len, uint32_t parse_flags,
+                                     uint32_t ip_offset, nexg_desc* d) {
+    const uint32_t shape = code & 0xFu, tags = (uint32_t)code >> NEXG_SPARSE_TAG_SHIFT;
+    if (shape == NEXG_SHAPE_EXCEPTION) return 0;
+    d->flags = NEXG_SHAPE_FLAGS(shape);
+    d->payload_off = 0;
+    d->payload_len = 0;
+    if (shape >= NEXG_SHAPE_IP_NONE) {
+        if (shape == NEXG_SHAPE_IP_NONE && tags) d->flags |= NEXG_L_VLAN;
+        return 1;
+    }
+    d->flags |= ((code & NEXG_SPARSE_IP_OK) ? NEXG_C_IP_OK : 0u) | ((code & NEXG_SPARSE_L4_OK) ? NEXG_C_L4_OK : 0u) |
+                (tags ? NEXG_L_VLAN : 0u);
+    const uint32_t h = ((parse_flags & NEXG_PARSE_FROM_IP) ? ip_offset : 14u) + 4u * tags + NEXG_SHAPE_HDR(shape);
+    d->payload_len = (uint16_t)(len - h);
+    d->payload_off = (uint16_t)(len > h ? h : 0u);
+    return 1;
+}
+
 /* FrameSlice::try_from_buf (frame.rs:84-287) per frame, out_kind
  * NEXG_OUT_SLICE, 16 bytes: layer boundaries only, no checksums. FrameSlice
  * has no ParseMode (NEXG_PARSE_STRICT is ignored) and reports every inner
@@ -216,15 +297,29 @@ typedef struct nexg_slice {
  *                     or offsets[i+1]-offsets[i] (offsets has count+1 entries)
  * Every len(i) must be <= 65535 (frames are at most one IPv4 datagram; the
  * reference's default read buffer is 4096, nex-datalink/src/lib.rs:229).
- * data_bytes bounds every device load: no byte at or past data+data_bytes is
- * read. All pointers are device pointers. */
+ * data_bytes bounds every frame extent: a frame reaching past data+data_bytes
+ * gets NEXG_ERR_BAD_EXTENT. Device loads are whole 16-B aligned blocks: the
+ * kernels read only inside the 16-B aligned blocks that overlap
+ * [data, data + data_bytes) (bytes of those blocks outside the range may be
+ * read and are ignored; such a block cannot cross a page, so this never
+ * faults). All pointers are device pointers.
+ *
+ * hints: NEXG_FRAMES_MONOTONE (offsets + lengths layouts) promises that
+ * offsets are nondecreasing and frames do not overlap, with small gaps
+ * between consecutive frames (e.g. the 16-B record headers a capture file
+ * keeps in place, nexg_pcap_read_raw). Such batches are streamed as
+ * contiguous spans (gap bytes are read and ignored) instead of by the
+ * two-pass explicit-length kernels. The kernels verify the promise per
+ * 256-frame group and fall back to per-frame reads where it fails, so a
+ * wrong hint costs speed, never correctness. */
+#define NEXG_FRAMES_MONOTONE 0x1u
 typedef struct nexg_frames {
     const uint8_t* data;
     uint64_t data_bytes;
     const uint64_t* offsets;
     const uint32_t* lengths;
     uint32_t stride;
-    uint32_t reserved;
+    uint32_t hints; /* NEXG_FRAMES_* */
     uint64_t count;
 } nexg_frames;
 
@@ -253,6 +348,51 @@ int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames,
 /* util::checksum(buf_i, skipword) for every buffer (util.rs:65-78). */
 int nexg_checksum_batch(nexg_ctx* ctx, const nexg_frames* bufs,
                         uint32_t skipword, uint16_t* out, void* stream);
+
+/* nexg_desc[count] from a NEXG_OUT_SPARSE result of the same batch and parse
+ * option (codes + exceptions, layout above). Stream-ordered, device pointers. */
+int nexg_sparse_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
+                       const void* sparse, nexg_desc* out, void* stream);
+
+/* ---- in-place checksum fix-up (mutable views) -------------
+ * Rewrites checksum fields inside the frames, with the raw-buffer semantics
+ * of the reference's mutable views, composed the way
+ * examples/mutable_chaining.rs:19-63 chains them (payload_mut of each layer
+ * is the buffer of the next):
+ *   MutableEthernetPacket (>= 14 B; payload = bytes after 14)
+ *   EtherType 0x0800 -> MutableIpv4Packet::new (ipv4.rs:540-566: >= 20 B,
+ *     IHL >= 5, IHL*4 <= len, total 0 or >= IHL*4); recompute_checksum
+ *     (ipv4.rs:669-679: util::checksum(raw[..header_len], 5) into bytes
+ *     10..11); payload_mut = [hl, hl + total_len - hl) with total_len = 0 ->
+ *     len, else min(total, len) (ipv4.rs:591-596, 697-704)
+ *   EtherType 0x86DD -> MutableIpv6Packet::new (>= 40 B); payload_mut =
+ *     every byte after 40 (ipv6.rs:423-426; extension headers not walked)
+ *   protocol / next header (raw byte) 17 -> MutableUdpPacket::new (udp.rs:
+ *     101-121) + recompute_checksum with the enclosing IP addresses as
+ *     context (udp.rs:338-369: pseudo-header sum over the WHOLE payload_mut
+ *     slice, skipword 3, into bytes 6..7); 6 -> MutableTcpPacket (tcp.rs:
+ *     857-876, 1009-1040, skipword 8, bytes 16..17); 1 (IPv4 only) ->
+ *     MutableIcmpPacket (icmp.rs:267-273 via IcmpPacket::from_buf, >= 8 B;
+ *     icmp.rs:372-377 util::checksum(raw, 1), bytes 2..3); 58 (IPv6 only) ->
+ *     MutableIcmpv6Packet (icmpv6.rs:316-322, 450-470).
+ * A view whose constructor returns None is skipped. `which` selects
+ * NEXG_FIX_IP and/or NEXG_FIX_L4. With parse flag NEXG_PARSE_FROM_IP the IP
+ * header starts at ip_offset and the version nibble picks the family.
+ * The bytes of frames->data are rewritten in place (the batch's data must be
+ * writable device memory; frames must not overlap). out (optional, may be
+ * NULL): nexg_fixup[count]. */
+#define NEXG_FIX_IP 0x1u
+#define NEXG_FIX_L4 0x2u
+typedef struct nexg_fixup {
+    uint8_t done;   /* NEXG_FIX_* bits of the fields written                 */
+    uint8_t proto;  /* L4 protocol number whose view was built (0 if none)  */
+    uint16_t ip_csum; /* value written at IPv4 bytes 10..11 (if NEXG_FIX_IP) */
+    uint16_t l4_csum; /* value written into the L4 header (if NEXG_FIX_L4)   */
+    uint16_t l4_off;  /* frame offset of the L4 header                       */
+} nexg_fixup;
+int nexg_recompute_checksums_batch(nexg_ctx* ctx, const nexg_frames* frames,
+                                   const nexg_parse_option* option, uint32_t which,
+                                   nexg_fixup* out, void* stream);
 
 /* ---- option lists ---------------------------------------
  * The Vec fields of Frame's headers, decoded on the device into fixed-capacity

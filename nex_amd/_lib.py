@@ -41,6 +41,9 @@ def load():
         "nexg_ctx_cu_count": (I, [P]),
         "nexg_parse_batch": (I, [P, ctypes.POINTER(abi.Frames), ctypes.POINTER(abi.ParseOptionC), I, P, P]),
         "nexg_checksum_batch": (I, [P, ctypes.POINTER(abi.Frames), U32, P, P]),
+        "nexg_sparse_expand": (I, [P, ctypes.POINTER(abi.Frames), ctypes.POINTER(abi.ParseOptionC), P, P, P]),
+        "nexg_recompute_checksums_batch": (I, [P, ctypes.POINTER(abi.Frames), ctypes.POINTER(abi.ParseOptionC),
+                                               U32, P, P]),
         "nexg_probe_stream": (I, [P, P, U64, U32, P, P]),
         "nexg_decode_options": (I, [P, ctypes.POINTER(abi.Frames), P, P, P]),
         "nexg_build_udp4_batch": (I, [P, ctypes.POINTER(abi.Udp4Build), P, U32, P]),

@@ -48,6 +48,66 @@ OUT_RECORD = 2
 OUT_SLICE = 3
 OUT_FLAGS = 4  # nexg_desc.flags only (include/nexg.h)
 OUT_VERDICT = 5  # lossless 2-B form of the flags word (include/nexg.h)
+OUT_SPARSE = 6  # 1-B shape codes + per-64-frame exception slots (include/nexg.h)
+
+# NEXG_FRAMES_* hints (nexg_frames.hints)
+FRAMES_MONOTONE = 0x1
+
+# NEXG_OUT_SPARSE code byte
+SPARSE_IP_OK = 0x10
+SPARSE_L4_OK = 0x20
+SPARSE_TAG_SHIFT = 6
+SHAPE_EXCEPTION, SHAPE_IP_NONE = 0, 10
+_V4 = L_ETHERNET | L_IP | L_IPV4 | C_IP_CHECKED
+_V6 = L_ETHERNET | L_IP | L_IPV6
+#: NEXG_SHAPE_FLAGS / NEXG_SHAPE_HDR (include/nexg.h), indexed by shape 0..15
+SHAPE_FLAGS = np.array([
+    0,
+    _V4 | L_TRANSPORT | L_UDP | C_L4_CHECKED, _V4 | L_TRANSPORT | L_TCP | C_L4_CHECKED, _V4 | L_ICMP | C_L4_CHECKED,
+    _V6 | L_TRANSPORT | L_UDP | C_L4_CHECKED, _V6 | L_TRANSPORT | L_TCP | C_L4_CHECKED, _V6 | L_ICMPV6 | C_L4_CHECKED,
+    L_ETHERNET, _V4, _V6, L_ETHERNET | L_IP,
+    1 << STATUS_SHIFT, 2 << STATUS_SHIFT, 3 << STATUS_SHIFT, 4 << STATUS_SHIFT, 7 << STATUS_SHIFT], np.uint32)
+SHAPE_HDR = np.array([0, 28, 40, 24, 48, 60, 44, 0, 20, 40, 0, 0, 0, 0, 0, 0], np.int64)
+
+
+def sparse_exc_offset(count):
+    """NEXG_SPARSE_EXC_OFFSET: byte offset of the exception slots."""
+    return (int(count) + 15) & ~15
+
+
+def sparse_bytes(count):
+    """NEXG_SPARSE_BYTES: size of a NEXG_OUT_SPARSE output."""
+    return sparse_exc_offset(count) + 8 * int(count)
+
+
+def sparse_to_desc(buf, count, lengths, parse_flags=0, ip_offset=0):
+    """nexg_desc[count] from a NEXG_OUT_SPARSE output (uint8 host array):
+    nexg_sparse_decode per code, exceptions looked up per 64-frame group.
+    `lengths` = every frame's length (int array)."""
+    buf = np.asarray(buf, np.uint8)
+    codes = buf[:count].astype(np.int64)
+    exc = buf[sparse_exc_offset(count):sparse_exc_offset(count) + 8 * count].view(DESC_DTYPE)
+    lengths = np.asarray(lengths, np.int64)[:count]
+    shape, tags = codes & 0xF, (codes >> SPARSE_TAG_SHIFT) & 3
+    out = np.zeros(count, DESC_DTYPE)
+    fl = SHAPE_FLAGS[shape].astype(np.int64)
+    pay = (shape >= 1) & (shape < SHAPE_IP_NONE)
+    fl |= np.where(pay & ((codes & SPARSE_IP_OK) != 0), C_IP_OK, 0)
+    fl |= np.where(pay & ((codes & SPARSE_L4_OK) != 0), C_L4_OK, 0)
+    fl |= np.where((pay | (shape == SHAPE_IP_NONE)) & (tags > 0), L_VLAN, 0)
+    base = ip_offset if parse_flags & PARSE_FROM_IP else 14
+    h = base + 4 * tags + SHAPE_HDR[shape]
+    plen = np.where(pay, lengths - h, 0)
+    out["flags"] = fl.astype(np.uint32)
+    out["payload_len"] = (plen & 0xFFFF).astype(np.uint16)
+    out["payload_off"] = np.where(pay & (lengths > h), h, 0).astype(np.uint16)
+    ex = np.nonzero(shape == SHAPE_EXCEPTION)[0]
+    if len(ex):
+        grp = ex // 64
+        first = np.searchsorted(ex, grp * 64)  # index in ex of the group's first exception
+        rank = np.arange(len(ex)) - first
+        out[ex] = exc[grp * 64 + rank]
+    return out
 
 # FrameSlice presence bits (nexg_slice.flags)
 S_DATALINK = 1 << 0
@@ -110,7 +170,7 @@ class Frames(ctypes.Structure):
         ("offsets", ctypes.c_void_p),
         ("lengths", ctypes.c_void_p),
         ("stride", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("hints", ctypes.c_uint32),
         ("count", ctypes.c_uint64),
     ]
 
@@ -205,10 +265,21 @@ class IcmpEchoBuild(ctypes.Structure):
     ]
 
 
+# in-place checksum fix-up (nexg_recompute_checksums_batch)
+FIX_IP = 0x1
+FIX_L4 = 0x2
+FIXUP_DTYPE = np.dtype([("done", "u1"), ("proto", "u1"), ("ip_csum", "<u2"), ("l4_csum", "<u2"),
+                        ("l4_off", "<u2")])
+assert FIXUP_DTYPE.itemsize == 8
+
+#: static inline helpers of include/nexg.h (header-only, not exported)
+HEADER_INLINE = ("nexg_sparse_decode",)
+
 #: every symbol include/nexg.h declares (tests check the .so exports them)
 EXPORTED_SYMBOLS = (
     "nexg_abi_version", "nexg_strerror", "nexg_ctx_create", "nexg_ctx_destroy",
     "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch", "nexg_decode_options", "nexg_probe_stream",
+    "nexg_sparse_expand", "nexg_recompute_checksums_batch",
     "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_build_tcp_batch",
     "nexg_build_icmp_echo_batch", "nexg_pcap_open", "nexg_pcap_linktype", "nexg_pcap_last_error",
     "nexg_pcap_read_batch", "nexg_pcap_read_raw", "nexg_pcap_set_read_threads", "nexg_pcap_close", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",

@@ -647,6 +647,51 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w)[20], uint32_t len, uint32_t op
     return true;
 }
 
+// nexg_sparse_decode (include/nexg.h) on the device: the same table macros
+NEXG_HD bool sparse_decode(uint32_t code, uint32_t len, uint32_t opt_flags, uint32_t ip_offset, nexg_desc& d) {
+    const uint32_t shape = code & 0xFu, tags = (code >> NEXG_SPARSE_TAG_SHIFT) & 3u;
+    if (shape == (uint32_t)NEXG_SHAPE_EXCEPTION) return false;
+    d.flags = NEXG_SHAPE_FLAGS(shape);
+    d.payload_off = 0;
+    d.payload_len = 0;
+    if (shape >= (uint32_t)NEXG_SHAPE_IP_NONE) {
+        if (shape == (uint32_t)NEXG_SHAPE_IP_NONE && tags) d.flags |= NEXG_L_VLAN;
+        return true;
+    }
+    d.flags |= ((code & NEXG_SPARSE_IP_OK) ? NEXG_C_IP_OK : 0u) | ((code & NEXG_SPARSE_L4_OK) ? NEXG_C_L4_OK : 0u) |
+               (tags ? NEXG_L_VLAN : 0u);
+    const uint32_t h = ((opt_flags & NEXG_PARSE_FROM_IP) ? ip_offset : 14u) + 4u * tags + NEXG_SHAPE_HDR(shape);
+    d.payload_len = (uint16_t)(len - h);
+    d.payload_off = (uint16_t)(len > h ? h : 0u);
+    return true;
+}
+
+// NEXG_OUT_SPARSE (include/nexg.h): the 1-B code of a finished record, or 0
+// (exception) unless sparse_decode(code, len, ...) reproduces the record's
+// descriptor exactly — lossless by construction.
+NEXG_HD uint32_t sparse_encode(const nexg_record& r, uint32_t opt_flags, uint32_t ip_offset) {
+    const uint32_t st = (r.flags >> NEXG_STATUS_SHIFT) & 7u;
+    uint32_t code = 0;
+    if (st) {
+        code = st == NEXG_ERR_BAD_EXTENT ? 15u : (st <= 4u ? 10u + st : 0u);
+    } else {
+        const uint32_t base = (opt_flags & NEXG_PARSE_FROM_IP) ? ip_offset : 14u;
+        const uint32_t l3 = r.l3_off, tags = (l3 - base) >> 2;
+        const uint32_t core = r.flags & ~(NEXG_C_IP_OK | NEXG_C_L4_OK | NEXG_L_VLAN);
+        uint32_t shape = 0;
+#pragma unroll
+        for (uint32_t s = 1; s <= (uint32_t)NEXG_SHAPE_IP_NONE; s++) shape = core == NEXG_SHAPE_FLAGS(s) ? s : shape;
+        if (shape == 0u || l3 < base || tags > 2u) return 0u;
+        code = shape | ((r.flags & NEXG_C_IP_OK) ? NEXG_SPARSE_IP_OK : 0u) |
+               ((r.flags & NEXG_C_L4_OK) ? NEXG_SPARSE_L4_OK : 0u) | (tags << NEXG_SPARSE_TAG_SHIFT);
+        const uint32_t hdr = shape < (uint32_t)NEXG_SHAPE_IP_NONE ? NEXG_SHAPE_HDR(shape) : 0u;
+        if (base + 4u * tags + hdr > r.packet_len) return 0u;
+    }
+    nexg_desc d;
+    if (!sparse_decode(code, r.packet_len, opt_flags, ip_offset, d)) return 0u;
+    return (d.flags == r.flags && d.payload_off == r.payload_off && d.payload_len == r.payload_len) ? code : 0u;
+}
+
 // frame.rs:570-607 parse_frame_from_bytes (+ 381-422 dummy Ethernet).
 template <class F>
 NEXG_HD void parse_frame(const F& f, uint32_t parity, uint32_t len,

@@ -16,9 +16,42 @@ struct nexg_ctx {
     int cu_count;
     char arch[64];
     char last_error[256];
+    void* scratch;          // device memory for per-call hand-offs (TwoPass tail sums)
+    uint64_t scratch_bytes;
 };
 
 namespace {
+
+// Every entry point runs with the context's device current and restores the
+// caller's afterwards: allocations and NULL-stream launches then land on the
+// device the context is bound to, whichever device the thread had selected.
+struct DeviceGuard {
+    int prev = -1;
+    bool switched = false;
+    explicit DeviceGuard(const nexg_ctx* ctx) {
+        if (ctx && hipGetDevice(&prev) == hipSuccess && prev != ctx->device)
+            switched = hipSetDevice(ctx->device) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (switched) (void)hipSetDevice(prev);
+    }
+};
+
+// ctx scratch of at least `bytes` (grown, never shrunk; hipFree is
+// device-synchronous, so no launch still reads the old block)
+void* scratch(nexg_ctx* ctx, uint64_t bytes) {
+    if (ctx->scratch_bytes >= bytes) return ctx->scratch;
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+    const uint64_t want = bytes < (1ull << 20) ? (1ull << 20) : bytes;
+    if (hipMalloc(&ctx->scratch, want) != hipSuccess) {
+        ctx->scratch = nullptr;
+        return nullptr;
+    }
+    ctx->scratch_bytes = want;
+    return ctx->scratch;
+}
 
 int fail(nexg_ctx* ctx, int code, const char* fmt, const char* detail) {
     if (ctx) snprintf(ctx->last_error, sizeof(ctx->last_error), fmt, detail ? detail : "");
@@ -47,6 +80,7 @@ nexg::ParseArgs to_args(const nexg_frames* f) {
     a.lengths = f->lengths;
     a.stride = f->stride;
     a.count = f->count;
+    a.hints = f->hints;
     return a;
 }
 
@@ -86,6 +120,10 @@ int nexg_ctx_create(int device, nexg_ctx** out) {
 }
 
 int nexg_ctx_destroy(nexg_ctx* ctx) {
+    if (ctx && ctx->scratch) {
+        DeviceGuard g(ctx);
+        (void)hipFree(ctx->scratch);
+    }
     free(ctx);
     return NEXG_OK;
 }
@@ -99,21 +137,55 @@ int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_
     if (!ctx) return NEXG_EINVAL;
     if (!frames_valid(frames)) return fail(ctx, NEXG_EINVAL, "invalid frame batch%s", nullptr);
     if (out_kind != NEXG_OUT_DESC && out_kind != NEXG_OUT_RECORD && out_kind != NEXG_OUT_SLICE &&
-        out_kind != NEXG_OUT_FLAGS && out_kind != NEXG_OUT_VERDICT)
+        out_kind != NEXG_OUT_FLAGS && out_kind != NEXG_OUT_VERDICT && out_kind != NEXG_OUT_SPARSE)
         return fail(ctx, NEXG_EINVAL, "invalid out_kind%s", nullptr);
     if (frames->count && !out) return fail(ctx, NEXG_EINVAL, "NULL output%s", nullptr);
     const uint64_t align_mask = out_kind == NEXG_OUT_VERDICT ? 1u : out_kind == NEXG_OUT_FLAGS ? 3u
                                 : out_kind == NEXG_OUT_DESC  ? 7u : 15u;
     if ((reinterpret_cast<uint64_t>(out) & align_mask) != 0)
         return fail(ctx, NEXG_EINVAL, "misaligned output%s", nullptr);
+    DeviceGuard g(ctx);
     nexg::ParseArgs a = to_args(frames);
     a.opt_flags = option ? option->flags : 0u;
     a.ip_offset = option ? option->ip_offset : 0u;
     a.out = out;
     a.tile_order = nexg::tile_order_for(a);
     const nexg::ParseVariant v = nexg::choose_parse_variant(a);
+    if (nexg::parse_needs_tail(v, out_kind) && a.count) {
+        a.tail = static_cast<uint32_t*>(scratch(ctx, a.count * 4u));
+        if (!a.tail) return fail(ctx, NEXG_ENOMEM, "device scratch allocation failed%s", nullptr);
+    }
     return hip_status(ctx, nexg::launch_parse(v, a, out_kind, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
+}
+
+int nexg_sparse_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
+                       const void* sparse, nexg_desc* out, void* stream) {
+    if (!ctx) return NEXG_EINVAL;
+    if (!frames_valid(frames)) return fail(ctx, NEXG_EINVAL, "invalid frame batch%s", nullptr);
+    if (frames->count && (!sparse || !out)) return fail(ctx, NEXG_EINVAL, "NULL sparse input or output%s", nullptr);
+    if (((reinterpret_cast<uint64_t>(sparse) & 15u) | (reinterpret_cast<uint64_t>(out) & 7u)) != 0)
+        return fail(ctx, NEXG_EINVAL, "misaligned sparse input or output%s", nullptr);
+    DeviceGuard g(ctx);
+    nexg::ParseArgs a = to_args(frames);
+    a.opt_flags = option ? option->flags : 0u;
+    a.ip_offset = option ? option->ip_offset : 0u;
+    return hip_status(ctx, nexg::launch_sparse_expand(a, static_cast<const uint8_t*>(sparse), out,
+                                                      static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
+int nexg_recompute_checksums_batch(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
+                                   uint32_t which, nexg_fixup* out, void* stream) {
+    if (!ctx) return NEXG_EINVAL;
+    if (!frames_valid(frames)) return fail(ctx, NEXG_EINVAL, "invalid frame batch%s", nullptr);
+    if ((which & ~(NEXG_FIX_IP | NEXG_FIX_L4)) != 0) return fail(ctx, NEXG_EINVAL, "invalid fix-up selection%s", nullptr);
+    if ((reinterpret_cast<uint64_t>(out) & 7u) != 0) return fail(ctx, NEXG_EINVAL, "misaligned output%s", nullptr);
+    DeviceGuard g(ctx);
+    nexg::ParseArgs a = to_args(frames);
+    a.opt_flags = option ? option->flags : 0u;
+    a.ip_offset = option ? option->ip_offset : 0u;
+    return hip_status(ctx, nexg::launch_recompute(a, which, out, static_cast<hipStream_t>(stream)), NEXG_ELAUNCH);
 }
 
 int nexg_checksum_batch(nexg_ctx* ctx, const nexg_frames* bufs, uint32_t skipword, uint16_t* out,
@@ -122,6 +194,7 @@ int nexg_checksum_batch(nexg_ctx* ctx, const nexg_frames* bufs, uint32_t skipwor
     if (!frames_valid(bufs)) return fail(ctx, NEXG_EINVAL, "invalid buffer batch%s", nullptr);
     if (bufs->count && !out) return fail(ctx, NEXG_EINVAL, "NULL output%s", nullptr);
     nexg::ParseArgs a = to_args(bufs);
+    DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_checksum(a, skipword, out, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
 }
@@ -134,6 +207,7 @@ int nexg_decode_options(nexg_ctx* ctx, const nexg_frames* frames, const nexg_rec
     if ((reinterpret_cast<uint64_t>(out) & 15u) != 0 || (reinterpret_cast<uint64_t>(records) & 15u) != 0)
         return fail(ctx, NEXG_EINVAL, "misaligned records or output%s", nullptr);
     const nexg::ParseArgs a = to_args(frames);
+    DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_decode_options(a, records, out, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
 }
@@ -145,6 +219,7 @@ int nexg_probe_stream(nexg_ctx* ctx, const void* data, uint64_t bytes, uint32_t 
         (reinterpret_cast<uint64_t>(data) & 15u) != 0 || (reinterpret_cast<uint64_t>(out) & 7u) != 0)
         return fail(ctx, NEXG_EINVAL, "probe: bytes must be a multiple of 16384, buffers aligned%s", nullptr);
     if (bytes / 16384u > 0x7FFFFFFFull) return fail(ctx, NEXG_ERANGE, "probe: too many tiles%s", nullptr);
+    DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_probe_stream(static_cast<const uint8_t*>(data), bytes / 16384u,
                                                      out_per_64 == 8, out, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
@@ -160,6 +235,7 @@ int nexg_build_udp4_batch(nexg_ctx* ctx, const nexg_udp4_build* p, uint8_t* out,
     if (p->payload_len && !p->payload) return fail(ctx, NEXG_EINVAL, "NULL payload%s", nullptr);
     if (out_stride < 42u + p->payload_len)
         return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_build_udp4(*p, out, out_stride, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
 }
@@ -176,6 +252,7 @@ int nexg_build_udp6_batch(nexg_ctx* ctx, const nexg_udp6_build* p, uint8_t* out,
     if (p->payload_len && !p->payload) return fail(ctx, NEXG_EINVAL, "NULL payload%s", nullptr);
     if (out_stride < 62u + p->payload_len)
         return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_build_udp6(*p, out, out_stride, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
 }
@@ -202,6 +279,7 @@ int nexg_build_tcp_batch(nexg_ctx* ctx, const nexg_tcp_build* p, uint8_t* out, u
     if (p->payload_len && !p->payload) return fail(ctx, NEXG_EINVAL, "NULL payload%s", nullptr);
     const uint64_t flen = 14u + (p->ip.family == 4 ? 20u : 40u) + seg;
     if (out_stride < flen) return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_build_tcp(*p, out, out_stride, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
 }
@@ -216,6 +294,7 @@ int nexg_build_icmp_echo_batch(nexg_ctx* ctx, const nexg_icmp_echo_build* p, uin
     if (p->payload_len && !p->payload) return fail(ctx, NEXG_EINVAL, "NULL payload%s", nullptr);
     const uint64_t flen = 14u + (p->ip.family == 4 ? 20u : 40u) + len;
     if (out_stride < flen) return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_build_icmp_echo(*p, out, out_stride, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
 }
@@ -225,6 +304,7 @@ int nexg_gen_lengths(nexg_ctx* ctx, int workload, uint64_t seed, uint64_t first_
     if (!ctx) return NEXG_EINVAL;
     if (workload != NEXG_WL_UDP64 && workload != NEXG_WL_IMIX) return fail(ctx, NEXG_EINVAL, "workload%s", nullptr);
     if (count && !lengths) return fail(ctx, NEXG_EINVAL, "NULL lengths%s", nullptr);
+    DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_gen_lengths(workload, seed, first_index, count, lengths,
                                                     static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
@@ -238,6 +318,7 @@ int nexg_gen_frames(nexg_ctx* ctx, int workload, uint64_t seed, uint64_t first_i
     if (count && !data) return fail(ctx, NEXG_EINVAL, "NULL data%s", nullptr);
     if (!offsets && stride < (workload == NEXG_WL_UDP64 ? 64u : 1500u))
         return fail(ctx, NEXG_EINVAL, "stride shorter than the workload's frames%s", nullptr);
+    DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_gen_frames(workload, seed, first_index, count, data, offsets,
                                                    stride, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
@@ -249,6 +330,7 @@ int nexg_gen_udp4_params(nexg_ctx* ctx, uint64_t seed, uint64_t first_index, uin
     if (!ctx) return NEXG_EINVAL;
     if (count && (!src_ip || !dst_ip || !src_port || !dst_port || !ip_id))
         return fail(ctx, NEXG_EINVAL, "NULL output array%s", nullptr);
+    DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_gen_udp4_params(seed, first_index, count, src_ip, dst_ip,
                                                         src_port, dst_port, ip_id,
                                                         static_cast<hipStream_t>(stream)),

@@ -20,6 +20,9 @@ struct ParseArgs {
     uint32_t ip_offset;
     void* out;
     uint32_t tile_order = 0;  // fixed-stride tiles: 0 in grid order, 1 XCD-contiguous
+    uint32_t hints = 0;       // NEXG_FRAMES_* (include/nexg.h)
+    uint32_t* tail = nullptr; // TwoPass tail-sum hand-off (count entries) for outputs
+                              // narrower than 4 B per frame; null -> the output itself
 };
 
 // Kernel variants of the parse path.
@@ -32,10 +35,19 @@ enum class ParseVariant {
 };
 
 hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStream_t s);
+// TwoPass hands each frame's tail sum to pass 2 through its own output
+// element; outputs narrower than 4 B need a.tail (count u32) instead.
+inline bool parse_needs_tail(ParseVariant v, int out_kind) {
+    return v == ParseVariant::TwoPass && (out_kind == NEXG_OUT_VERDICT || out_kind == NEXG_OUT_SPARSE);
+}
 uint32_t tile_order_for(const ParseArgs& a);
 ParseVariant choose_parse_variant(const ParseArgs& a);
 
 hipError_t launch_checksum(const ParseArgs& a, uint32_t skipword, uint16_t* out, hipStream_t s);
+
+hipError_t launch_sparse_expand(const ParseArgs& a, const uint8_t* sparse, nexg_desc* out, hipStream_t s);
+
+hipError_t launch_recompute(const ParseArgs& a, uint32_t which, nexg_fixup* out, hipStream_t s);
 
 hipError_t launch_decode_options(const ParseArgs& a, const nexg_record* recs, nexg_options* out,
                                  hipStream_t s);

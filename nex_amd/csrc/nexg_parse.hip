@@ -42,7 +42,22 @@ ParseVariant choose_parse_variant(const ParseArgs& a) {
         return a.stride == 64u ? ParseVariant::TileStride64 : ParseVariant::TileStride;
     }
     if (!a.lengths && (a.offsets || a.stride > 0)) return ParseVariant::SpanTile;
+    // explicit lengths in file order (capture records with their headers in
+    // place): one ordered span per group, gaps read through (include/nexg.h)
+    if (a.offsets && (a.hints & NEXG_FRAMES_MONOTONE)) return ParseVariant::SpanTile;
     return ParseVariant::TwoPass;
+}
+
+// Span kernel generation: NEXG_SPAN=1 (4 barriers per 16-KiB sub-tile),
+// 2 (2 barriers), 2d (8-KiB double-buffered sub-tiles, 1 barrier) overrides
+// for measurement; the default is the measured best.
+static int span_variant() {
+    static const int v = [] {
+        const char* e = getenv("NEXG_SPAN");
+        if (!e) return 2;
+        return strcmp(e, "1") == 0 ? 1 : strcmp(e, "2d") == 0 ? 3 : 2;
+    }();
+    return v;
 }
 
 template <int OUT>
@@ -60,7 +75,9 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             hipLaunchKernelGGL((k_parse<1, OUT, 0, 128>), grid, block, 0, s, a);
             break;
         case ParseVariant::SpanTile:
-            hipLaunchKernelGGL((k_parse_span<OUT, 1>), grid, block, 0, s, a);
+            if (span_variant() == 1) hipLaunchKernelGGL((k_parse_span<OUT, 1>), grid, block, 0, s, a);
+            else if (span_variant() == 3) hipLaunchKernelGGL((k_parse_span2<OUT, 8192, 2>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_parse_span2<OUT, 16384, 1>), grid, block, 0, s, a);
             break;
         case ParseVariant::TwoPass:
             hipLaunchKernelGGL((k_tail_sums<OUT, 4>), grid, block, 0, s, a);
@@ -89,11 +106,36 @@ hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStr
     if (a.count == 0) return hipSuccess;
     if (out_kind == NEXG_OUT_SLICE) return launch_slice(v, a, s);
     if (out_kind == NEXG_OUT_FLAGS) return launch_parse_out<NEXG_OUT_FLAGS>(v, a, s);
-    if (out_kind == NEXG_OUT_VERDICT)  // no 4-B hand-off slot for the TwoPass tail sums
-        return launch_parse_out<NEXG_OUT_VERDICT>(v == ParseVariant::TwoPass ? ParseVariant::LaneWindow : v,
-                                                  a, s);
+    // TwoPass with the 2-B / 1-B outputs hands tail sums through a.tail
+    if (parse_needs_tail(v, out_kind) && !a.tail) return hipErrorInvalidValue;
+    if (out_kind == NEXG_OUT_VERDICT) return launch_parse_out<NEXG_OUT_VERDICT>(v, a, s);
+    if (out_kind == NEXG_OUT_SPARSE) return launch_parse_out<NEXG_OUT_SPARSE>(v, a, s);
     return out_kind == NEXG_OUT_DESC ? launch_parse_out<NEXG_OUT_DESC>(v, a, s)
                                      : launch_parse_out<NEXG_OUT_RECORD>(v, a, s);
+}
+
+// nexg_sparse_expand: lane per frame; code -> nexg_desc (include/nexg.h
+// table), exception codes take the group's next exception in frame order.
+__global__ __launch_bounds__(256) void k_sparse_expand(ParseArgs a, const uint8_t* sparse, nexg_desc* out) {
+    const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
+    const bool valid = idx < a.count;
+    const uint32_t code = valid ? sparse[idx] : 0xFFu;
+    const uint64_t m = __ballot(code == 0u);
+    if (!valid) return;
+    uint64_t off;
+    uint32_t len = 0;
+    frame_extent(a, idx, off, len);
+    nexg_desc d;
+    if (!sparse_decode(code, len, a.opt_flags, a.ip_offset, d))
+        d = reinterpret_cast<const nexg_desc*>(sparse + NEXG_SPARSE_EXC_OFFSET(a.count))[(idx & ~63ull) + lanes_below(m)];
+    out[idx] = d;
+}
+
+hipError_t launch_sparse_expand(const ParseArgs& a, const uint8_t* sparse, nexg_desc* out, hipStream_t s) {
+    if (a.count == 0) return hipSuccess;
+    const uint64_t blocks = (a.count + kTile - 1) / kTile;
+    hipLaunchKernelGGL(k_sparse_expand, dim3((uint32_t)blocks), dim3(kTile), 0, s, a, sparse, out);
+    return hipGetLastError();
 }
 
 // nexg_decode_options: Ipv4Header.options (ipv4.rs:442-508) and
@@ -201,6 +243,32 @@ hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, bool write8,
     if (write8) hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out);
     else hipLaunchKernelGGL(k_probe_stream<false>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out);
     return hipGetLastError();
+}
+
+// util.rs:65-71 checksum(buf, skipword) per buffer; words outside the buffer
+// and the skipped word contribute nothing; empty -> 0.
+__global__ __launch_bounds__(256) void k_checksum(ParseArgs a, uint32_t skipword, uint16_t* out) {
+    const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
+    if (idx >= a.count) return;
+    const uint64_t off = a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride;
+    const uint64_t l64 = a.lengths ? (uint64_t)a.lengths[idx]
+                                   : (a.offsets ? a.offsets[idx + 1] - off : (uint64_t)a.stride);
+    if (l64 == 0 || l64 > 65535u || off > a.data_bytes || l64 > a.data_bytes - off) {
+        out[idx] = 0;
+        return;
+    }
+    const uint32_t len = (uint32_t)l64;
+    GlobalFrame f{a.data + off};
+    FrameOps<GlobalFrame> o{f, (uint32_t)((reinterpret_cast<uint64_t>(f.g)) & 1u)};
+    const uint64_t sk = 2ull * skipword;
+    uint64_t t;
+    if (sk >= len) {
+        t = o.wsum(0, len);
+    } else {
+        t = o.wsum(0, (uint32_t)sk);
+        if (sk + 2 < len) t += o.wsum((uint32_t)sk + 2u, len);
+    }
+    out[idx] = (uint16_t)fold_complement(t);
 }
 
 hipError_t launch_checksum(const ParseArgs& a, uint32_t skipword, uint16_t* out, hipStream_t s) {

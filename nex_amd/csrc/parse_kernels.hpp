@@ -53,6 +53,41 @@ __device__ __forceinline__ void store_result(void* out, uint64_t idx, const nexg
     }
 }
 
+// rank of this lane among the set lanes of m below it (v_mbcnt)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// NEXG_OUT_SPARSE store (include/nexg.h). Called by all 64 lanes of a wave
+// together (valid = the lane holds frame idx; idx = 64-frame-group base +
+// lane): a ballot compacts the wave's exceptions into exc[group*64 + rank];
+// the 1-B codes of lanes 4q..4q+3 are gathered by DPP quad broadcasts and
+// stored as one non-temporal dword by lane 4q.
+__device__ __forceinline__ void store_sparse(const ParseArgs& a, uint64_t idx, bool valid, const nexg_record& r) {
+    const uint32_t code = valid ? sparse_encode(r, a.opt_flags, a.ip_offset) : 0u;
+    const bool exc = valid && code == 0u;
+    const uint64_t m = __ballot(exc);
+    uint8_t* codes = reinterpret_cast<uint8_t*>(a.out);
+    if (exc) {
+        uint2* x = reinterpret_cast<uint2*>(codes + NEXG_SPARSE_EXC_OFFSET(a.count));
+        x[(idx & ~63ull) + lanes_below(m)] =
+            make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
+    }
+    const uint32_t c1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)code, 0x55, 0xF, 0xF, false);  // quad_perm 1111
+    const uint32_t c2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)code, 0xAA, 0xF, 0xF, false);  // quad_perm 2222
+    const uint32_t c3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)code, 0xFF, 0xF, 0xF, false);  // quad_perm 3333
+    if ((idx & 3u) == 0u && idx < a.count)
+        __builtin_nontemporal_store(code | (c1 << 8) | (c2 << 16) | (c3 << 24),
+                                    reinterpret_cast<uint32_t*>(codes + idx));
+}
+
+// every lane of the wave calls this together (see store_sparse)
+template <int OUT>
+__device__ __forceinline__ void store_out(const ParseArgs& a, uint64_t idx, bool valid, const nexg_record& r) {
+    if constexpr (OUT == NEXG_OUT_SPARSE) store_sparse(a, idx, valid, r);
+    else if (valid) store_result<OUT>(a.out, idx, r);
+}
+
 // Record output of a 256-frame tile through LDS: each thread has written its
 // 64-B record at stage + t * PITCH (call after a barrier); the tile's nf
 // records leave as contiguous 16-B stores (1 KiB per wave instruction)
@@ -137,12 +172,14 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
             bad = len > 65535u || (first + tid) * S + len > a.data_bytes;
         }
     } else {
-        if (tid >= nf) return;
-        const uint64_t off = a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride;
-        const uint64_t l64 = a.lengths ? (uint64_t)a.lengths[idx]
-                                       : (a.offsets ? a.offsets[idx + 1] - off : (uint64_t)a.stride);
+        // SPARSE stores need every lane of the wave; other outputs leave early
+        if (OUT != NEXG_OUT_SPARSE && tid >= nf) return;
+        const uint64_t off = tid < nf ? (a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride) : 0u;
+        const uint64_t l64 = tid >= nf ? 0u
+                             : a.lengths ? (uint64_t)a.lengths[idx]
+                                         : (a.offsets ? a.offsets[idx + 1] - off : (uint64_t)a.stride);
         bad = l64 > 65535u || off > a.data_bytes || l64 > a.data_bytes - off;
-        if (!bad) {
+        if (!bad && tid < nf) {
             len = (uint32_t)l64;
             g = a.data + off;
             o = (uint32_t)(reinterpret_cast<uint64_t>(g) & 15u);
@@ -198,38 +235,13 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
             }
         }
         if (kStaged) stage_record(slot, r);  // own slot: no other thread reads it
-        else store_result<OUT>(a.out, idx, r);
+        else if constexpr (OUT != NEXG_OUT_SPARSE) store_result<OUT>(a.out, idx, r);
     }
+    if constexpr (OUT == NEXG_OUT_SPARSE) store_sparse(a, idx, tid < nf, r);
     if (kStaged) {
         __syncthreads();
         copy_out_records<PITCH>(smem, a.out, first, nf);
     }
-}
-
-// util.rs:65-71 checksum(buf, skipword) per buffer; words outside the buffer
-// and the skipped word contribute nothing; empty -> 0.
-__global__ __launch_bounds__(256) void k_checksum(ParseArgs a, uint32_t skipword, uint16_t* out) {
-    const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
-    if (idx >= a.count) return;
-    const uint64_t off = a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride;
-    const uint64_t l64 = a.lengths ? (uint64_t)a.lengths[idx]
-                                   : (a.offsets ? a.offsets[idx + 1] - off : (uint64_t)a.stride);
-    if (l64 == 0 || l64 > 65535u || off > a.data_bytes || l64 > a.data_bytes - off) {
-        out[idx] = 0;
-        return;
-    }
-    const uint32_t len = (uint32_t)l64;
-    GlobalFrame f{a.data + off};
-    FrameOps<GlobalFrame> o{f, (uint32_t)((reinterpret_cast<uint64_t>(f.g)) & 1u)};
-    const uint64_t sk = 2ull * skipword;
-    uint64_t t;
-    if (sk >= len) {
-        t = o.wsum(0, len);
-    } else {
-        t = o.wsum(0, (uint32_t)sk);
-        if (sk + 2 < len) t += o.wsum((uint32_t)sk + 2u, len);
-    }
-    out[idx] = (uint16_t)fold_complement(t);
 }
 
 // wave-scope LDS visibility: the wave's LDS ops run in order; this only stops
@@ -244,9 +256,11 @@ constexpr uint32_t kLaneWin = 80;  // register window of k_parse_lane80
 
 // Per-frame slot the two-kernel IMIX path hands the tail sum through: the
 // first 4 bytes of the frame's own output element (overwritten by pass 2).
+// Outputs narrower than 4 B (verdict, sparse codes) hand off through a.tail.
 template <int OUT>
-__device__ __forceinline__ uint32_t* handoff_slot(void* out, uint64_t idx) {
-    return reinterpret_cast<uint32_t*>(out) + idx * (OUT == NEXG_OUT_FLAGS ? 1u : OUT == NEXG_OUT_DESC ? 2u : 16u);
+__device__ __forceinline__ uint32_t* handoff_slot(const ParseArgs& a, uint64_t idx) {
+    if (OUT == NEXG_OUT_VERDICT || OUT == NEXG_OUT_SPARSE) return a.tail + idx;
+    return reinterpret_cast<uint32_t*>(a.out) + idx * (OUT == NEXG_OUT_FLAGS ? 1u : OUT == NEXG_OUT_DESC ? 2u : 16u);
 }
 
 __device__ __forceinline__ bool frame_extent(const ParseArgs& a, uint64_t idx, uint64_t& off, uint32_t& len) {
@@ -302,7 +316,7 @@ __global__ __launch_bounds__(256) void k_tail_sums(ParseArgs a) {
         }
     }
     if (!__all(fits)) {  // wave spans >2 GiB (unordered offsets): each lane sums its own tail
-        if (have) *handoff_slot<OUT>(a.out, idx) = (uint32_t)global_le_sum(myA, myA + len - kLaneWin);
+        if (have) *handoff_slot<OUT>(a, idx) = (uint32_t)global_le_sum(myA, myA + len - kLaneWin);
         return;
     }
     acc[lane] = 0;
@@ -383,7 +397,7 @@ __global__ __launch_bounds__(256) void k_tail_sums(ParseArgs a) {
         if (gl == 0 && s) atomicAdd(&acc[fi], s);
     }
     wave_lds_sync();
-    if (have) *handoff_slot<OUT>(a.out, idx) = acc[lane];
+    if (have) *handoff_slot<OUT>(a, idx) = acc[lane];
 }
 
 // Pass 2: one lane per frame. The first 80 bytes are loaded straight into
@@ -393,20 +407,18 @@ __global__ __launch_bounds__(256) void k_tail_sums(ParseArgs a) {
 template <int OUT>
 __global__ __launch_bounds__(256) void k_parse_lane80(ParseArgs a) {
     const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
-    if (idx >= a.count) return;
-    uint64_t off;
-    uint32_t len;
+    const bool valid = idx < a.count;
+    if (OUT != NEXG_OUT_SPARSE && !valid) return;  // sparse stores need the whole wave
+    uint64_t off = 0;
+    uint32_t len = 0;
     nexg_record r{};
-    if (!frame_extent(a, idx, off, len)) {
-        r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
-        store_result<OUT>(a.out, idx, r);
-        return;
-    }
+    const bool ext = valid && frame_extent(a, idx, off, len);
+    if (valid && !ext) r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
     const uint64_t abs = reinterpret_cast<uint64_t>(a.data) + off;
     const uint64_t dend = reinterpret_cast<uint64_t>(a.data) + a.data_bytes;
-    bool done = false;
-    if ((abs & 3u) == 0 && abs + kLaneWin <= dend) {
-        const uint32_t tail = len > kLaneWin ? *handoff_slot<OUT>(a.out, idx) : 0u;
+    bool done = !ext;
+    if (ext && (abs & 3u) == 0 && abs + kLaneWin <= dend) {
+        const uint32_t tail = len > kLaneWin ? *handoff_slot<OUT>(a, idx) : 0u;
         uint32_t w[20];
 #pragma unroll
         for (int k = 0; k < 5; k++) {
@@ -421,7 +433,7 @@ __global__ __launch_bounds__(256) void k_parse_lane80(ParseArgs a) {
         GlobalFrame f{a.data + off};
         parse_frame(f, (uint32_t)(abs & 1u), len, a.opt_flags, a.ip_offset, r);
     }
-    store_result<OUT>(a.out, idx, r);
+    store_out<OUT>(a, idx, valid, r);
 }
 
 }  // namespace nexg
@@ -502,8 +514,8 @@ __global__ __launch_bounds__(256) void k_parse_span(ParseArgs a) {
                 GlobalFrame f{a.data + off};
                 parse_frame(f, (uint32_t)((base + off) & 1u), len, a.opt_flags, a.ip_offset, r);
             }
-            store_result<OUT>(a.out, idx, r);
         }
+        store_out<OUT>(a, idx, have, r);
         return;
     }
     const uint64_t A0 = (base + lo) & ~15ull;
@@ -596,12 +608,156 @@ __global__ __launch_bounds__(256) void k_parse_span(ParseArgs a) {
             GlobalFrame f{a.data + off};
             parse_frame(f, (uint32_t)((base + off) & 1u), len, a.opt_flags, a.ip_offset, r);
         }
-        if (OUT != NEXG_OUT_RECORD) store_result<OUT>(a.out, idx, r);
     }
+    if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
     if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the (now idle) byte buffer
         static_assert(OUT != NEXG_OUT_RECORD || NB * SUB >= kTile * 64u, "record staging needs 16 KiB");
         uint8_t* stage = &s_bytes[0][0];
         if (NB == 2) __syncthreads();
+        if (have) stage_record(stage + 64u * t, r);
+        __syncthreads();
+        copy_out_records<64>(stage, a.out, f0, nf);
+    }
+}
+
+// k_parse_span with two barriers per sub-tile instead of four (NB = 1), or
+// one (NB = 2, double-buffered stage). The scan needs no exchange of chunk
+// sums: chunk c = t + 256 i (the coalesced load order) sits in scan block
+// b = c / 64 = 4 i + wave, whose 64 chunks are exactly one wave's i-th
+// loads, so each wave scans its blocks in registers (DPP), stores the
+// in-block exclusive prefixes and the block totals, and after the one
+// publishing barrier a lookup adds the totals of the blocks before its
+// chunk (NBLK predicated adds). NB = 2 stages sub-tile k into buffer k & 1:
+// the barrier that publishes sub-tile k+1 also retires every lookup into
+// sub-tile k, so buffer k & 1 is free again when sub-tile k+2 arrives.
+template <int OUT, uint32_t SUB = 16384, int NB = 1, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_parse_span2(ParseArgs a) {
+    constexpr uint32_t CPT = SUB / 4096u;  // 16-B chunks per thread per sub-tile
+    constexpr uint32_t NBLK = 4u * CPT;    // 64-chunk scan blocks per sub-tile
+    static_assert(CPT >= 1 && SUB % 4096u == 0, "sub-tile is a multiple of 4 KiB");
+    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[NB][SUB];
+    __shared__ __attribute__((aligned(16))) uint32_t s_pfx[NB][SUB / 16u];
+    __shared__ __attribute__((aligned(16))) uint32_t s_tot[NB][NBLK];
+    __shared__ uint64_t s_span[2];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint64_t f0 = (uint64_t)blockIdx.x * kTile;
+    const uint64_t idx = f0 + t;
+    const uint32_t nf = a.count - f0 < kTile ? (uint32_t)(a.count - f0) : kTile;
+    const uint64_t base = reinterpret_cast<uint64_t>(a.data);
+    uint64_t off = 0;
+    uint32_t len = 0;
+    const bool have = t < nf;
+    const bool ok = have && frame_extent(a, idx, off, len);
+    if (t == 0) s_span[0] = off;
+    if (t == nf - 1) s_span[1] = off + len;
+    __syncthreads();
+    const uint64_t lo = s_span[0], hi = s_span[1];
+    const bool inside = !have || (ok && off >= lo && off + len <= hi);
+    const bool span_ok = __syncthreads_and(inside) && hi >= lo && hi - lo <= (1ull << 30);
+    nexg_record r{};
+    if (!span_ok) {  // not one ordered span here: every lane parses its own frame from HBM
+        if (have) {
+            if (!ok) {
+                r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
+            } else {
+                GlobalFrame f{a.data + off};
+                parse_frame(f, (uint32_t)((base + off) & 1u), len, a.opt_flags, a.ip_offset, r);
+            }
+        }
+        store_out<OUT>(a, idx, have, r);
+        return;
+    }
+    const uint64_t A0 = (base + lo) & ~15ull;
+    const uint32_t span = (uint32_t)(((base + hi + 15u) & ~15ull) - A0);
+    const uint32_t hr = (uint32_t)(base + off - A0);
+    const bool want_tail = have && len > kLaneWin;
+    const bool fast = have && ((base + off) & 3u) == 0 && !(a.opt_flags & NEXG_PARSE_FROM_IP);
+    uint32_t qa = 0, qb = 0, run = 0;
+    uint32_t w[20];
+#pragma unroll
+    for (int j = 0; j < 20; j++) w[j] = 0;
+
+    uint4 cur[CPT];
+    auto fetch = [&](uint32_t S) {
+#pragma unroll
+        for (uint32_t i = 0; i < CPT; i++) {
+            const uint32_t c = S + 16u * (t + 256u * i);
+            cur[i] = c < span ? load16<true>(reinterpret_cast<const void*>(A0 + c)) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    fetch(0);
+    uint32_t buf = 0;
+    for (uint32_t S = 0; S < span; S += SUB, buf = NB == 2 ? buf ^ 1u : 0u) {
+        uint8_t* sb = s_bytes[buf];
+        uint32_t* sp = s_pfx[buf];
+        uint32_t* st = s_tot[buf];
+        // (1) stage bytes; in-block exclusive prefixes and block totals in registers
+#pragma unroll
+        for (uint32_t i = 0; i < CPT; i++) {
+            const uint32_t c = t + 256u * i;
+            *reinterpret_cast<uint4*>(sb + 16u * c) = cur[i];
+            const uint32_t cs = chunk_le_sum(cur[i]);
+            const uint32_t inc = wave_incl_scan_dpp(cs);
+            sp[c] = inc - cs;
+            if (lane == 63u) st[4u * i + wv] = inc;
+        }
+        const uint32_t E = S + SUB;
+        if (E < span) fetch(E);
+        __syncthreads();
+        // (2) prefix values at this sub-tile's positions, head window copy
+        // (block totals re-read from LDS as broadcasts: no registers held)
+        const bool last = E >= span;
+        auto q_at = [&](uint32_t d) {  // d = position - S, 0 <= d <= SUB
+            const uint32_t c = d >> 4, m = d & 15u, b = c >> 6;
+            uint32_t q = run;
+#pragma unroll
+            for (uint32_t k = 0; k < NBLK; k += 4) {
+                const uint4 v = *reinterpret_cast<const uint4*>(st + k);
+                q += (k < b ? v.x : 0u) + (k + 1 < b ? v.y : 0u) + (k + 2 < b ? v.z : 0u) + (k + 3 < b ? v.w : 0u);
+            }
+            if (c < SUB / 16u) q += sp[c] + (m ? chunk_prefix_sum(sb + 16u * c, m) : 0u);
+            return q;
+        };
+        const uint32_t da = hr + kLaneWin - S, db = hr + len - S;  // wrap: < 0 -> huge
+        if (want_tail && (da < SUB || (last && da == SUB))) qa = q_at(da);
+        if (have && (db < SUB || (last && db == SUB))) qb = q_at(db);
+        const uint32_t dh = hr - S;
+        if (fast) {
+            if (dh <= SUB - kLaneWin) {  // whole window in this sub-tile (the usual case)
+#pragma unroll
+                for (int j = 0; j < 20; j++) w[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4u * j);
+            } else if (dh < SUB || dh + kLaneWin - 1u < kLaneWin - 1u) {  // straddles a sub-tile edge
+#pragma unroll
+                for (int j = 0; j < 20; j++) {
+                    const uint32_t d = dh + 4u * j;
+                    if (d < SUB) w[j] = *reinterpret_cast<const uint32_t*>(sb + d);
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < NBLK; k += 4) {
+            const uint4 v = *reinterpret_cast<const uint4*>(st + k);
+            run += v.x + v.y + v.z + v.w;
+        }
+        if (NB == 1) __syncthreads();
+    }
+    if (have) {
+        bool done = false;
+        if (fast) {
+#pragma unroll
+            for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
+            done = fast_canonical80(w, len, a.opt_flags, want_tail ? (uint32_t)(qb - qa) : 0u, r);
+        }
+        if (!done) {
+            GlobalFrame f{a.data + off};
+            parse_frame(f, (uint32_t)((base + off) & 1u), len, a.opt_flags, a.ip_offset, r);
+        }
+    }
+    if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
+    if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the (now idle) byte buffer
+        static_assert(OUT != NEXG_OUT_RECORD || NB * SUB >= kTile * 64u, "record staging needs 16 KiB");
+        uint8_t* stage = &s_bytes[0][0];
+        __syncthreads();  // NB = 2: the other buffer may still be read; NB = 1: already idle
         if (have) stage_record(stage + 64u * t, r);
         __syncthreads();
         copy_out_records<64>(stage, a.out, f0, nf);

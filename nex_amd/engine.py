@@ -55,6 +55,7 @@ class FrameBatch:
     stride: int = 0
     offsets: Optional[object] = None
     lengths: Optional[object] = None
+    hints: int = 0  # abi.FRAMES_* (nexg_frames.hints)
 
     def to_c(self):
         return abi.Frames(
@@ -62,7 +63,16 @@ class FrameBatch:
             data_bytes=self.data.numel(),
             offsets=None if self.offsets is None else self.offsets.data_ptr(),
             lengths=None if self.lengths is None else self.lengths.data_ptr(),
-            stride=self.stride, reserved=0, count=self.count)
+            stride=self.stride, hints=self.hints, count=self.count)
+
+    def frame_lengths(self):
+        """Host int64 array of every frame's length (the nexg_frames rules)."""
+        if self.lengths is not None:
+            return self.lengths[: self.count].cpu().numpy().astype(np.int64)
+        if self.offsets is not None:
+            o = self.offsets[: self.count + 1].cpu().numpy().astype(np.int64)
+            return np.diff(o)
+        return np.full(self.count, self.stride, np.int64)
 
     @property
     def total_bytes(self):
@@ -165,24 +175,66 @@ class Engine:
         out_kind=OUT_FLAGS, the nexg_desc.flags word alone (4 B), or with
         OUT_VERDICT its lossless 2-B form (abi.verdict_to_flags)."""
         torch = _torch()
-        width = {abi.OUT_DESC: 8, abi.OUT_RECORD: 64, abi.OUT_SLICE: 16, abi.OUT_FLAGS: 4,
-                 abi.OUT_VERDICT: 2}[out_kind]
+        nbytes = self.out_bytes(out_kind, batch.count)
         if out is None:
-            out = torch.empty(max(batch.count, 1) * width, dtype=torch.uint8, device=self.torch_device)
+            out = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=self.torch_device)
+        elif out.numel() * out.element_size() < nbytes or out.device != self.torch_device:
+            raise ValueError(f"out holds {out.numel() * out.element_size()} B on {out.device}; "
+                             f"{nbytes} B on {self.torch_device} needed")
         fr = batch.to_c()
         opt = abi.ParseOptionC(option.flags(mode), option.offset)
         self._check(self.lib.nexg_parse_batch(self.ctx, ctypes.byref(fr), ctypes.byref(opt), out_kind,
                                               _ptr(out), self._stream(stream)))
         return out
 
+    @staticmethod
+    def out_bytes(out_kind, count):
+        """Bytes of a nexg_parse_batch output of `out_kind` for `count` frames."""
+        if out_kind == abi.OUT_SPARSE:
+            return abi.sparse_bytes(count)
+        return count * {abi.OUT_DESC: 8, abi.OUT_RECORD: 64, abi.OUT_SLICE: 16, abi.OUT_FLAGS: 4,
+                        abi.OUT_VERDICT: 2}[out_kind]
+
     def parse_to_numpy(self, batch, option=ParseOption(), mode=ParseMode.Lenient,
                        out_kind=abi.OUT_RECORD):
+        """Host copy of the parse output; OUT_SPARSE comes back decoded on the
+        host into nexg_desc (abi.sparse_to_desc)."""
         out = self.parse(batch, option, mode, out_kind)
         _torch().cuda.synchronize(self.torch_device)
+        if out_kind == abi.OUT_SPARSE:
+            return abi.sparse_to_desc(out.cpu().numpy(), batch.count, batch.frame_lengths(),
+                                      option.flags(mode), option.offset)
         dt = {abi.OUT_DESC: abi.DESC_DTYPE, abi.OUT_RECORD: abi.RECORD_DTYPE,
               abi.OUT_SLICE: abi.SLICE_DTYPE, abi.OUT_FLAGS: abi.FLAGS_DTYPE,
               abi.OUT_VERDICT: abi.VERDICT_DTYPE}[out_kind]
         return out.cpu().numpy()[: batch.count * dt.itemsize].view(dt)
+
+    def sparse_expand(self, batch: FrameBatch, sparse, option: ParseOption = ParseOption(),
+                      mode: ParseMode = ParseMode.Lenient, out=None, stream=None):
+        """nexg_desc[count] (uint8 device tensor) from a NEXG_OUT_SPARSE output
+        of the same batch and option (nexg_sparse_expand)."""
+        torch = _torch()
+        if out is None:
+            out = torch.empty(max(batch.count, 1) * 8, dtype=torch.uint8, device=self.torch_device)
+        fr = batch.to_c()
+        opt = abi.ParseOptionC(option.flags(mode), option.offset)
+        self._check(self.lib.nexg_sparse_expand(self.ctx, ctypes.byref(fr), ctypes.byref(opt), _ptr(sparse),
+                                                _ptr(out), self._stream(stream)))
+        return out
+
+    def recompute_checksums(self, batch: FrameBatch, which: int = abi.FIX_IP | abi.FIX_L4,
+                            option: ParseOption = ParseOption(), report=True, stream=None):
+        """In-place checksum fix-up of batch.data with the mutable views'
+        raw-buffer semantics (nexg_recompute_checksums_batch; ipv4.rs:669-679,
+        udp.rs:338-369, tcp.rs:1009-1040, icmp.rs:372-377, icmpv6.rs:450-470).
+        Returns the nexg_fixup[count] report (uint8 device tensor) or None."""
+        torch = _torch()
+        out = torch.empty(max(batch.count, 1) * 8, dtype=torch.uint8, device=self.torch_device) if report else None
+        fr = batch.to_c()
+        opt = abi.ParseOptionC(option.flags(ParseMode.Lenient), option.offset)
+        self._check(self.lib.nexg_recompute_checksums_batch(self.ctx, ctypes.byref(fr), ctypes.byref(opt), which,
+                                                            _ptr(out), self._stream(stream)))
+        return out
 
     def decode_options(self, batch: FrameBatch, records, stream=None):
         """Ipv4Header.options / TcpHeader.options of every frame as positions

@@ -1264,3 +1264,127 @@ void nexo_gen_udp4_params(uint64_t seed, uint64_t index, uint32_t* src_ip,
     *dport = (uint16_t)(r1 >> 16);
     *ip_id = (uint16_t)(r1 >> 32);
 }
+
+/* ---- mutable views: recompute_checksum chained as
+ * examples/mutable_chaining.rs:19-63 (include/nexg.h nexg_recompute_checksums_batch).
+ * Each view is constructed with its MutablePacket::new validation over the
+ * enclosing view's payload_mut slice; recompute_checksum sums that view's
+ * whole raw buffer. */
+
+/* MutableIpv4Packet::new (ipv4.rs:540-566) */
+static int mut_ipv4_new(const uint8_t* b, size_t len) {
+    if (len < 20) return 0;
+    size_t ihl = b[0] & 0x0F;
+    if (ihl < 5) return 0;
+    size_t header_len = ihl * 4;
+    if (header_len > len) return 0;
+    size_t total_len = be16(b + 2);
+    if (total_len != 0 && total_len < header_len) return 0;
+    return 1;
+}
+/* MutableIpv4Packet::header_len / total_len / payload_len (ipv4.rs:682-704) */
+static size_t mut_ipv4_header_len(const uint8_t* b, size_t len) {
+    size_t hl = (size_t)(b[0] & 0x0F) * 4;
+    if (hl < 20) hl = 20;
+    return hl < len ? hl : len;
+}
+static size_t mut_ipv4_total_len(const uint8_t* b, size_t len) {
+    size_t total = be16(b + 2);
+    return total == 0 ? len : (total < len ? total : len);
+}
+/* MutableUdpPacket::new (udp.rs:101-121) */
+static int mut_udp_new(const uint8_t* b, size_t len) {
+    if (len < 8) return 0;
+    uint16_t length = be16(b + 4);
+    if (length != 0) {
+        if (length < 8) return 0;
+        if (length > len) return 0;
+    }
+    return 1;
+}
+/* MutableTcpPacket::new (tcp.rs:857-876) */
+static int mut_tcp_new(const uint8_t* b, size_t len) {
+    if (len < 20) return 0;
+    uint8_t data_offset = b[12] >> 4;
+    if (data_offset < 5) return 0;
+    if ((size_t)data_offset * 4 > len) return 0;
+    return 1;
+}
+
+void nexo_recompute_frame(uint8_t* frame, size_t len, uint32_t flags, uint32_t ip_offset, uint32_t which,
+                          nexg_fixup* out) {
+    nexg_fixup fx;
+    memset(&fx, 0, sizeof(fx));
+    uint8_t* ip;
+    size_t n;
+    int family = 0;
+    if (flags & NEXG_PARSE_FROM_IP) {
+        if (ip_offset >= len) goto done;
+        ip = frame + ip_offset;
+        n = len - ip_offset;
+        family = (ip[0] >> 4) == 4 ? 4 : ((ip[0] >> 4) == 6 ? 6 : 0);
+    } else {
+        if (len < 14) goto done; /* MutableEthernetPacket::new (ethernet.rs:355-361) */
+        ip = frame + 14;         /* payload_mut (ethernet.rs:384-387) */
+        n = len - 14;
+        uint16_t et = be16(frame + 12);
+        family = et == 0x0800 ? 4 : (et == 0x86DD ? 6 : 0);
+    }
+    uint8_t* pay = NULL;
+    size_t plen = 0;
+    uint8_t proto = 0;
+    if (family == 4) {
+        if (!mut_ipv4_new(ip, n)) goto done;
+        size_t hl = mut_ipv4_header_len(ip, n);
+        if (which & NEXG_FIX_IP) { /* recompute_checksum (ipv4.rs:669-679) */
+            if (hl <= n) {
+                uint16_t c = nexo_checksum(ip, hl, 5);
+                put16(ip + 10, c);
+                fx.done |= NEXG_FIX_IP;
+                fx.ip_csum = c;
+            }
+        }
+        size_t total = mut_ipv4_total_len(ip, n);
+        pay = ip + hl; /* payload_mut (ipv4.rs:591-596) */
+        plen = total > hl ? total - hl : 0;
+        proto = ip[9];
+        if (!(proto == 17 || proto == 6 || proto == 1)) goto done;
+    } else if (family == 6) {
+        if (n < 40) goto done; /* MutableIpv6Packet::new (ipv6.rs:394-400) */
+        pay = ip + 40;         /* payload_mut (ipv6.rs:423-426) */
+        plen = n - 40;
+        proto = ip[6];
+        if (!(proto == 17 || proto == 6 || proto == 58)) goto done;
+    } else {
+        goto done;
+    }
+    if (!(which & NEXG_FIX_L4)) goto done;
+    uint16_t c;
+    size_t csum_at;
+    if (proto == 17) { /* udp.rs:338-369 */
+        if (!mut_udp_new(pay, plen)) goto done;
+        c = family == 4 ? nexo_ipv4_checksum(pay, plen, 3, NULL, 0, ip + 12, ip + 16, 17)
+                        : nexo_ipv6_checksum(pay, plen, 3, NULL, 0, ip + 8, ip + 24, 17);
+        csum_at = 6;
+    } else if (proto == 6) { /* tcp.rs:1009-1040 */
+        if (!mut_tcp_new(pay, plen)) goto done;
+        c = family == 4 ? nexo_ipv4_checksum(pay, plen, 8, NULL, 0, ip + 12, ip + 16, 6)
+                        : nexo_ipv6_checksum(pay, plen, 8, NULL, 0, ip + 8, ip + 24, 6);
+        csum_at = 16;
+    } else if (proto == 1) { /* icmp.rs:372-377; IcmpPacket::from_buf needs 8 B */
+        if (plen < 8) goto done;
+        c = nexo_checksum(pay, plen, 1);
+        csum_at = 2;
+    } else { /* icmpv6.rs:450-470 */
+        if (plen < 8) goto done;
+        c = nexo_ipv6_checksum(pay, plen, 1, NULL, 0, ip + 8, ip + 24, 58);
+        csum_at = 2;
+    }
+    put16(pay + csum_at, c);
+    fx.done |= NEXG_FIX_L4;
+    fx.proto = proto;
+    fx.l4_csum = c;
+    fx.l4_off = (uint16_t)(pay - frame);
+done:
+    if (out) *out = fx;
+}

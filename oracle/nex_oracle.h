@@ -100,6 +100,11 @@ int nexo_build_udp6(const uint8_t src_mac[6], const uint8_t dst_mac[6],
                     uint32_t flow_label, const uint8_t* payload, uint32_t payload_len,
                     uint8_t* out);
 
+/* nexg_recompute_checksums_batch's semantics for one frame, in place: the
+ * mutable views' recompute_checksum chained as mutable_chaining.rs:19-63. */
+void nexo_recompute_frame(uint8_t* frame, size_t len, uint32_t flags, uint32_t ip_offset, uint32_t which,
+                          nexg_fixup* out);
+
 /* Synthetic workloads, independent CPU implementation
  * of the generator the engine ships (nexg_gen_*). */
 uint32_t nexo_gen_length(int workload, uint64_t seed, uint64_t index);

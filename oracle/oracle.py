@@ -62,6 +62,8 @@ def lib():
         L.nexo_build_udp6.restype = I
         L.nexo_build_udp6.argtypes = [P, P, P, P, U16, U16, ctypes.c_uint8, ctypes.c_uint8, U32, P,
                                       U32, P]
+        L.nexo_recompute_frame.restype = None
+        L.nexo_recompute_frame.argtypes = [P, S, U32, U32, U32, P]
         L.nexo_gen_length.restype = U32
         L.nexo_gen_length.argtypes = [I, U64, U64]
         L.nexo_gen_frame.restype = None
@@ -225,6 +227,15 @@ def build_icmp_echo(spec, icmp_type, code, ident, seqno, payload=b""):
     if n < 0:
         raise ValueError("BuildError::LengthOverflow")
     return out.raw[:n]
+
+
+def recompute_frame(frame: bytes, which=abi.FIX_IP | abi.FIX_L4, flags=0, ip_offset=0):
+    """(fixed frame bytes, nexg_fixup) — the mutable views' recompute_checksum
+    chained as examples/mutable_chaining.rs does (nexo_recompute_frame)."""
+    buf, n = _buf(frame)
+    out = np.zeros(1, abi.FIXUP_DTYPE)
+    lib().nexo_recompute_frame(buf, n, flags, ip_offset, which, out.ctypes.data)
+    return buf.raw[:n], out[0]
 
 
 def gen_length(workload, index, seed=abi.DEFAULT_SEED):

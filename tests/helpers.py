@@ -23,8 +23,20 @@ def golden():
         return json.load(f)
 
 
-def check_expect(rec, frame: bytes, exp: dict, name=""):
-    """Assert a record satisfies a reference-test expectation dict."""
+def rfc1071(data: bytes) -> int:
+    """Independent Internet checksum (RFC 1071) of `data` (pure Python)."""
+    if len(data) % 2:
+        data += b"\0"
+    s = sum(int.from_bytes(data[i:i + 2], "big") for i in range(0, len(data), 2))
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return ~s & 0xFFFF
+
+
+def check_expect(rec, frame: bytes, exp: dict, name="", reparse=None, parse_flags=0, ip_offset=0):
+    """Assert a record satisfies a reference-test expectation dict.
+    `reparse(frame) -> record` re-parses a modified frame (default: the
+    oracle; GPU tests pass the engine)."""
     flags = int(rec["flags"])
     if "status" in exp:
         assert (flags >> abi.STATUS_SHIFT) & 7 == exp["status"], name
@@ -51,7 +63,22 @@ def check_expect(rec, frame: bytes, exp: dict, name=""):
             e = fr.datalink.ethernet
             assert (e.destination if k == "eth_dst" else e.source).hex() == v, name
         elif k == "ip_csum_consistent":
-            assert int(rec["ip_csum_calc"]) != 0 or int(rec["ip_csum"]) == 0, name
+            # ipv4.rs:1073-1095: the computed checksum written back into bytes
+            # 10..11 makes a packet whose header verifies and whose bytes are
+            # raw_copy; the value itself is an independent RFC 1071 sum.
+            assert int(rec["flags"]) & abi.C_IP_CHECKED, name
+            calc, l3 = int(rec["ip_csum_calc"]), int(rec["l3_off"])
+            hl = (int(rec["ip_ver_ihl"]) & 15) * 4
+            hdr = frame[l3:l3 + 10] + b"\0\0" + frame[l3 + 12:l3 + hl]
+            assert calc == rfc1071(hdr), (name, hex(calc), hex(rfc1071(hdr)))
+            raw_copy = frame[:l3 + 10] + calc.to_bytes(2, "big") + frame[l3 + 12:]
+            if reparse is None:
+                from oracle import oracle
+                r2 = oracle.parse_frame(raw_copy, parse_flags, ip_offset)
+            else:
+                r2 = reparse(raw_copy)
+            assert int(r2["flags"]) & abi.C_IP_OK, name
+            assert int(r2["ip_csum"]) == calc == int(r2["ip_csum_calc"]), name
         else:
             assert int(rec[k]) == v, (name, k, int(rec[k]), v)
 

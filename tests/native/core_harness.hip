@@ -99,3 +99,38 @@ extern "C" int harness_slice(const uint8_t* data, uint64_t data_bytes, const uin
     }
     return 0;
 }
+
+// NEXG_OUT_SPARSE on the host: the kernels' encoder (sparse_encode) over
+// records, and both decoders (the kernels' sparse_decode and the C header's
+// nexg_sparse_decode) back into descriptors. out_desc[i].flags = 0xFFFFFFFF
+// marks an exception code (code 0), which neither decoder resolves.
+extern "C" int harness_sparse(const nexg_record* recs, uint64_t count, uint32_t flags, uint32_t ip_offset,
+                              uint8_t* codes, nexg_desc* dev_desc, nexg_desc* hdr_desc) {
+    for (uint64_t i = 0; i < count; i++) {
+        const uint32_t c = nexg::sparse_encode(recs[i], flags, ip_offset);
+        codes[i] = (uint8_t)c;
+        const uint32_t len = recs[i].packet_len;
+        nexg_desc d{0xFFFFFFFFu, 0, 0}, h{0xFFFFFFFFu, 0, 0};
+        if (c) {
+            if (!nexg::sparse_decode(c, len, flags, ip_offset, d)) return -1;
+            if (!nexg_sparse_decode((uint8_t)c, len, flags, ip_offset, &h)) return -1;
+        }
+        dev_desc[i] = d;
+        hdr_desc[i] = h;
+    }
+    return 0;
+}
+
+// both decoders on arbitrary (code, length) pairs; flags 0xFFFFFFFF = exception
+extern "C" int harness_sparse_decode(const uint8_t* codes, const uint32_t* lens, uint64_t count, uint32_t flags,
+                                     uint32_t ip_offset, nexg_desc* dev_desc, nexg_desc* hdr_desc) {
+    for (uint64_t i = 0; i < count; i++) {
+        nexg_desc d{0xFFFFFFFFu, 0, 0}, h{0xFFFFFFFFu, 0, 0};
+        const bool a = nexg::sparse_decode(codes[i], lens[i], flags, ip_offset, d);
+        const bool b = nexg_sparse_decode(codes[i], lens[i], flags, ip_offset, &h) != 0;
+        if (a != b) return -1;
+        dev_desc[i] = d;
+        hdr_desc[i] = h;
+    }
+    return 0;
+}

@@ -20,6 +20,10 @@ def lib():
         P, U32, U64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
         L.harness_parse.restype = ctypes.c_int
         L.harness_parse.argtypes = [P, U64, P, P, U32, U64, U32, U32, U32, ctypes.c_int, P]
+        L.harness_sparse.restype = ctypes.c_int
+        L.harness_sparse.argtypes = [P, U64, U32, U32, P, P, P]
+        L.harness_sparse_decode.restype = ctypes.c_int
+        L.harness_sparse_decode.argtypes = [P, P, U64, U32, U32, P, P]
         L.harness_slice.restype = ctypes.c_int
         L.harness_slice.argtypes = [P, U64, P, P, U32, U64, U32, U32, U32, P]
         _lib = L
@@ -53,3 +57,32 @@ def slice_packed(data, offsets=None, lengths=None, stride=0, flags=0, ip_offset=
                         None if lens is None else lens.ctypes.data, stride, count, flags,
                         ip_offset, window, out.ctypes.data)
     return out
+
+
+def sparse(recs, flags=0, ip_offset=0):
+    """(codes, device-decoder descs, header-decoder descs) of the kernels'
+    NEXG_OUT_SPARSE encoder run on the host over `recs`."""
+    import numpy as np
+    from nex_amd import abi
+    recs = np.ascontiguousarray(recs)
+    n = len(recs)
+    codes = np.zeros(max(n, 1), np.uint8)
+    dd = np.zeros(max(n, 1), abi.DESC_DTYPE)
+    hd = np.zeros(max(n, 1), abi.DESC_DTYPE)
+    assert lib().harness_sparse(recs.ctypes.data, n, flags, ip_offset, codes.ctypes.data, dd.ctypes.data,
+                                hd.ctypes.data) == 0
+    return codes[:n], dd[:n], hd[:n]
+
+
+def sparse_decode(codes, lens, flags=0, ip_offset=0):
+    """(kernels' decoder, C header decoder) descriptors of (code, length) pairs."""
+    import numpy as np
+    from nex_amd import abi
+    codes = np.ascontiguousarray(codes, np.uint8)
+    lens = np.ascontiguousarray(lens, np.uint32)
+    n = len(codes)
+    dd = np.zeros(max(n, 1), abi.DESC_DTYPE)
+    hd = np.zeros(max(n, 1), abi.DESC_DTYPE)
+    assert lib().harness_sparse_decode(codes.ctypes.data, lens.ctypes.data, n, flags, ip_offset,
+                                       dd.ctypes.data, hd.ctypes.data) == 0
+    return dd[:n], hd[:n]

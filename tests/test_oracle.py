@@ -49,7 +49,7 @@ def test_icmpv6_checksum_kat(oracle):
 def test_golden_frames(oracle, v):
     fr = bytes.fromhex(v["frame"])
     rec = oracle.parse_frame(fr, v["parse_flags"], v["ip_offset"])
-    helpers.check_expect(rec, fr, v["expect"], v["name"])
+    helpers.check_expect(rec, fr, v["expect"], v["name"], parse_flags=v["parse_flags"], ip_offset=v["ip_offset"])
 
 
 def test_survey_crosscheck_values(oracle):

@@ -216,6 +216,14 @@ int main(int argc, char** argv) {
     vars.push_back({"prod_fast", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, true, false>), count * 64.0});
     vars.push_back({"prod_fast_nt", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, true, true>), count * 64.0});
     vars.push_back({"flags_fast_nt", parse(k_parse<0, NEXG_OUT_FLAGS, 64, 64, true, true>), count * 64.0});
+    vars.push_back({"verdict_fast_nt", parse(k_parse<0, NEXG_OUT_VERDICT, 64, 64, true, true>), count * 64.0});
+    uint8_t* sparse_out;
+    CK(hipMalloc(&sparse_out, NEXG_SPARSE_BYTES(count)));
+    {
+        ParseArgs sa = a;
+        sa.out = sparse_out;
+        vars.push_back({"sparse_fast_nt", [=]() { hipLaunchKernelGGL((k_parse<0, NEXG_OUT_SPARSE, 64, 64, true, true>), grid, blk, 0, 0, sa); }, count * 64.0});
+    }
     vars.push_back({"prod_generic", parse(k_parse<0, NEXG_OUT_DESC, 64, 64, false, false>), count * 64.0});
     vars.push_back({"span_udp64_nb2", parse(k_parse_span<NEXG_OUT_DESC, 2>), count * 64.0});
     vars.push_back({"span_udp64_nb1", parse(k_parse_span<NEXG_OUT_DESC, 1>), count * 64.0});
@@ -241,6 +249,19 @@ int main(int argc, char** argv) {
         uint64_t bad = 0;
         for (uint64_t i = 0; i < count; i++) bad += memcmp(&h_out[i], &h_ref[i], 8) != 0;
         printf("check %-20s mismatches=%llu\n", v.name.c_str(), (unsigned long long)bad);
+    }
+    {  // sparse codes expand (nexg_sparse_expand) to exactly the product descriptors
+        CK(hipMemset(out, 0, count * 8));
+        ParseArgs sa = a;
+        sa.out = sparse_out;
+        hipLaunchKernelGGL((k_parse<0, NEXG_OUT_SPARSE, 64, 64, true, true>), grid, blk, 0, 0, sa);
+        nexg_frames fr{data, count * 64, nullptr, nullptr, 64, 0, count};
+        if (nexg_sparse_expand(ctx, &fr, nullptr, sparse_out, reinterpret_cast<nexg_desc*>(out), nullptr) != 0) return 1;
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h_out.data(), out, count * 8, hipMemcpyDeviceToHost));
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < count; i++) bad += memcmp(&h_out[i], &h_ref[i], 8) != 0;
+        printf("check %-20s mismatches=%llu\n", "sparse_fast_nt", (unsigned long long)bad);
     }
     // ---- IMIX (offset table) ----
     const uint64_t icount = count;
@@ -269,6 +290,18 @@ int main(int argc, char** argv) {
     ivars.push_back({"imix_span_nb2", iparse(k_parse_span<NEXG_OUT_DESC, 2>), ibytes});
     ivars.push_back({"imix_flags_span_nb1", iparse(k_parse_span<NEXG_OUT_FLAGS, 1>), ibytes});
     ivars.push_back({"imix_span_nb1", iparse(k_parse_span<NEXG_OUT_DESC, 1>), ibytes});
+    ivars.push_back({"imix_span2_16k", iparse(k_parse_span2<NEXG_OUT_DESC, 16384, 1>), ibytes});
+    ivars.push_back({"imix_span2_16k_w6", iparse(k_parse_span2<NEXG_OUT_DESC, 16384, 1, 6>), ibytes});
+    ivars.push_back({"imix_span2_8k_nb2", iparse(k_parse_span2<NEXG_OUT_DESC, 8192, 2>), ibytes});
+    ivars.push_back({"imix_span2_8k_nb1", iparse(k_parse_span2<NEXG_OUT_DESC, 8192, 1>), ibytes});
+    ivars.push_back({"imix_span2_12k_nb1", iparse(k_parse_span2<NEXG_OUT_DESC, 12288, 1>), ibytes});
+    {
+        ParseArgs sa = ia;
+        sa.out = sparse_out;
+        ivars.push_back({"imix_sparse_span2_16k", [=]() { hipLaunchKernelGGL((k_parse_span2<NEXG_OUT_SPARSE, 16384, 1>), grid, blk, 0, 0, sa); }, ibytes});
+        ivars.push_back({"imix_sparse_span2_8k_nb2", [=]() { hipLaunchKernelGGL((k_parse_span2<NEXG_OUT_SPARSE, 8192, 2>), grid, blk, 0, 0, sa); }, ibytes});
+        ivars.push_back({"imix_sparse_span_v1", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1>), grid, blk, 0, 0, sa); }, ibytes});
+    }
     ivars.push_back({"imix_span_nb1_8k", iparse(k_parse_span<NEXG_OUT_DESC, 1, 8192>), ibytes});
     ivars.push_back({"imix_span_nb2_8k", iparse(k_parse_span<NEXG_OUT_DESC, 2, 8192>), ibytes});
     ivars.push_back({"imix_span_nb1_32k", iparse(k_parse_span<NEXG_OUT_DESC, 1, 32768>), ibytes});
@@ -287,8 +320,15 @@ int main(int argc, char** argv) {
     for (auto& v : ivars) {
         if (v.name.rfind("ABL", 0) == 0 || v.name.rfind("udp64", 0) == 0 || v.name.find("_rec") != std::string::npos ||
             v.name.find("flags") != std::string::npos) continue;
-        CK(hipMemset(out, 0, count * 8));
-        v.run();
+        if (v.name.find("sparse") != std::string::npos) {  // codes -> nexg_sparse_expand -> descriptors
+            nexg_frames fr{idata, ho[icount], ioff, nullptr, 0, 0, icount};
+            CK(hipMemset(out, 0, count * 8));
+            v.run();
+            if (nexg_sparse_expand(ctx, &fr, nullptr, sparse_out, reinterpret_cast<nexg_desc*>(out), nullptr) != 0) return 1;
+        } else {
+            CK(hipMemset(out, 0, count * 8));
+            v.run();
+        }
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(h_out.data(), out, count * 8, hipMemcpyDeviceToHost));
         uint64_t bad = 0;
