@@ -327,7 +327,8 @@ int nexg_pcap_read_batch(nexg_pcap* p, uint8_t* data, uint64_t data_cap, uint64_
             p->bpos += used;
             continue;
         }
-        if (r.caplen > 65535u) return set_err(p, NEXG_ERANGE, "record longer than 65535 bytes");
+        // a record longer than 65535 B (loopback / GRO captures) passes through:
+        // the parse kernels report it per frame as NEXG_ERR_BAD_EXTENT
         if (pos + r.caplen > data_cap) {
             if (n == 0) return set_err(p, NEXG_ERANGE, "data_cap smaller than one record");
             break;
@@ -383,8 +384,7 @@ int nexg_pcap_read_raw(nexg_pcap* p, uint8_t* buf, uint64_t cap, uint64_t* offse
             if (n) break;
             return rc;
         }
-        if (rc == 1) {
-            if (r.caplen > 65535u) return set_err(p, NEXG_ERANGE, "record longer than 65535 bytes");
+        if (rc == 1) {  // > 65535 B passes through (NEXG_ERR_BAD_EXTENT in the parse)
             offsets[n] = pos + r.data;
             lengths[n] = r.caplen;
             if (ts_ns) ts_ns[n] = r.ts_ns;
@@ -393,12 +393,12 @@ int nexg_pcap_read_raw(nexg_pcap* p, uint8_t* buf, uint64_t cap, uint64_t* offse
         pos += used;
     }
     if (pos < have) {  // an incomplete record, or records past max_frames: next call
-        if (n == 0 && pos == 0) {
-            if (p->file_eof && p->carry.empty())
-                return p->fatal = set_err(p, NEXG_EINVAL, "truncated capture file");
-            return set_err(p, NEXG_ERANGE, "buffer smaller than one record");
-        }
+        if (n == 0 && pos == 0 && p->file_eof && p->carry.empty() && have < cap)
+            return p->fatal = set_err(p, NEXG_EINVAL, "truncated capture file");
+        // every byte not described goes back in front of the carry, so a retry
+        // (e.g. with a larger buffer after NEXG_ERANGE) resumes at this record
         p->carry.insert(p->carry.begin(), buf + pos, buf + have);
+        if (n == 0 && pos == 0) return set_err(p, NEXG_ERANGE, "buffer smaller than one record");
     }
     *n_frames = n;
     *bytes_used = pos;

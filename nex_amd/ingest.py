@@ -140,3 +140,30 @@ def device_batches(reader: PcapReader, max_frames: int = 1 << 20, data_cap: int 
             o = offs[: n + 1].to(device, non_blocking=True)
         s.synchronize()  # the pinned staging buffers are reused by the next read
         yield FrameBatch(data=d[:nbytes], count=n, offsets=o)
+
+
+def device_raw_batches(reader: PcapReader, max_frames: int = 1 << 20, cap: int = 1 << 28,
+                       device="cuda", stream=None):
+    """Yield FrameBatch objects in the in-place shape (nexg_pcap_read_raw):
+    the file bytes themselves go H2D, frames are described by offsets +
+    lengths with the record headers left in place. The batch carries
+    NEXG_FRAMES_MONOTONE (records are in file order), so the parse streams each
+    256-frame group as one span through the gaps instead of the two-pass
+    explicit-length kernels (include/nexg.h)."""
+    import torch
+    from .engine import FrameBatch
+    buf = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+    offs = torch.empty(max_frames, dtype=torch.int64, pin_memory=True)
+    lens = torch.empty(max_frames, dtype=torch.int32, pin_memory=True)
+    bnp, onp, lnp = buf.numpy(), offs.numpy().view(np.uint64), lens.numpy().view(np.uint32)
+    while True:
+        n, used = reader.read_raw_into(bnp, onp, lnp)
+        if n == 0 and used == 0:
+            return
+        s = stream or torch.cuda.current_stream()
+        with torch.cuda.stream(s):
+            d = buf[:max(used, 1)].to(device, non_blocking=True)
+            o = offs[:max(n, 1)].to(device, non_blocking=True)
+            ln = lens[:max(n, 1)].to(device, non_blocking=True)
+        s.synchronize()  # the pinned staging buffers are reused by the next read
+        yield FrameBatch(data=d[:used], count=n, offsets=o[:n], lengths=ln[:n], hints=abi.FRAMES_MONOTONE)

@@ -211,3 +211,49 @@ def test_raw_shape_parallel_reads(tmp_path, frames, threads):
     with PcapReader(path) as r:
         with pytest.raises(PcapError):
             r.set_read_threads(0)
+
+
+def test_oversized_record_passes_through(tmp_path, frames):
+    """A legal record longer than 65535 B (loopback / GRO captures) in the
+    middle of a file: both shapes deliver every frame in order, the big one
+    included (the parse kernels flag it NEXG_ERR_BAD_EXTENT), and the reader
+    never gets stuck (it used to fail every later call)."""
+    from nex_amd.ingest import raw_frames
+    big = bytes(range(256)) * 274  # 70144 B
+    fr = frames[:20] + [big] + frames[20:40]
+    for name, blob in (("classic", pcapfile.classic(fr)),
+                       ("ng", pcapfile.ng_shb() + pcapfile.ng_idb(1) + b"".join(pcapfile.ng_epb(f, i)
+                                                                               for i, f in enumerate(fr)))):
+        path = _write(tmp_path, name, blob)
+        with PcapReader(path) as r:
+            assert list(r.frames(max_frames=7, data_cap=1 << 20)) == fr, name
+        with PcapReader(path) as r:
+            assert list(raw_frames(r, cap=1 << 20, max_frames=5)) == fr, name
+
+
+def test_raw_retry_after_erange_resumes(tmp_path, frames):
+    """read_raw with a buffer smaller than the next record returns ERANGE and
+    keeps every byte it took (carry + file): retrying with a larger buffer
+    yields exactly the frames one large read gives."""
+    fr = frames[:30] + [frames[-1]] + frames[30:50]  # a 9000-B record in the middle
+    path = _write(tmp_path, "r.pcap", pcapfile.classic(fr))
+    got = []
+    with PcapReader(path) as r:
+        small = np.empty(4096, np.uint8)
+        big = np.empty(1 << 20, np.uint8)
+        offs = np.empty(64, np.uint64)
+        lens = np.empty(64, np.uint32)
+        errors = 0
+        while True:
+            try:
+                n, used = r.read_raw_into(small, offs, lens)
+                buf = small
+            except PcapError:
+                errors += 1
+                n, used = r.read_raw_into(big, offs, lens)
+                buf = big
+            if n == 0 and used == 0:
+                break
+            got += [bytes(buf[int(offs[k]):int(offs[k]) + int(lens[k])]) for k in range(n)]
+        assert errors >= 1
+    assert got == fr

@@ -155,7 +155,10 @@ def main():
             free[k].release()
             comp_s.wait_event(ev)
             if args.shape == "raw":
-                fb = FrameBatch(data=dev[k][:nb], count=n, offsets=doff[k][:n], lengths=dlen[k][:n])
+                # records in file order with their headers in place: one ordered span per
+                # group (NEXG_FRAMES_MONOTONE routes to the span kernel, gaps read through)
+                fb = FrameBatch(data=dev[k][:nb], count=n, offsets=doff[k][:n], lengths=dlen[k][:n],
+                                hints=abi.FRAMES_MONOTONE)
             else:
                 fb = FrameBatch(data=dev[k][:nb], count=n, offsets=doff[k][: n + 1])
             eng.parse(fb, out_kind=abi.OUT_DESC, out=out[first * 8:(first + n) * 8], stream=comp_s)
