@@ -92,29 +92,18 @@ def load_traffic(workload, out_kind):
 
 def timed(step, steps, warmup, stream, device, host_clock=False):
     """W untimed steps, then exactly K steps bracketed by barrier + sync on
-    both sides. Returns (max-over-ranks elapsed seconds, per-launch kernel
-    seconds from HIP events on the launch stream)."""
+    both sides (nex_amd.dist.timed_steps). Returns (max-over-ranks elapsed
+    seconds, per-launch kernel seconds from HIP events on the launch stream)."""
     import torch
     from nex_amd import dist
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize(device)
-    dist.barrier(device)
-    torch.cuda.synchronize(device)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(device)
-    t1 = time.perf_counter()
-    dist.barrier(device)
-    elapsed = dist.max_over_ranks(t1 - t0, device)
+    elapsed, local = dist.timed_steps(step, steps, warmup, sync=lambda: torch.cuda.synchronize(device),
+                                      device=device, before=lambda: ev0.record(stream),
+                                      after=lambda: ev1.record(stream))
     kernel_s = ev0.elapsed_time(ev1) / 1e3 / steps
     if host_clock:  # copies + kernels on side streams: the host clock is the measure
-        kernel_s = (t1 - t0) / steps
+        kernel_s = local / steps
     return elapsed, kernel_s
 
 
@@ -161,16 +150,14 @@ def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
     steps = max(1, args.steps // 2)
     elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
                               steps, max(20, args.warmup), stream, device)
-    frames = dist.sum_over_ranks(F, device) * steps
-    nbytes = dist.sum_over_ranks(alg, device) * steps
+    tp = dist.throughput(F, alg, steps, elapsed, device)
     if rank != 0:
         return None
     ach = alg / kernel_s / 1e9
     r = {"workload": f"configs[2]: {F} IMIX frames per GPU (64/576/1500 at 7:4:1, "
                      "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table; " + OUT_NOTE[args.out],
-         "value": round(frames / elapsed / 1e6, 2), "unit": "Mpkt/s", "steps": steps,
-         "ms_per_step": round(elapsed / steps * 1e3, 4),
-         "gib_s": round(nbytes / elapsed / 2**30, 2), "bytes_per_gpu": alg,
+         "value": tp["value"], "unit": "Mpkt/s", "steps": steps, "ms_per_step": tp["ms_per_step"],
+         "gib_s": tp["gib_s"], "bytes_per_gpu": alg,
          "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("imix", args.out),
                       "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg}}
@@ -210,7 +197,7 @@ def main():
         log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    dist.init("nccl")
+    dist.init()  # RCCL when this process has a GPU, gloo otherwise
     eng = Engine(local)
     F = args.frames
     first = rank * F
@@ -294,8 +281,7 @@ def main():
 
     warm = max(args.warmup, 20) if args.workload == "imix" and not args.e2e else args.warmup  # see imix_line
     elapsed, kernel_s = timed(step, args.steps, warm, stream, device, host_clock=args.e2e)
-    total_frames = dist.sum_over_ranks(F, device) * args.steps
-    total_bytes = dist.sum_over_ranks(alg_bytes, device) * args.steps
+    tp = dist.throughput(F, alg_bytes, args.steps, elapsed, device)
     ceilings = None
     if args.workload == "udp64" and not args.e2e and not args.no_imix:
         ceilings = stream_ceilings(eng, batch, args, stream, device)
@@ -309,19 +295,19 @@ def main():
     traffic = load_traffic(args.workload, args.out)
     res = {
         "metric": METRIC if args.workload != "ser" else "Mpkt/s build+checksum udp_ping-shape frames",
-        "value": round(total_frames / elapsed / 1e6, 2),
+        "value": tp["value"],
         "unit": "Mpkt/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": tp["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: SURVEY.md App. C generator (splitmix64, seed 0x6E6578), generated on device",
         "config": cfg,
-        "gib_s": round(total_bytes / elapsed / 2**30, 2),
+        "gib_s": tp["gib_s"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,

@@ -18,14 +18,62 @@ def shard(total: int, rank: int, world: int):
     return begin, end
 
 
-def init(backend: str):
+def pick_backend() -> str:
+    """RCCL ("nccl" on ROCm) when this process has a GPU, gloo otherwise.
+    Only the timing barrier and two scalar reductions ever use it."""
+    import torch
+    import torch.distributed as dist
+    if torch.cuda.is_available() and dist.is_nccl_available():
+        return "nccl"
+    return "gloo"
+
+
+def init(backend: str = None):
     import torch.distributed as dist
     rank, world, _ = env_rank_world()
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+        dist.init_process_group(backend=backend or pick_backend(), rank=rank, world_size=world)
     return rank, world
+
+
+def timed_steps(step, steps: int, warmup: int, sync=None, device=None, before=None, after=None):
+    """bench.py's timing discipline: `warmup` untimed steps, then exactly
+    `steps` steps bracketed by sync + barrier + sync on both sides; returns
+    (max-over-ranks elapsed seconds, this rank's elapsed seconds). `sync`
+    waits for this rank's device work (torch.cuda.synchronize on a GPU);
+    before/after run inside the timed bracket around the steps (HIP event
+    records)."""
+    import time
+    sync = sync or (lambda: None)
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier(device)
+    sync()
+    t0 = time.perf_counter()
+    if before:
+        before()
+    for _ in range(steps):
+        step()
+    if after:
+        after()
+    sync()
+    t1 = time.perf_counter()
+    barrier(device)
+    return max_over_ranks(t1 - t0, device), t1 - t0
+
+
+def throughput(frames_per_rank: int, bytes_per_rank: int, steps: int, elapsed_max: float, device=None):
+    """Whole-job numbers of a weak-scaling run: every rank processed its own
+    shard `steps` times; value = frames over all ranks / MAX elapsed."""
+    total_frames = sum_over_ranks(frames_per_rank, device) * steps
+    total_bytes = sum_over_ranks(bytes_per_rank, device) * steps
+    return {"value": round(total_frames / elapsed_max / 1e6, 2), "unit": "Mpkt/s",
+            "ms_per_step": round(elapsed_max / steps * 1e3, 4),
+            "gib_s": round(total_bytes / elapsed_max / 2**30, 2),
+            "total_frames": total_frames, "total_bytes": total_bytes}
 
 
 def barrier(device=None):

@@ -62,3 +62,46 @@ def test_shard_covers_range():
             spans = [dist.shard(total, r, world) for r in range(world)]
             assert spans[0][0] == 0 and spans[-1][1] == total
             assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+def _bench_worker(rank, world, port, q):
+    """bench.py's multi-rank leg with a stub step: dist.timed_steps (barriers,
+    MAX over ranks) + dist.throughput (SUM over ranks), the functions
+    bench.py's timed() / main() call, on gloo."""
+    import time
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as tdist
+    assert dist.pick_backend() == "gloo"  # no GPU in this process
+    dist.init()
+    calls = []
+    step = lambda: (calls.append(1), time.sleep(0.002 * (rank + 1)))
+    elapsed_max, local = dist.timed_steps(step, steps=5, warmup=2)
+    frames, nbytes = 1000 + rank, 64 * (1000 + rank)
+    tp = dist.throughput(frames, nbytes, 5, elapsed_max)
+    q.put((rank, len(calls), elapsed_max, local, tp))
+    tdist.destroy_process_group()
+
+
+def test_two_rank_bench_reduction():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] == 7 for r in res)  # warmup + exactly the timed steps
+    emax = max(r[3] for r in res)
+    assert all(r[2] == emax for r in res)  # every rank sees the MAX of the local times
+    assert emax >= 5 * 0.004  # the slower rank bounds the job
+    total = (1000 + 1001) * 5
+    for r in res:
+        tp = r[4]
+        assert tp["total_frames"] == total and tp["total_bytes"] == 64 * total
+        assert tp["value"] == round(total / emax / 1e6, 2)
+        assert tp["ms_per_step"] == round(emax / 5 * 1e3, 4)
