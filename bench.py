@@ -173,7 +173,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=25,
+                    help="untimed steps; a freshly generated batch runs its first launches "
+                         "slow (clock ramp), profiles/r01_staging/imix_ramp.txt")
     ap.add_argument("--workload", choices=["udp64", "imix", "ser"], default="udp64")
     ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
     ap.add_argument("--out", choices=list(OUT_KINDS), default="sparse",

@@ -124,7 +124,32 @@ typedef struct nexg_desc {
 /* Full decoded record per frame (out_kind NEXG_OUT_RECORD), 64 bytes.
  * Field values are the reference's parsed values (ipv4.rs:510-528,
  * ipv6.rs:259-268, tcp.rs:820-835, udp.rs:227-235, icmp.rs:188-204,
- * arp.rs:340-371). Fields of absent layers are 0. */
+ * arp.rs:340-371). Fields of absent layers are 0.
+ *
+ * A frame whose status is a ParseError kind carries the error's payload
+ * (parse.rs:53-81) and nothing else:
+ *   l4_type = NEXG_CTX_* (which reference check failed: its context string)
+ *   ip_src  = BufferTooShort.minimum | InvalidLength.value | Truncated.expected
+ *   ip_dst  = BufferTooShort.actual  | Truncated.actual       (else 0) */
+enum {
+    NEXG_CTX_NONE = 0,
+    NEXG_CTX_ETHERNET_PACKET = 1,     /* "Ethernet packet"  ethernet.rs:310-316           */
+    NEXG_CTX_DUMMY_ETHERNET = 2,      /* "Frame dummy Ethernet classification" frame.rs:585 */
+    NEXG_CTX_IPV4_PACKET = 3,         /* "IPv4 packet"  BufferTooShort ipv4.rs:380-386,
+                                         Truncated (strict) ipv4.rs:429-435                */
+    NEXG_CTX_IPV4_VERSION = 4,        /* "IPv4 packet version"  ipv4.rs:388-393           */
+    NEXG_CTX_IPV4_HEADER_LENGTH = 5,  /* "IPv4 header length"  ipv4.rs:395-401            */
+    NEXG_CTX_IPV4_HEADER = 6,         /* "IPv4 header"  ipv4.rs:403-410                   */
+    NEXG_CTX_IPV4_TOTAL_LENGTH = 7,   /* "IPv4 total length" (value = declared) 421-427   */
+    NEXG_CTX_IPV4_OPTIONS = 8,        /* "IPv4 options" (strict)  ipv4.rs:476-481          */
+    NEXG_CTX_IPV4_OPTION_LENGTH = 9,  /* "IPv4 option length" (strict)  ipv4.rs:485-491    */
+    NEXG_CTX_IPV6_PACKET = 10,        /* "IPv6 packet"  ipv6.rs:225-231                   */
+    NEXG_CTX_IPV6_VERSION = 11,       /* "IPv6 packet version"  ipv6.rs:235-239           */
+    NEXG_CTX_IPV6_PAYLOAD = 12,       /* "IPv6 payload" (strict)  ipv6.rs:271-277          */
+    NEXG_CTX_IPV6_EXTENSION = 13,     /* "IPv6 extension header"  ipv6.rs:288-308         */
+    NEXG_CTX_IPV6_ROUTING = 14,       /* "IPv6 routing header"  ipv6.rs:319-335           */
+    NEXG_CTX_IPV6_FRAGMENT = 15       /* "IPv6 fragment header"  ipv6.rs:346-352          */
+};
 typedef struct nexg_record {
     uint32_t flags;          /* as nexg_desc.flags                              */
     uint16_t payload_off;    /* Frame.payload offset in the frame               */

@@ -124,6 +124,13 @@ WL_IMIX = 2
 DEFAULT_SEED = 0x6E6578
 
 
+#: NEXG_CTX_* -> the reference's ParseError context string (include/nexg.h)
+ERR_CONTEXTS = (None, "Ethernet packet", "Frame dummy Ethernet classification", "IPv4 packet",
+                "IPv4 packet version", "IPv4 header length", "IPv4 header", "IPv4 total length",
+                "IPv4 options", "IPv4 option length", "IPv6 packet", "IPv6 packet version", "IPv6 payload",
+                "IPv6 extension header", "IPv6 routing header", "IPv6 fragment header")
+
+
 def status_of(flags):
     return (np.asarray(flags) >> STATUS_SHIFT) & 0x7
 

@@ -312,19 +312,20 @@ NEXG_HD uint32_t parse_ipv4(const O& o, uint32_t l3, uint32_t len,
                                                bool strict, nexg_record& r) {
     const uint32_t n = len - l3;
     r.flags |= NEXG_L_IP;
-    uint32_t err = 0, hl = 0, total = 0;
+    // err: ParseError kind; ctx / ea / eb: its payload (include/nexg.h NEXG_CTX_*)
+    uint32_t err = 0, ctx = 0, ea = 0, eb = 0, hl = 0, total = 0;
     uint32_t b0 = n >= 20u ? o.f.u8(l3) : 0u;
-    if (n < 20u) err = NEXG_ERR_BUFFER_TOO_SHORT;
-    else if ((b0 >> 4) != 4u) err = NEXG_ERR_MALFORMED;
-    else if ((b0 & 15u) < 5u) err = NEXG_ERR_INVALID_LENGTH;
+    if (n < 20u) { err = NEXG_ERR_BUFFER_TOO_SHORT; ctx = NEXG_CTX_IPV4_PACKET; ea = 20u; eb = n; }
+    else if ((b0 >> 4) != 4u) { err = NEXG_ERR_MALFORMED; ctx = NEXG_CTX_IPV4_VERSION; }
+    else if ((b0 & 15u) < 5u) { err = NEXG_ERR_INVALID_LENGTH; ctx = NEXG_CTX_IPV4_HEADER_LENGTH; ea = b0 & 15u; }
     else {
         hl = (b0 & 15u) * 4u;
-        if (hl > n) err = NEXG_ERR_TRUNCATED;
+        if (hl > n) { err = NEXG_ERR_TRUNCATED; ctx = NEXG_CTX_IPV4_HEADER; ea = hl; eb = n; }
         else {
             uint32_t declared = o.be16(l3 + 2);
             uint32_t eff = declared ? declared : n;
-            if (eff < hl) err = NEXG_ERR_INVALID_LENGTH;
-            else if (strict && eff > n) err = NEXG_ERR_TRUNCATED;
+            if (eff < hl) { err = NEXG_ERR_INVALID_LENGTH; ctx = NEXG_CTX_IPV4_TOTAL_LENGTH; ea = declared; }
+            else if (strict && eff > n) { err = NEXG_ERR_TRUNCATED; ctx = NEXG_CTX_IPV4_PACKET; ea = eff; eb = n; }
             else total = eff < n ? eff : n;
         }
     }
@@ -337,13 +338,13 @@ NEXG_HD uint32_t parse_ipv4(const O& o, uint32_t l3, uint32_t len,
             if (num == 0u) { nopt++; stop = i + 1; break; }  // EOL
             if (num == 1u) { nopt++; i++; continue; }        // NOP
             if (i + 2u > hl) {
-                if (strict) err = NEXG_ERR_MALFORMED;
+                if (strict) { err = NEXG_ERR_MALFORMED; ctx = NEXG_CTX_IPV4_OPTIONS; }
                 stop = i;
                 break;
             }
             uint32_t l = o.f.u8(l3 + i + 1);
             if (l < 2u || i + l > hl) {
-                if (strict) err = NEXG_ERR_INVALID_LENGTH;
+                if (strict) { err = NEXG_ERR_INVALID_LENGTH; ctx = NEXG_CTX_IPV4_OPTION_LENGTH; ea = l; }
                 stop = i;
                 break;
             }
@@ -351,7 +352,13 @@ NEXG_HD uint32_t parse_ipv4(const O& o, uint32_t l3, uint32_t len,
             i += l;
         }
     }
-    if (err) return strict ? err : 0u;  // Q4: ip = Some(all None), payload empty
+    if (err) {  // Q4: lenient -> ip = Some(all None), payload empty
+        if (!strict) return 0u;
+        r.l4_type = (uint8_t)ctx;
+        r.ip_src = ea;
+        r.ip_dst = eb;
+        return err;
+    }
 
     uint32_t tos = o.f.u8(l3 + 1);
     uint32_t id = o.be16(l3 + 4), ff = o.be16(l3 + 6);
@@ -400,32 +407,40 @@ NEXG_HD uint32_t parse_ipv6(const O& o, uint32_t l3, uint32_t len,
                                                bool strict, nexg_record& r) {
     const uint32_t n = len - l3;
     r.flags |= NEXG_L_IP;
-    if (n < 40u) return strict ? NEXG_ERR_BUFFER_TOO_SHORT : 0u;
+    // ParseError payload of a strict failure (include/nexg.h NEXG_CTX_*)
+    auto fail = [&](uint32_t err, uint32_t ctx, uint32_t ea, uint32_t eb) -> uint32_t {
+        if (!strict) return 0u;
+        r.l4_type = (uint8_t)ctx;
+        r.ip_src = ea;
+        r.ip_dst = eb;
+        return err;
+    };
+    if (n < 40u) return fail(NEXG_ERR_BUFFER_TOO_SHORT, NEXG_CTX_IPV6_PACKET, 40u, n);
     uint32_t w0 = o.be32(l3);
-    if ((w0 >> 28) != 6u) return strict ? NEXG_ERR_MALFORMED : 0u;
+    if ((w0 >> 28) != 6u) return fail(NEXG_ERR_MALFORMED, NEXG_CTX_IPV6_VERSION, 0u, 0u);
     uint32_t pl = o.be16(l3 + 4);
     uint32_t declared = 40u + pl;
-    if (strict && declared > n) return NEXG_ERR_TRUNCATED;
+    if (strict && declared > n) return fail(NEXG_ERR_TRUNCATED, NEXG_CTX_IPV6_PAYLOAD, declared, n);
     uint32_t avail = declared < n ? declared : n;
     uint32_t first = ip_next_protocol_value(o.f.u8(l3 + 6));
-    uint32_t nh = first, off = 40, next = 0, err = 0;
+    uint32_t nh = first, off = 40, next = 0, ctx = 0, need = 0;
     while (nh == 0u || nh == 43u || nh == 44u || nh == 60u) {
-        if (off + 2u > avail) { err = NEXG_ERR_TRUNCATED; break; }
+        if (off + 2u > avail) { ctx = NEXG_CTX_IPV6_EXTENSION; need = off + 2u; break; }
         uint32_t nh2 = ip_next_protocol_value(o.f.u8(l3 + off));
         uint32_t el = o.f.u8(l3 + off + 1);
         if (nh == 44u) {
-            if (off + 8u > avail) { err = NEXG_ERR_TRUNCATED; break; }
+            if (off + 8u > avail) { ctx = NEXG_CTX_IPV6_FRAGMENT; need = off + 8u; break; }
             off += 8u;
         } else {
-            if (nh == 43u && off + 4u > avail) { err = NEXG_ERR_TRUNCATED; break; }
+            if (nh == 43u && off + 4u > avail) { ctx = NEXG_CTX_IPV6_ROUTING; need = off + 4u; break; }
             uint32_t tl = 8u + el * 8u;
-            if (off + tl > avail) { err = NEXG_ERR_TRUNCATED; break; }
+            if (off + tl > avail) { ctx = nh == 43u ? NEXG_CTX_IPV6_ROUTING : NEXG_CTX_IPV6_EXTENSION; need = off + tl; break; }
             off += tl;
         }
         next++;
         nh = nh2;
     }
-    if (err) return strict ? err : 0u;  // Q12
+    if (ctx) return fail(NEXG_ERR_TRUNCATED, ctx, need, avail);  // Q12
     r.flags |= NEXG_L_IPV6;
     r.ip_ver_ihl = (uint8_t)((w0 >> 28) << 4);
     r.ip_tos = (uint8_t)(w0 >> 20);
@@ -704,6 +719,7 @@ NEXG_HD void parse_frame(const F& f, uint32_t parity, uint32_t len,
     if (opt_flags & NEXG_PARSE_FROM_IP) {
         if (ip_offset >= len) {
             r.flags = (uint32_t)NEXG_ERR_MALFORMED << NEXG_STATUS_SHIFT;
+            r.l4_type = NEXG_CTX_DUMMY_ETHERNET;
             return;
         }
         uint32_t n = len - ip_offset, v = f.u8(ip_offset);
@@ -711,12 +727,16 @@ NEXG_HD void parse_frame(const F& f, uint32_t parity, uint32_t len,
         else if (n >= 40u && (v >> 4) == 6u) ethertype = 0x86DDu;
         else {
             r.flags = (uint32_t)NEXG_ERR_MALFORMED << NEXG_STATUS_SHIFT;
+            r.l4_type = NEXG_CTX_DUMMY_ETHERNET;
             return;
         }
         l3 = ip_offset;
     } else {
         if (len < 14u) {  // Q2: ethernet.rs:310-316
             r.flags = (uint32_t)NEXG_ERR_BUFFER_TOO_SHORT << NEXG_STATUS_SHIFT;
+            r.l4_type = NEXG_CTX_ETHERNET_PACKET;
+            r.ip_src = 14u;
+            r.ip_dst = len;
             return;
         }
         ethertype = o.be16(12);
@@ -741,9 +761,14 @@ NEXG_HD void parse_frame(const F& f, uint32_t parity, uint32_t len,
     else if (ethertype == 0x86DDu) err = parse_ipv6(o, l3, len, strict, r);
     else if (ethertype == 0x0806u) parse_arp(o, l3, len, r);
     else set_payload(r, l3, len - l3);  // Q3
-    if (err) {
+    if (err) {  // only the ParseError (kind + payload) survives
+        const uint8_t ctx = r.l4_type;
+        const uint32_t ea = r.ip_src, eb = r.ip_dst;
         r = nexg_record{};
         r.flags = err << NEXG_STATUS_SHIFT;
+        r.l4_type = ctx;
+        r.ip_src = ea;
+        r.ip_dst = eb;
     }
 }
 

@@ -48,13 +48,15 @@ ParseVariant choose_parse_variant(const ParseArgs& a) {
     return ParseVariant::TwoPass;
 }
 
-// Span kernel generation: NEXG_SPAN=1 (4 barriers per 16-KiB sub-tile),
-// 2 (2 barriers), 2d (8-KiB double-buffered sub-tiles, 1 barrier) overrides
-// for measurement; the default is the measured best.
+// Span kernel generation: NEXG_SPAN=1 (4 barriers per 16-KiB sub-tile, the
+// default: measured best), 2 (2 barriers), 2d (8-KiB double-buffered
+// sub-tiles, 1 barrier). Fewer barriers measured slower (0.66 vs 0.73 of
+// peak, profiles/r02_kbench/): the per-group stream, not the barriers,
+// bounds the loop.
 static int span_variant() {
     static const int v = [] {
         const char* e = getenv("NEXG_SPAN");
-        if (!e) return 2;
+        if (!e) return 1;
         return strcmp(e, "1") == 0 ? 1 : strcmp(e, "2d") == 0 ? 3 : 2;
     }();
     return v;

@@ -63,8 +63,10 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // lane): a ballot compacts the wave's exceptions into exc[group*64 + rank];
 // the 1-B codes of lanes 4q..4q+3 are gathered by DPP quad broadcasts and
 // stored as one non-temporal dword by lane 4q.
-__device__ __forceinline__ void store_sparse(const ParseArgs& a, uint64_t idx, bool valid, const nexg_record& r) {
-    const uint32_t code = valid ? sparse_encode(r, a.opt_flags, a.ip_offset) : 0u;
+__device__ __forceinline__ void store_sparse(const ParseArgs& a, uint64_t idx, bool valid, const nexg_record& r,
+                                             uint32_t known = 0u) {
+    // known: the code when the caller already proved the shape (fast paths)
+    const uint32_t code = !valid ? 0u : known ? known : sparse_encode(r, a.opt_flags, a.ip_offset);
     const bool exc = valid && code == 0u;
     const uint64_t m = __ballot(exc);
     uint8_t* codes = reinterpret_cast<uint8_t*>(a.out);
@@ -237,7 +239,14 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
         if (kStaged) stage_record(slot, r);  // own slot: no other thread reads it
         else if constexpr (OUT != NEXG_OUT_SPARSE) store_result<OUT>(a.out, idx, r);
     }
-    if constexpr (OUT == NEXG_OUT_SPARSE) store_sparse(a, idx, tid < nf, r);
+    if constexpr (OUT == NEXG_OUT_SPARSE) {
+        // fast_udp4_64 proved IPv4/UDP with the datagram to the frame end (payload
+        // [42, 64)): the code is the shape and the two verdicts
+        const uint32_t known = have ? NEXG_SHAPE_V4_UDP | ((r.flags & NEXG_C_IP_OK) ? NEXG_SPARSE_IP_OK : 0u) |
+                                          ((r.flags & NEXG_C_L4_OK) ? NEXG_SPARSE_L4_OK : 0u)
+                                    : 0u;
+        store_sparse(a, idx, tid < nf, r, known);
+    }
     if (kStaged) {
         __syncthreads();
         copy_out_records<PITCH>(smem, a.out, first, nf);

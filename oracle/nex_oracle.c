@@ -141,23 +141,27 @@ typedef struct {
     ipv4_option options[40];
     const uint8_t* bytes; /* backing buffer (Bytes) */
     size_t payload_off, payload_len;
+    uint32_t err_ctx, err_a, err_b; /* ParseError payload of a failed parse (NEXG_CTX_*) */
 } ipv4_packet;
+
+/* return ParseError kind `kind` with its payload (parse.rs:53-81) */
+#define PERR(pk, kind, ctx, a, b) ((pk)->err_ctx = (ctx), (pk)->err_a = (uint32_t)(a), (pk)->err_b = (uint32_t)(b), (kind))
 
 /* ipv4.rs:372-529 parse_ipv4_parts; returns ParseError kind or 0 */
 static int parse_ipv4(const uint8_t* bytes, size_t len, int strict, ipv4_packet* pk) {
-    if (len < 20) return NEXG_ERR_BUFFER_TOO_SHORT;
+    if (len < 20) return PERR(pk, NEXG_ERR_BUFFER_TOO_SHORT, NEXG_CTX_IPV4_PACKET, 20, len);
     uint8_t version = (bytes[0] & 0xF0) >> 4;
-    if (version != 4) return NEXG_ERR_MALFORMED;
+    if (version != 4) return PERR(pk, NEXG_ERR_MALFORMED, NEXG_CTX_IPV4_VERSION, 0, 0);
     size_t header_length = bytes[0] & 0x0F;
-    if (header_length < 5) return NEXG_ERR_INVALID_LENGTH;
+    if (header_length < 5) return PERR(pk, NEXG_ERR_INVALID_LENGTH, NEXG_CTX_IPV4_HEADER_LENGTH, header_length, 0);
     size_t ihl_bytes = header_length * 4;
-    if (ihl_bytes < 20 || ihl_bytes > len) return NEXG_ERR_TRUNCATED;
+    if (ihl_bytes < 20 || ihl_bytes > len) return PERR(pk, NEXG_ERR_TRUNCATED, NEXG_CTX_IPV4_HEADER, ihl_bytes, len);
     size_t declared = be16(bytes + 2);
     size_t eff = declared == 0 ? len : declared;
-    if (eff < ihl_bytes) return NEXG_ERR_INVALID_LENGTH;
+    if (eff < ihl_bytes) return PERR(pk, NEXG_ERR_INVALID_LENGTH, NEXG_CTX_IPV4_TOTAL_LENGTH, declared, 0);
     size_t total_length;
     if (strict) {
-        if (eff > len) return NEXG_ERR_TRUNCATED;
+        if (eff > len) return PERR(pk, NEXG_ERR_TRUNCATED, NEXG_CTX_IPV4_PACKET, eff, len);
         total_length = eff;
     } else {
         total_length = eff < len ? eff : len;
@@ -178,12 +182,12 @@ static int parse_ipv4(const uint8_t* bytes, size_t len, int strict, ipv4_packet*
             i += 1;
         } else {
             if (i + 2 > ihl_bytes) {
-                if (strict) return NEXG_ERR_MALFORMED;
+                if (strict) return PERR(pk, NEXG_ERR_MALFORMED, NEXG_CTX_IPV4_OPTIONS, 0, 0);
                 break;
             }
             size_t l = bytes[i + 1];
             if (l < 2 || i + l > ihl_bytes) {
-                if (strict) return NEXG_ERR_INVALID_LENGTH;
+                if (strict) return PERR(pk, NEXG_ERR_INVALID_LENGTH, NEXG_CTX_IPV4_OPTION_LENGTH, l, 0);
                 break;
             }
             *o = (ipv4_option){copied, klass, number, 1, (uint8_t)l, i + 2, l - 2, i};
@@ -279,13 +283,14 @@ typedef struct {
     uint8_t source[16], destination[16];
     int next;
     size_t payload_off, payload_len;
+    uint32_t err_ctx, err_a, err_b; /* ParseError payload of a failed parse */
 } ipv6_packet;
 
 /* ipv6.rs:217-384 parse_ipv6_parts */
 static int parse_ipv6(const uint8_t* bytes, size_t len, int strict, ipv6_packet* pk) {
-    if (len < 40) return NEXG_ERR_BUFFER_TOO_SHORT;
+    if (len < 40) return PERR(pk, NEXG_ERR_BUFFER_TOO_SHORT, NEXG_CTX_IPV6_PACKET, 40, len);
     uint8_t version = bytes[0] >> 4;
-    if (version != 6) return NEXG_ERR_MALFORMED;
+    if (version != 6) return PERR(pk, NEXG_ERR_MALFORMED, NEXG_CTX_IPV6_VERSION, 0, 0);
     pk->version = version;
     pk->traffic_class = (uint8_t)(((bytes[0] & 0x0F) << 4) | (bytes[1] >> 4));
     pk->flow_label = ((uint32_t)(bytes[1] & 0x0F) << 16) | ((uint32_t)bytes[2] << 8) | bytes[3];
@@ -296,27 +301,32 @@ static int parse_ipv6(const uint8_t* bytes, size_t len, int strict, ipv6_packet*
     memcpy(pk->source, bytes + 8, 16);
     memcpy(pk->destination, bytes + 24, 16);
     size_t declared_total = 40 + (size_t)pk->payload_length;
-    if (strict && declared_total > len) return NEXG_ERR_TRUNCATED;
+    if (strict && declared_total > len) return PERR(pk, NEXG_ERR_TRUNCATED, NEXG_CTX_IPV6_PAYLOAD, declared_total, len);
     size_t avail_end = declared_total < len ? declared_total : len;
     size_t offset = 40;
     pk->next = 0;
     for (;;) {
         if (next_header == PROTO_HOPOPT || next_header == PROTO_IPV6_ROUTE ||
             next_header == PROTO_IPV6_FRAG || next_header == PROTO_IPV6_OPTS) {
-            if (offset + 2 > avail_end) return NEXG_ERR_TRUNCATED;
+            if (offset + 2 > avail_end)
+                return PERR(pk, NEXG_ERR_TRUNCATED, NEXG_CTX_IPV6_EXTENSION, offset + 2, avail_end);
             uint8_t nh = ip_next_protocol_value(bytes[offset]);
             size_t ext_len = bytes[offset + 1];
             if (next_header == PROTO_HOPOPT || next_header == PROTO_IPV6_OPTS) {
                 size_t total_len = 8 + ext_len * 8;
-                if (offset + total_len > avail_end) return NEXG_ERR_TRUNCATED;
+                if (offset + total_len > avail_end)
+                    return PERR(pk, NEXG_ERR_TRUNCATED, NEXG_CTX_IPV6_EXTENSION, offset + total_len, avail_end);
                 offset += total_len;
             } else if (next_header == PROTO_IPV6_ROUTE) {
-                if (offset + 4 > avail_end) return NEXG_ERR_TRUNCATED;
+                if (offset + 4 > avail_end)
+                    return PERR(pk, NEXG_ERR_TRUNCATED, NEXG_CTX_IPV6_ROUTING, offset + 4, avail_end);
                 size_t total_len = 8 + ext_len * 8;
-                if (offset + total_len > avail_end) return NEXG_ERR_TRUNCATED;
+                if (offset + total_len > avail_end)
+                    return PERR(pk, NEXG_ERR_TRUNCATED, NEXG_CTX_IPV6_ROUTING, offset + total_len, avail_end);
                 offset += total_len;
             } else { /* Ipv6Frag */
-                if (offset + 8 > avail_end) return NEXG_ERR_TRUNCATED;
+                if (offset + 8 > avail_end)
+                    return PERR(pk, NEXG_ERR_TRUNCATED, NEXG_CTX_IPV6_FRAGMENT, offset + 8, avail_end);
                 offset += 8;
             }
             pk->next++;
@@ -557,7 +567,12 @@ static int frame_parse_ipv4(const uint8_t* fr, size_t l3, size_t len, int strict
     int err = parse_ipv4(fr + l3, len - l3, strict, &pk);
     rec->flags |= NEXG_L_IP;
     if (err) {
-        if (strict) return err;
+        if (strict) { /* the ParseError and its payload propagate (Q24) */
+            rec->l4_type = (uint8_t)pk.err_ctx;
+            rec->ip_src = pk.err_a;
+            rec->ip_dst = pk.err_b;
+            return err;
+        }
         return 0; /* ip = Some(all None), payload empty */
     }
     rec->flags |= NEXG_L_IPV4;
@@ -597,7 +612,12 @@ static int frame_parse_ipv6(const uint8_t* fr, size_t l3, size_t len, int strict
     int err = parse_ipv6(fr + l3, len - l3, strict, &pk);
     rec->flags |= NEXG_L_IP;
     if (err) {
-        if (strict) return err;
+        if (strict) {
+            rec->l4_type = (uint8_t)pk.err_ctx;
+            rec->ip_src = pk.err_a;
+            rec->ip_dst = pk.err_b;
+            return err;
+        }
         return 0;
     }
     rec->flags |= NEXG_L_IPV6;
@@ -660,8 +680,11 @@ void nexo_parse_frame(const uint8_t* fr, size_t len, uint32_t flags,
         else goto malformed;
         l3 = off;
     } else {
-        if (len < 14) {
+        if (len < 14) { /* ethernet.rs:310-316 */
             rec->flags = (uint32_t)NEXG_ERR_BUFFER_TOO_SHORT << NEXG_STATUS_SHIFT;
+            rec->l4_type = NEXG_CTX_ETHERNET_PACKET;
+            rec->ip_src = 14;
+            rec->ip_dst = (uint32_t)len;
             return;
         }
         ethertype = be16(fr + 12);
@@ -686,13 +709,19 @@ void nexo_parse_frame(const uint8_t* fr, size_t len, uint32_t flags,
         case 0x0806: frame_parse_arp(fr, l3, len, rec); break;
         default: set_payload(rec, l3, len - l3); break;
     }
-    if (err) {
+    if (err) { /* Err(ParseError): nothing but the error survives */
+        uint8_t ctx = rec->l4_type;
+        uint32_t a = rec->ip_src, b = rec->ip_dst;
         memset(rec, 0, sizeof(*rec));
         rec->flags = (uint32_t)err << NEXG_STATUS_SHIFT;
+        rec->l4_type = ctx;
+        rec->ip_src = a;
+        rec->ip_dst = b;
     }
     return;
-malformed:
+malformed: /* frame.rs:585-587 */
     rec->flags = (uint32_t)NEXG_ERR_MALFORMED << NEXG_STATUS_SHIFT;
+    rec->l4_type = NEXG_CTX_DUMMY_ETHERNET;
 }
 
 void nexo_record_to_desc(const nexg_record* rec, nexg_desc* d) {

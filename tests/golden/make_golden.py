@@ -138,7 +138,8 @@ add("ethernet_parse_basic", "ethernet.rs:458-476",
     {"layers": ["eth", "ip"], "ethertype": 0x0800, "eth_dst": "aabbccddeeff", "eth_src": "112233445566"},
     note="EtherType Ipv4 with a 4-B payload: IPv4 fails -> ip Some(all None), payload empty (Q4)")
 add("ethernet_too_short", "ethernet.rs:510-528 (BufferTooShort, actual 4)", bytes([0, 1, 2, 3]),
-    {"status": 1})
+    {"status": 1, "err_context": "Ethernet packet", "err_a": 14, "err_b": 4},
+    note="ethernet.rs:513-520 asserts BufferTooShort{context 'Ethernet packet', minimum 14, actual 4}")
 add("ethernet_unknown_ethertype_dead", "ethernet.rs:530-539 (EtherType::Unknown(0xdead))",
     bytes([0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff, 0x11, 0x22, 0x33, 0x44, 0x55, 0x66, 0xde, 0xad,
            0x00, 0x11, 0x22, 0x33]),
@@ -179,7 +180,12 @@ add("ipv4_checksum_zero_field", "ipv4.rs:1073-1095 (checksum(&p) then reparse)",
 STRICT = bytes([0x45, 0x00, 0x00, 0x28, 0x00, 0x00, 0x00, 0x00, 64, 17, 0, 0, 127, 0, 0, 1, 127,
                 0, 0, 1, 1, 2, 3, 4])
 add("ipv4_strict_truncation", "ipv4.rs:1176-1187 (strict -> Truncated)", STRICT,
-    {"status": 4}, flags=3)
+    {"status": 4, "err_context": "IPv4 packet", "err_a": 40, "err_b": 24}, flags=3,
+    note="the test asserts the kind; expected/actual follow ipv4.rs:429-435 (total 40, captured 24)")
+STRICT6 = bytes([0x60, 0x00, 0x00, 0x00, 0x00, 0x10, 0x11, 0x40] + [0] * 15 + [1] + [0] * 15 + [1, 1, 2, 3, 4])
+add("ipv6_strict_truncation", "ipv6.rs:915-928 (strict -> Truncated)", STRICT6,
+    {"status": 4, "err_context": "IPv6 payload", "err_a": 56, "err_b": 44}, flags=3,
+    note="the test asserts the kind; expected/actual follow ipv6.rs:270-276 (40 + 16 declared, 44 captured)")
 add("ipv4_lenient_truncation", "ipv4.rs:1186 (lenient parse succeeds)", STRICT,
     {"layers": ["eth", "ip", "ipv4", "transport"], "ip_length": 24}, flags=2)
 ZERO = bytes([0x45, 0x00, 0x00, 0x00, 0x68, 0x23, 0x40, 0x00, 0x80, 0x06, 0x00, 0x00, 192, 168,

@@ -40,6 +40,9 @@ def check_expect(rec, frame: bytes, exp: dict, name="", reparse=None, parse_flag
     flags = int(rec["flags"])
     if "status" in exp:
         assert (flags >> abi.STATUS_SHIFT) & 7 == exp["status"], name
+        if "err_context" in exp:  # the ParseError payload (parse.rs:53-81)
+            assert abi.ERR_CONTEXTS[int(rec["l4_type"])] == exp["err_context"], (name, int(rec["l4_type"]))
+            assert (int(rec["ip_src"]), int(rec["ip_dst"])) == (exp["err_a"], exp["err_b"]), name
         return
     assert (flags >> abi.STATUS_SHIFT) & 7 == 0, name
     if "layers" in exp:

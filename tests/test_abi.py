@@ -130,3 +130,13 @@ def test_l4_build_layouts_match_c(tmp_path, cname, cls):
     out = list(map(int, subprocess.check_output([str(exe)], text=True).split()))
     assert out[0] == ctypes.sizeof(cls)
     assert out[1:] == [getattr(cls, f).offset for f, _ in cls._fields_]
+
+
+def test_error_contexts_match_header():
+    """NEXG_CTX_* values and the context strings they name (include/nexg.h)
+    are the table the Python / C++ host layers report ParseError with."""
+    text = open(HDR).read()
+    pairs = re.findall(r'NEXG_CTX_\w+ = (\d+),?\s*/\* "([^"]+)"', text)
+    assert len(pairs) == len(abi.ERR_CONTEXTS) - 1
+    for v, ctx in pairs:
+        assert abi.ERR_CONTEXTS[int(v)] == ctx
