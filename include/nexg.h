@@ -54,7 +54,9 @@ enum {
     NEXG_ENOMEM = -2,  /* host allocation failed                          */
     NEXG_EDEVICE = -3, /* HIP device error / not a gfx950 device          */
     NEXG_ELAUNCH = -4, /* kernel launch failed                            */
-    NEXG_ERANGE = -5   /* BuildError::LengthOverflow (builder/error.rs:8)  */
+    NEXG_ERANGE = -5,  /* BuildError::LengthOverflow (builder/error.rs:8)  */
+    NEXG_EPERM = -6,   /* datalink socket: no CAP_NET_RAW                 */
+    NEXG_EIO = -7      /* datalink socket / ring system call failed       */
 };
 
 /* ---- per-frame status: ParseError kind (parse.rs:51-97) --------------- */
@@ -612,6 +614,80 @@ int nexg_pcap_read_raw(nexg_pcap* p, uint8_t* buf, uint64_t cap, uint64_t* offse
  * staging measured 2.5-4x slower on the GPU boxes, profiles/r01_ingest/threads.) */
 int nexg_pcap_set_read_threads(nexg_pcap* p, uint32_t threads);
 int nexg_pcap_close(nexg_pcap* p);
+
+/* ---- live datalink batch rx / tx ---------------------------
+ * The reference's Linux channel (nex-datalink/src/linux.rs:102-218) hands one
+ * frame per RawReceiver::next (poll + recvfrom into a 4096-B buffer,
+ * linux.rs:356-397) and sends one per RawSender::send (poll + sendto,
+ * linux.rs:302-346); its scale-out is PACKET_FANOUT (lib.rs:70-131,
+ * linux.rs:154-193). Here an AF_PACKET socket with the same Config knobs
+ * (read_buffer_size, promiscuous, linux_fanout, read timeout) fills whole
+ * batches: the TPACKET_V3 mmap ring (blocks of frames retired by the kernel)
+ * or recvmmsg, copied into the caller's (pinned) buffer in the packed layout
+ * nexg_pcap_read_batch produces (offsets only, parse with SpanTile). Each
+ * frame is its first min(len, read_buffer_size) bytes, as recvfrom into the
+ * reference's read buffer truncates it. One rx per GPU in one fanout group
+ * is the multi-GPU ingest. Host-side only; needs
+ * CAP_NET_RAW (open fails with NEXG_EPERM without it). */
+#define NEXG_RX_RING 0u  /* TPACKET_V3 mmap ring (default)                   */
+#define NEXG_RX_MMSG 1u  /* recvmmsg into read_buffer_size slots             */
+/* FanoutType (nex-datalink/src/lib.rs:70-90) = PACKET_FANOUT_* */
+#define NEXG_FANOUT_HASH 0u
+#define NEXG_FANOUT_LB 1u
+#define NEXG_FANOUT_CPU 2u
+#define NEXG_FANOUT_ROLLOVER 3u
+#define NEXG_FANOUT_RND 4u
+#define NEXG_FANOUT_QM 5u
+#define NEXG_FANOUT_FLAG_ROLLOVER 0x1000u /* FanoutOption.rollover */
+#define NEXG_FANOUT_FLAG_DEFRAG 0x8000u   /* FanoutOption.defrag   */
+/* rx flags: drop the loopback echo of frames this host sends (sll_pkttype
+ * PACKET_OUTGOING); the reference keeps them (recvfrom discards sockaddr_ll,
+ * linux.rs:358), so the default is to keep them too. */
+#define NEXG_RX_SKIP_OUTGOING 0x1u
+typedef struct nexg_rx_config {
+    uint32_t read_buffer_size; /* Config.read_buffer_size (default 4096, lib.rs:229) */
+    int32_t read_timeout_ms;   /* Config.read_timeout; -1 = wait (default)          */
+    uint32_t promiscuous;      /* Config.promiscuous (default 1)                    */
+    uint32_t fanout;           /* 1: join linux_fanout group below                  */
+    uint32_t fanout_type;      /* NEXG_FANOUT_* | NEXG_FANOUT_FLAG_*               */
+    uint32_t fanout_group;     /* FanoutOption.group_id                             */
+    uint32_t mode;             /* NEXG_RX_RING / NEXG_RX_MMSG                       */
+    uint32_t ring_block_size;  /* TPACKET_V3 block bytes (default 1 MiB)            */
+    uint32_t ring_blocks;      /* blocks in the ring (default 64)                   */
+    uint32_t ring_block_tov_ms;/* block retire timeout (default 2 ms)               */
+    uint32_t flags;            /* NEXG_RX_*                                         */
+    uint32_t reserved;
+} nexg_rx_config;
+typedef struct nexg_rx nexg_rx;
+typedef struct nexg_tx nexg_tx;
+void nexg_rx_config_default(nexg_rx_config* cfg);
+int nexg_rx_open(const char* ifname, const nexg_rx_config* cfg, nexg_rx** out);
+/* Up to max_frames frames (bytes packed: frame k at data + offsets[k],
+ * offsets[n] = end; offsets holds max_frames + 1 entries); waits up to the
+ * read timeout for the first frame (*n_frames = 0 on timeout), then takes
+ * whatever the ring / socket already holds. ts_ns optional. */
+int nexg_rx_next_batch(nexg_rx* rx, uint8_t* data, uint64_t data_cap, uint64_t* offsets,
+                       uint64_t max_frames, uint64_t* ts_ns, uint64_t* n_frames);
+/* PACKET_STATISTICS since the last call: frames seen, frames dropped. */
+int nexg_rx_stats(nexg_rx* rx, uint64_t* packets, uint64_t* drops);
+int nexg_rx_close(nexg_rx* rx);
+/* The ring walker on one retired TPACKET_V3 block (struct tpacket_block_desc
+ * + tpacket3_hdr chain, linux/if_packet.h), from packet `first` on: frames
+ * appended to the packed batch at data[*pos...] with offsets[*n...] until
+ * max_frames / data_cap; *next_pkt = the first packet not taken (== the
+ * block's num_pkts when done). What nexg_rx_next_batch runs on each block;
+ * exported so the walk is tested on synthetic blocks without a socket. */
+int nexg_tpacket3_walk(const uint8_t* block, uint64_t block_bytes, uint32_t first, uint32_t snap,
+                       uint32_t flags, uint8_t* data, uint64_t data_cap, uint64_t* pos,
+                       uint64_t* offsets, uint64_t max_frames, uint64_t* ts_ns, uint64_t* n,
+                       uint32_t* next_pkt);
+int nexg_tx_open(const char* ifname, nexg_tx** out);
+/* Sends frames (host memory, the nexg_frames layout: offsets NULL -> stride)
+ * with sendmmsg, up to 1024 per system call, waiting for POLLOUT as
+ * RawSender::send does; *n_sent = frames the kernel accepted. */
+int nexg_tx_send_batch(nexg_tx* tx, const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
+                       uint32_t stride, uint64_t count, uint64_t* n_sent);
+int nexg_tx_close(nexg_tx* tx);
 
 /* ---- synthetic workloads --------------------------
  * Frame i of a workload depends only on (seed, first_index + i), so shards

@@ -57,6 +57,16 @@ def load():
         "nexg_pcap_read_raw": (I, [P, P, U64, P, P, U64, P, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "nexg_pcap_set_read_threads": (I, [P, U32]),
         "nexg_pcap_close": (I, [P]),
+        "nexg_rx_config_default": (None, [P]),
+        "nexg_rx_open": (I, [ctypes.c_char_p, P, ctypes.POINTER(P)]),
+        "nexg_rx_next_batch": (I, [P, P, U64, P, U64, P, ctypes.POINTER(U64)]),
+        "nexg_rx_stats": (I, [P, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+        "nexg_rx_close": (I, [P]),
+        "nexg_tpacket3_walk": (I, [P, U64, U32, U32, U32, P, U64, ctypes.POINTER(U64), P, U64, P,
+                                   ctypes.POINTER(U64), ctypes.POINTER(U32)]),
+        "nexg_tx_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
+        "nexg_tx_send_batch": (I, [P, P, P, P, U32, U64, ctypes.POINTER(U64)]),
+        "nexg_tx_close": (I, [P]),
         "nexg_gen_lengths": (I, [P, I, U64, U64, U64, P, P]),
         "nexg_gen_frames": (I, [P, I, U64, U64, U64, P, P, U32, P]),
         "nexg_gen_udp4_params": (I, [P, U64, U64, U64, P, P, P, P, P, P]),

@@ -10,7 +10,7 @@ import numpy as np
 ABI_VERSION = 1
 
 # call status
-OK, EINVAL, ENOMEM, EDEVICE, ELAUNCH, ERANGE = 0, -1, -2, -3, -4, -5
+OK, EINVAL, ENOMEM, EDEVICE, ELAUNCH, ERANGE, EPERM, EIO = 0, -1, -2, -3, -4, -5, -6, -7
 
 # per-frame status: ParseError kind (nex-packet/src/parse.rs:51-97)
 FRAME_OK = 0
@@ -287,6 +287,8 @@ EXPORTED_SYMBOLS = (
     "nexg_abi_version", "nexg_strerror", "nexg_ctx_create", "nexg_ctx_destroy",
     "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch", "nexg_decode_options", "nexg_probe_stream",
     "nexg_sparse_expand", "nexg_recompute_checksums_batch",
+    "nexg_rx_config_default", "nexg_rx_open", "nexg_rx_next_batch", "nexg_rx_stats", "nexg_rx_close",
+    "nexg_tpacket3_walk", "nexg_tx_open", "nexg_tx_send_batch", "nexg_tx_close",
     "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_build_tcp_batch",
     "nexg_build_icmp_echo_batch", "nexg_pcap_open", "nexg_pcap_linktype", "nexg_pcap_last_error",
     "nexg_pcap_read_batch", "nexg_pcap_read_raw", "nexg_pcap_set_read_threads", "nexg_pcap_close", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",

@@ -23,6 +23,7 @@ for s in ${STEPS:-tests}; do
     bench) step bench_udp64 400 python bench.py --steps 50 --warmup 5 --cpu-seconds 5 ;;
     benchimix) step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5 ;;
     spanvar) for v in 1 2 2d; do step bench_imix_span$v 300 env NEXG_SPAN=$v python bench.py --workload imix --steps 20 --warmup 20 --no-cpu-baseline; done ;;
+    pmc) step pmc 900 bash tools/pmc.sh ;;
     prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-imix
           step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 10 --warmup 20 --no-cpu-baseline ;;
   esac
