@@ -169,6 +169,39 @@ def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
     return r
 
 
+def malformed_line(eng, args, F, first, out_kind, stream, device, rank, world):
+    """The SURVEY.md App. C malformed mix (nex_amd/workloads.py: half of the
+    IMIX frames carry one structural mutation) at the configs[2] size, same
+    output kind and timing: the cost of the frames that leave the canonical
+    fast paths for the generic parse core. 1M distinct frames tiled to F."""
+    import torch
+    from nex_amd import abi, dist, workloads
+    from nex_amd.engine import Engine
+    distinct = min(F, 1 << 20)
+    mix, counts = workloads.malformed_mix(eng, distinct, seed=abi.DEFAULT_SEED + first)
+    batch = workloads.tiled(mix, max(1, F // distinct))
+    n = batch.count
+    out = torch.empty(Engine.out_bytes(out_kind, n), dtype=torch.uint8, device=device)
+    alg = batch.total_bytes
+    steps = max(1, args.steps // 2)
+    elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
+                              steps, max(20, args.warmup), stream, device)
+    tp = dist.throughput(n, alg, steps, elapsed, device)
+    canonical = None
+    if out_kind == abi.OUT_SPARSE:  # share of frames with a shape code (no exception slot)
+        canonical = round(float((out[:n] != 0).float().mean().item()), 4)
+    if rank != 0:
+        return None
+    ach = alg / kernel_s / 1e9
+    return {"workload": f"SURVEY App. C malformed mix: {n} frames per GPU ({distinct} distinct, tiled), "
+                        f"IMIX with half the frames mutated {counts}; " + OUT_NOTE[args.out],
+            "value": tp["value"], "unit": "Mpkt/s", "steps": steps, "ms_per_step": tp["ms_per_step"],
+            "gib_s": tp["gib_s"], "bytes_per_gpu": alg, "sparse_shape_share": canonical,
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -182,6 +215,8 @@ def main():
                     help="output kind (default: lossless sparse descriptors, NEXG_OUT_SPARSE)")
     ap.add_argument("--no-imix", action="store_true",
                     help="skip the configs[2] IMIX line reported beside the default UDP64 run")
+    ap.add_argument("--no-malformed", action="store_true",
+                    help="skip the malformed-mix line (fallback cost) reported beside the default run")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true",
@@ -290,6 +325,9 @@ def main():
     imix = None
     if args.workload == "udp64" and not args.e2e and not args.no_imix and F == 16 << 20:
         imix = imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
+    malformed = None
+    if args.workload == "udp64" and not args.e2e and not args.no_malformed and F == 16 << 20:
+        malformed = malformed_line(eng, args, F, first, out_kind, stream, device, rank, world)
 
     if rank != 0:
         return
@@ -330,6 +368,8 @@ def main():
             frac_of_read64_write8=round(achieved / ceilings["read64_write8_gbs"], 4))
     if imix is not None:
         res["imix"] = imix
+    if malformed is not None:
+        res["malformed"] = malformed
     print(json.dumps(res), flush=True)
 
 

@@ -61,7 +61,7 @@ struct ParseOption {  // frame.rs:47-50 (+ the NEXG_PARSE_VLAN extension, off by
     }
 };
 
-enum class ParseErrorKind : uint8_t {  // parse.rs:51-97 (kinds; context strings are not carried)
+enum class ParseErrorKind : uint8_t {  // parse.rs:51-97
     BufferTooShort = NEXG_ERR_BUFFER_TOO_SHORT,
     InvalidLength = NEXG_ERR_INVALID_LENGTH,
     Malformed = NEXG_ERR_MALFORMED,
@@ -69,8 +69,14 @@ enum class ParseErrorKind : uint8_t {  // parse.rs:51-97 (kinds; context strings
     BadExtent = NEXG_ERR_BAD_EXTENT,  // caller error: frame longer than 65535 bytes
 };
 
+// The reference's ParseError with its payload (parse.rs:53-81), carried in
+// the failed frame's record (include/nexg.h NEXG_CTX_*): `context` is the
+// reference's context string; minimum / actual (BufferTooShort), value
+// (InvalidLength), expected / actual (Truncated).
 struct ParseError {
     ParseErrorKind kind;
+    const char* context = nullptr;
+    size_t minimum = 0, actual = 0, value = 0, expected = 0;
     const char* name() const {
         switch (kind) {
             case ParseErrorKind::BufferTooShort: return "BufferTooShort";
@@ -79,6 +85,24 @@ struct ParseError {
             case ParseErrorKind::Truncated: return "Truncated";
             default: return "BadExtent";
         }
+    }
+    static const char* context_of(uint32_t ctx) {
+        static const char* const k[] = {nullptr, "Ethernet packet", "Frame dummy Ethernet classification",
+                                        "IPv4 packet", "IPv4 packet version", "IPv4 header length", "IPv4 header",
+                                        "IPv4 total length", "IPv4 options", "IPv4 option length", "IPv6 packet",
+                                        "IPv6 packet version", "IPv6 payload", "IPv6 extension header",
+                                        "IPv6 routing header", "IPv6 fragment header"};
+        return ctx < sizeof(k) / sizeof(k[0]) ? k[ctx] : nullptr;
+    }
+    // the error of a failed frame's NEXG_OUT_RECORD record
+    static ParseError from_record(const nexg_record& r) {
+        ParseError e{(ParseErrorKind)NEXG_STATUS(r.flags)};
+        if (e.kind == ParseErrorKind::BadExtent) return e;
+        e.context = context_of(r.l4_type);
+        if (e.kind == ParseErrorKind::BufferTooShort) { e.minimum = r.ip_src; e.actual = r.ip_dst; }
+        if (e.kind == ParseErrorKind::InvalidLength) e.value = r.ip_src;
+        if (e.kind == ParseErrorKind::Truncated) { e.expected = r.ip_src; e.actual = r.ip_dst; }
+        return e;
     }
 };
 
@@ -355,7 +379,7 @@ inline Result<Frame> frame_from_record(const nexg_record& r, const uint8_t* b, s
                                        const nexg_options& opts) {
     using namespace detail;
     const uint32_t f = r.flags;
-    if (NEXG_STATUS(f)) return ParseError{(ParseErrorKind)NEXG_STATUS(f)};
+    if (NEXG_STATUS(f)) return ParseError::from_record(r);
     if (r.payload_off + (size_t)r.payload_len > len || r.l3_off > len) throw Error("record does not fit its frame");
     Frame fr;
     const uint32_t l3 = r.l3_off;
@@ -446,6 +470,86 @@ inline Result<Frame> frame_from_record(const nexg_record& r, const uint8_t* b, s
                              r.l4_csum_calc};
     return fr;
 }
+
+/* ---- ICMP sub-message views (icmp.rs:434-700, icmpv6.rs echo) ---------------
+ * What examples/dump.rs:226-350 downcasts an IcmpPacket / Icmpv6Packet to.
+ * The packet comes from a Frame (Frame.ip.icmp + Frame.payload, which for
+ * ICMP is every byte after the 4-B header, Q15); each conversion applies the
+ * reference's type check and minimum payload and fails with its message. */
+struct IcmpPacket {  // icmp.rs:178-183
+    IcmpHeader header;
+    std::vector<uint8_t> payload;
+    size_t total_len() const { return 4 + payload.size(); }  // icmp.rs:241-243
+};
+struct Icmpv6Packet {  // icmpv6.rs:236-241
+    Icmpv6Header header;
+    std::vector<uint8_t> payload;
+    size_t total_len() const { return 4 + payload.size(); }
+};
+inline std::optional<IcmpPacket> icmp_packet(const Frame& f) {
+    if (!f.ip || !f.ip->icmp) return std::nullopt;
+    return IcmpPacket{*f.ip->icmp, f.payload};
+}
+inline std::optional<Icmpv6Packet> icmpv6_packet(const Frame& f) {
+    if (!f.ip || !f.ip->icmpv6) return std::nullopt;
+    return Icmpv6Packet{*f.ip->icmpv6, f.payload};
+}
+namespace icmp {
+template <uint8_t TYPE>
+struct EchoPacket {  // echo_request (icmp.rs:478-504) / echo_reply (icmp.rs:547-573)
+    IcmpHeader header;
+    uint16_t identifier = 0, sequence_number = 0;
+    std::vector<uint8_t> payload;
+    static Result<EchoPacket, const char*> try_from(const IcmpPacket& p) {
+        if (p.header.icmp_type != TYPE) return TYPE == 8 ? "Not an Echo Request" : "Not an Echo Reply";
+        if (p.payload.size() < 4) return TYPE == 8 ? "Payload too short for Echo Request" : "Payload too short for Echo Reply";
+        return EchoPacket{p.header, detail::be16(p.payload.data()), detail::be16(p.payload.data() + 2),
+                          std::vector<uint8_t>(p.payload.begin() + 4, p.payload.end())};
+    }
+};
+using EchoRequestPacket = EchoPacket<8>;
+using EchoReplyPacket = EchoPacket<0>;
+struct DestinationUnreachablePacket {  // icmp.rs:618-647
+    IcmpHeader header;
+    uint16_t unused = 0, next_hop_mtu = 0;
+    std::vector<uint8_t> payload;
+    static Result<DestinationUnreachablePacket, const char*> try_from(const IcmpPacket& p) {
+        if (p.header.icmp_type != 3) return "Not a Destination Unreachable";
+        if (p.payload.size() < 4) return "Payload too short for Destination Unreachable";
+        return DestinationUnreachablePacket{p.header, detail::be16(p.payload.data()), detail::be16(p.payload.data() + 2),
+                                            std::vector<uint8_t>(p.payload.begin() + 4, p.payload.end())};
+    }
+};
+struct TimeExceededPacket {  // icmp.rs:664-699
+    IcmpHeader header;
+    uint32_t unused = 0;
+    std::vector<uint8_t> payload;
+    static Result<TimeExceededPacket, const char*> try_from(const IcmpPacket& p) {
+        if (p.header.icmp_type != 11) return "Not a Time Exceeded";
+        if (p.payload.size() < 4) return "Payload too short for Time Exceeded";
+        const uint32_t u = ((uint32_t)detail::be16(p.payload.data()) << 16) | detail::be16(p.payload.data() + 2);
+        return TimeExceededPacket{p.header, u, std::vector<uint8_t>(p.payload.begin() + 4, p.payload.end())};
+    }
+};
+}  // namespace icmp
+namespace icmpv6 {
+template <uint8_t TYPE>
+struct EchoPacket {  // echo_request (icmpv6.rs:2268-2294) / echo_reply (2427-2453): 8-B minimum
+    Icmpv6Header header;
+    uint16_t identifier = 0, sequence_number = 0;
+    std::vector<uint8_t> payload;
+    static Result<EchoPacket, const char*> try_from(const Icmpv6Packet& p) {
+        if (p.header.icmpv6_type != TYPE)
+            return TYPE == 128 ? "Not an Echo Request packet" : "Not an Echo Reply packet";
+        if (p.payload.size() < 8) return TYPE == 128 ? "Payload too short for Echo Request" : "Payload too short for Echo Reply";
+        return EchoPacket{p.header, detail::be16(p.payload.data()), detail::be16(p.payload.data() + 2),
+                          std::vector<uint8_t>(p.payload.begin() + 4, p.payload.end())};
+    }
+    size_t total_len() const { return 8 + payload.size(); }
+};
+using EchoRequestPacket = EchoPacket<128>;
+using EchoReplyPacket = EchoPacket<129>;
+}  // namespace icmpv6
 
 /* ---- the engine --------------------------------------------------------- */
 

@@ -491,8 +491,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 // sub-tile k also retires every lookup into sub-tile k-2's buffer (3 barriers
 // per sub-tile, 41 KB LDS); NB = 1: one buffer and a 4th barrier (21 KB LDS,
 // more workgroups per CU).
-template <int OUT, int NB = 1, uint32_t SUB = 16384>
-__global__ __launch_bounds__(256) void k_parse_span(ParseArgs a) {
+template <int OUT, int NB = 1, uint32_t SUB = 16384, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_parse_span(ParseArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t s_bytes[NB][SUB];
     __shared__ __attribute__((aligned(16))) uint32_t s_pfx[NB][(SUB / 16u) + 4];  // [1024] = total
     __shared__ uint32_t s_wsum[NB][4];

@@ -39,9 +39,20 @@ class ParseOption:
 
 
 class ParseError(Exception):
-    """parse.rs:51-97 (kind only; the reference's context strings are not
-    carried across the batch boundary)."""
+    """parse.rs:51-97. The record of a failed frame carries the error's payload
+    (include/nexg.h NEXG_CTX_*): `context` is the reference's context string;
+    BufferTooShort has minimum / actual, InvalidLength value, Truncated
+    expected / actual."""
     kind = None
+    fields = ()
+
+    def __init__(self, msg="", context=None, a=0, b=0):
+        super().__init__(msg)
+        self.context = context
+        names = {1: ("minimum", "actual"), 2: ("value",), 4: ("expected", "actual")}.get(self.kind, ())
+        for n, v in zip(names, (a, b)):
+            setattr(self, n, v)
+        self.fields = names
 
 
 class BufferTooShort(ParseError):
@@ -67,8 +78,17 @@ class BadExtent(ParseError):
 _ERRORS = {c.kind: c for c in (BufferTooShort, InvalidLength, Malformed, Truncated, BadExtent)}
 
 
-def parse_error(kind: int) -> ParseError:
-    return _ERRORS.get(kind, ParseError)(f"ParseError kind {kind}")
+def parse_error(kind: int, rec=None) -> ParseError:
+    """The ParseError of a failed frame; with its record, the payload too."""
+    cls = _ERRORS.get(kind, ParseError)
+    if rec is None or kind == abi.ERR_BAD_EXTENT:
+        return cls(f"ParseError kind {kind}")
+    ctx = abi.ERR_CONTEXTS[int(rec["l4_type"])] if int(rec["l4_type"]) < len(abi.ERR_CONTEXTS) else None
+    e = cls(f"{cls.__name__} {{ context: {ctx!r} }}", ctx, int(rec["ip_src"]), int(rec["ip_dst"]))
+    if e.fields:
+        e.args = (f"{cls.__name__} {{ context: {ctx!r}, " +
+                  ", ".join(f"{n}: {getattr(e, n)}" for n in e.fields) + " }",)
+    return e
 
 
 # ---- headers (field names follow the reference structs) ------------------
@@ -275,7 +295,7 @@ def frame_from_record(rec, frame: bytes, options=None) -> Frame:
     flags = int(rec["flags"])
     st = (flags >> abi.STATUS_SHIFT) & 7
     if st:
-        raise parse_error(st)
+        raise parse_error(st, rec)
     b = frame
     l3 = int(rec["l3_off"])
     eth = None

@@ -1,0 +1,114 @@
+"""The SURVEY.md Appendix C malformed mix, for measuring the parse path's
+fallback cost (bench.py --workload malformed).
+
+Frames start as the IMIX generator's (nexg_gen_frames on the device), then
+half of them get one structural mutation, drawn and applied with vectorised
+numpy on the host so the mix is deterministic (seeded) and fast to build:
+truncation, Ethernet padding, a random IPv4 total length / IPv6 payload
+length, a random version/IHL byte, random UDP / TCP length fields, an IPv6
+hop-by-hop header, an 802.1Q tag, IP protocol 200 (-> Reserved), or random
+bytes. Mutated frames leave the canonical fast paths and run the generic
+parse core on the GPU; the result is a packed batch (offsets only).
+"""
+import numpy as np
+
+from . import abi
+
+MUTATIONS = ("truncate", "pad", "ip_length", "ver_ihl", "l4_length", "ipv6_hbh", "vlan", "proto200", "random")
+
+
+def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share: float = 0.5):
+    """(FrameBatch on the engine's device, dict of per-mutation counts)."""
+    import torch
+
+    from .engine import FrameBatch
+    base = engine.gen_batch(abi.WL_IMIX, count, seed=seed)
+    torch.cuda.synchronize(engine.torch_device)
+    offs = base.offsets.cpu().numpy().astype(np.int64)
+    data = base.data.cpu().numpy()[: offs[-1]]
+    lens = np.diff(offs)
+    rng = np.random.default_rng(seed)
+    kind = np.where(rng.random(count) < mutate_share, rng.integers(0, len(MUTATIONS), count), -1)
+    # per-frame byte edits on a copy of the frame bytes (lengths unchanged)
+    buf = data.copy()
+    eth_v4 = (buf[offs[:-1] + 12] == 0x08) & (buf[offs[:-1] + 13] == 0x00)
+    sel = lambda k: np.nonzero(kind == MUTATIONS.index(k))[0]
+    i = sel("ip_length")  # bytes 16..17 (IPv4 total length) / 18..19 (IPv6 payload length)
+    pos = offs[i] + np.where(eth_v4[i], 16, 18)
+    v = rng.integers(0, 1 << 16, len(i))
+    buf[pos], buf[pos + 1] = v >> 8, v & 0xFF
+    i = sel("ver_ihl")
+    buf[offs[i] + 14] = rng.integers(0, 256, len(i))
+    i = sel("l4_length")  # UDP length / TCP data offset / ICMP type area of a v4 or v6 frame
+    l4 = offs[i] + np.where(eth_v4[i], 34, 54)
+    buf[l4 + 4] = rng.integers(0, 256, len(i))
+    buf[l4 + 12] = rng.integers(0, 256, len(i))
+    i = sel("proto200")
+    buf[offs[i] + np.where(eth_v4[i], 23, 20)] = 200
+    i = sel("random")
+    for j in i:  # few enough frames to fill one at a time
+        buf[offs[j]:offs[j + 1]] = rng.integers(0, 256, lens[j], dtype=np.uint8)
+    # length-changing mutations: new lengths + inserted / appended bytes
+    new_len = lens.copy()
+    i = sel("truncate")
+    new_len[i] = (rng.random(len(i)) * lens[i]).astype(np.int64)
+    pad = np.zeros(count, np.int64)
+    i = sel("pad")
+    pad[i] = rng.integers(1, 64, len(i))
+    ins = np.zeros(count, np.int64)  # bytes inserted after byte 13 (VLAN) / 54 (IPv6 HBH)
+    ins[sel("vlan")] = 4
+    hbh = sel("ipv6_hbh")
+    hbh = hbh[~eth_v4[hbh]]
+    ins[hbh] = 8
+    new_len = new_len + pad + ins
+    new_offs = np.zeros(count + 1, np.int64)
+    np.cumsum(new_len, out=new_offs[1:])
+    out = np.zeros(int(new_offs[-1]), np.uint8)
+    plain = (ins == 0) & (pad == 0)
+    # frames without inserts: one gather of their (possibly truncated) bytes
+    src = np.repeat(offs[:-1][plain], new_len[plain]) + _ramp(new_len[plain])
+    dst = np.repeat(new_offs[:-1][plain], new_len[plain]) + _ramp(new_len[plain])
+    out[dst] = buf[src]
+    for j in np.nonzero(~plain)[0]:
+        f = buf[offs[j]:offs[j + 1]]
+        if pad[j]:
+            f = np.concatenate([f, rng.integers(0, 256, pad[j], dtype=np.uint8)])
+        elif ins[j] == 4:  # 802.1Q tag in front of the EtherType (frame[12:14])
+            f = np.concatenate([f[:12], np.array([0x81, 0, 0, 0x64], np.uint8), f[12:]])
+        elif ins[j] == 8:  # hop-by-hop header carrying the original next header
+            nh = f[20]
+            g = f.copy()
+            g[20] = 0
+            pl = ((int(g[18]) << 8) | int(g[19])) + 8
+            g[18], g[19] = pl >> 8, pl & 0xFF
+            f = np.concatenate([g[:54], np.array([nh, 0, 0, 0, 0, 0, 0, 0], np.uint8), g[54:]])
+        out[new_offs[j]:new_offs[j] + len(f)] = f
+    dev = torch.from_numpy(np.concatenate([out, np.zeros(16, np.uint8)])).to(engine.torch_device)
+    doffs = torch.from_numpy(new_offs).to(engine.torch_device)
+    counts = {m: int((kind == k).sum()) for k, m in enumerate(MUTATIONS)}
+    counts["unmodified"] = int((kind < 0).sum())
+    return FrameBatch(data=dev[: int(new_offs[-1])], count=count, offsets=doffs), counts
+
+
+def _ramp(lengths):
+    """[0..l0), [0..l1), ... concatenated (vectorised)."""
+    total = int(lengths.sum())
+    if total == 0:
+        return np.zeros(0, np.int64)
+    starts = np.repeat(np.cumsum(lengths) - lengths, lengths)
+    return np.arange(total, dtype=np.int64) - starts
+
+
+def tiled(batch, times: int):
+    """The packed batch repeated `times` times back to back on its device
+    (the bench's full-size malformed batch from a 1M-frame mix)."""
+    import torch
+
+    from .engine import FrameBatch
+    n, span = batch.count, int(batch.offsets[batch.count].item())
+    data = batch.data[:span].repeat(times)
+    base = batch.offsets[:n]
+    offs = torch.cat([base + k * span for k in range(times)] +
+                     [torch.tensor([times * span], dtype=base.dtype, device=base.device)])
+    pad = torch.zeros(16, dtype=data.dtype, device=data.device)
+    return FrameBatch(data=torch.cat([data, pad])[: times * span], count=n * times, offsets=offs)

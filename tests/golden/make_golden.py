@@ -153,7 +153,9 @@ ECHO6 = bytes([0x80, 0x00, 0xbe, 0xef, 0x12, 0x34, 0x56, 0x78]) + b"ping!"
 add("icmpv6_echo_request_parse", "icmpv6.rs:2531-2549 (type EchoRequest, code 0, checksum 0xbeef, "
     "id 0x1234, seq 0x5678, payload 'ping!')", eth(ipv6_hdr(ECHO6, 58), 0x86DD),
     {"layers": ["eth", "ip", "ipv6", "icmpv6"], "l4_type": 128, "l4_code": 0, "l4_csum": 0xbeef,
-     "payload": (bytes([0x12, 0x34, 0x56, 0x78]) + b"ping!").hex()},
+     "payload": (bytes([0x12, 0x34, 0x56, 0x78]) + b"ping!").hex(),
+     "view": {"kind": "Icmpv6EchoRequest", "identifier": 0x1234, "sequence_number": 0x5678,
+              "payload": b"ping!".hex()}},
     note="Frame.payload of ICMPv6 = bytes after the 4-B header (Q15): identifier, sequence, data")
 
 # ---- ipv4.rs:944-1204 ------------------------------------------------------
@@ -215,17 +217,24 @@ def ipv4_hdr(payload, proto, src=(10, 0, 0, 1), dst=(10, 0, 0, 2), ident=0):
 # icmp.rs:728-815: EchoReply / DestinationUnreachable / TimeExceeded messages
 # as the tests assemble them (checksum field left 0: the tests only assert the
 # fields and payloads below), carried as IPv4 protocol 1 in a Frame
-for name, cite, msg, typ, code, pl in (
+# "view": the sub-message the test downcasts to (icmp.rs:434-700) and the
+# fields it asserts (echo reply: identifier, sequence, payload; unreachable:
+# next_hop_mtu, payload; time exceeded: unused, payload)
+for name, cite, msg, typ, code, pl, view in (
         ("icmp_echo_reply_roundtrip", "icmp.rs:728-757 (id 5678, seq 99, payload 'pong')",
          bytes([0, 0, 0, 0, 0x16, 0x2e, 0x00, 0x63]) + b"pong", 0, 0,
-         bytes([0x16, 0x2e, 0x00, 0x63]) + b"pong"),
+         bytes([0x16, 0x2e, 0x00, 0x63]) + b"pong",
+         {"kind": "EchoReply", "identifier": 5678, "sequence_number": 99, "payload": b"pong".hex()}),
         ("icmp_destination_unreachable", "icmp.rs:759-787 (code 3, next_hop_mtu 1500, payload 'bad ip')",
-         bytes([3, 3, 0, 0, 0, 0, 0x05, 0xdc]) + b"bad ip", 3, 3, bytes([0, 0, 0x05, 0xdc]) + b"bad ip"),
+         bytes([3, 3, 0, 0, 0, 0, 0x05, 0xdc]) + b"bad ip", 3, 3, bytes([0, 0, 0x05, 0xdc]) + b"bad ip",
+         {"kind": "DestinationUnreachable", "next_hop_mtu": 1500, "payload": b"bad ip".hex()}),
         ("icmp_time_exceeded", "icmp.rs:789-815 (unused 0xdeadbeef, payload 'timeout')",
          bytes([11, 0, 0, 0, 0xde, 0xad, 0xbe, 0xef]) + b"timeout", 11, 0,
-         bytes([0xde, 0xad, 0xbe, 0xef]) + b"timeout")):
+         bytes([0xde, 0xad, 0xbe, 0xef]) + b"timeout",
+         {"kind": "TimeExceeded", "unused": 0xdeadbeef, "payload": b"timeout".hex()})):
     add(name, cite, eth(ipv4_hdr(msg, 1)),
-        {"layers": ["eth", "ip", "ipv4", "icmp"], "l4_type": typ, "l4_code": code, "payload": pl.hex()},
+        {"layers": ["eth", "ip", "ipv4", "icmp"], "l4_type": typ, "l4_code": code, "payload": pl.hex(),
+         "view": view},
         note="Frame.payload of ICMP = bytes after the 4-B header (Q15)")
 
 
@@ -244,7 +253,8 @@ add("udp_basic_parse", "udp.rs:510-527 (wrapped in Eth/IPv4)", eth(ipv4_hdr(UDP_
 ICMP_P = bytes([8, 0, 0x3a, 0xbc, 0x04, 0xd2, 0x00, 0x2a]) + b"ping"
 add("icmp_echo_request", "icmp.rs:708-725 (wrapped in Eth/IPv4)", eth(ipv4_hdr(ICMP_P, 1)),
     {"layers": ["eth", "ip", "ipv4", "icmp"], "l4_type": 8, "l4_code": 0, "l4_csum": 0x3ABC,
-     "payload": "04d2002a" + b"ping".hex()})
+     "payload": "04d2002a" + b"ping".hex(),
+     "view": {"kind": "EchoRequest", "identifier": 1234, "sequence_number": 42, "payload": b"ping".hex()}})
 
 # ---- bench fixtures (nex-packet/benches) -----------------------------------
 BENCH_V4_TCP = bytes([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 0x08, 0x00, 0x45, 0x00, 0x00, 0x30,

@@ -65,6 +65,20 @@ def check_expect(rec, frame: bytes, exp: dict, name="", reparse=None, parse_flag
         elif k in ("eth_dst", "eth_src"):
             e = fr.datalink.ethernet
             assert (e.destination if k == "eth_dst" else e.source).hex() == v, name
+        elif k == "view":  # the ICMP / ICMPv6 sub-message the reference test downcasts to
+            from nex_amd import views
+            kind = v["kind"]
+            if kind.startswith("Icmpv6"):
+                pkt = views.icmpv6_from_record(rec, frame)
+                m = views.Icmpv6EchoPacket.try_from(pkt, reply=kind == "Icmpv6EchoReply")
+            else:
+                m = views.icmp_message(views.icmp_from_record(rec, frame))
+                assert type(m).__name__ == kind + "Packet", (name, type(m).__name__)
+            for f, want in v.items():
+                if f == "kind":
+                    continue
+                got = getattr(m, f)
+                assert (got.hex() if isinstance(got, bytes) else got) == want, (name, f, got, want)
         elif k == "ip_csum_consistent":
             # ipv4.rs:1073-1095: the computed checksum written back into bytes
             # 10..11 makes a packet whose header verifies and whose bytes are

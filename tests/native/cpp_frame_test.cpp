@@ -95,6 +95,9 @@ int main(int argc, char** argv) {
         CHECK(f.datalink->ethernet->ethertype == 0x0800);
         const auto& s = got.at("ethernet_too_short");
         CHECK(s.is_err() && s.error().kind == ParseErrorKind::BufferTooShort);
+        // ethernet.rs:513-520: BufferTooShort { "Ethernet packet", minimum 14, actual 4 }
+        CHECK(s.error().context && std::string(s.error().context) == "Ethernet packet");
+        CHECK(s.error().minimum == 14 && s.error().actual == 4);
         const Frame& u = frame("ethernet_unknown_ethertype_dead");
         CHECK(u.datalink->ethernet->ethertype == 0xdead && !u.ip);
     }
@@ -109,6 +112,26 @@ int main(int argc, char** argv) {
         CHECK(e.ip->icmpv6->checksum == 0xbeef);
         CHECK(e.payload.size() == 9 && e.payload[0] == 0x12 && e.payload[1] == 0x34 && e.payload[2] == 0x56 &&
               e.payload[3] == 0x78 && e.payload[4] == 'p');
+        // icmpv6.rs:2531-2549: EchoRequestPacket id 0x1234, seq 0x5678, payload "ping!"
+        const auto er = icmpv6::EchoRequestPacket::try_from(*icmpv6_packet(e));
+        CHECK(er.is_ok() && er.value().identifier == 0x1234 && er.value().sequence_number == 0x5678);
+        CHECK(er.is_ok() && er.value().payload == bytes("ping!"));
+        CHECK(icmpv6::EchoReplyPacket::try_from(*icmpv6_packet(e)).is_err());
+    }
+    {  // icmp.rs:708-815: the sub-message views dump.rs downcasts to
+        const auto rq = icmp::EchoRequestPacket::try_from(*icmp_packet(frame("icmp_echo_request")));
+        CHECK(rq.is_ok() && rq.value().identifier == 1234 && rq.value().sequence_number == 42);
+        CHECK(rq.is_ok() && rq.value().payload == bytes("ping") && rq.value().header.checksum == 0x3abc);
+        const auto rp = icmp::EchoReplyPacket::try_from(*icmp_packet(frame("icmp_echo_reply_roundtrip")));
+        CHECK(rp.is_ok() && rp.value().identifier == 5678 && rp.value().sequence_number == 99);
+        CHECK(rp.is_ok() && rp.value().payload == bytes("pong"));
+        const auto du = icmp::DestinationUnreachablePacket::try_from(*icmp_packet(frame("icmp_destination_unreachable")));
+        CHECK(du.is_ok() && du.value().next_hop_mtu == 1500 && du.value().payload == bytes("bad ip"));
+        const auto te = icmp::TimeExceededPacket::try_from(*icmp_packet(frame("icmp_time_exceeded")));
+        CHECK(te.is_ok() && te.value().unused == 0xdeadbeefu && te.value().payload == bytes("timeout"));
+        CHECK(icmp::TimeExceededPacket::try_from(*icmp_packet(frame("icmp_echo_request"))).is_err());
+        CHECK(std::string(icmp::EchoReplyPacket::try_from(*icmp_packet(frame("icmp_echo_request"))).error()) ==
+              "Not an Echo Reply");
     }
     {  // frame.rs:665-680 unknown EtherType keeps the payload
         const Frame& f = frame("unknown_ethertype_keeps_payload");
@@ -148,6 +171,7 @@ int main(int argc, char** argv) {
     {  // ipv4.rs:1176-1204 strict truncation is an error, lenient is not; zero total length
         const auto& s = got.at("ipv4_strict_truncation");
         CHECK(s.is_err() && s.error().kind == ParseErrorKind::Truncated);
+        CHECK(std::string(s.error().context) == "IPv4 packet" && s.error().expected == 40 && s.error().actual == 24);
         CHECK(frame("ipv4_lenient_truncation").ip->ipv4->total_length == 24);
         const Frame& z = frame("ipv4_zero_total_length");
         CHECK(z.ip->ipv4->total_length == 24);

@@ -1,0 +1,58 @@
+"""GPU: the bench's malformed mix (nex_amd/workloads.py)
+parses to exactly the oracle's records in every output kind, and its tiled
+full-size form repeats the per-copy results."""
+import numpy as np
+import pytest
+
+from nex_amd import abi, workloads
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mix(engine):
+    return workloads.malformed_mix(engine, 60000, seed=77)
+
+
+def host_frames(batch):
+    offs = batch.offsets.cpu().numpy().astype(np.int64)
+    data = batch.data.cpu().numpy()
+    return [bytes(data[a:b]) for a, b in zip(offs[:-1], offs[1:])]
+
+
+def test_mix_shape(mix):
+    batch, counts = mix
+    assert sum(counts.values()) == batch.count == 60000
+    assert 0.45 < counts["unmodified"] / batch.count < 0.55
+    assert all(counts[m] > 2000 for m in workloads.MUTATIONS)
+
+
+def test_malformed_mix_matches_oracle(engine, oracle, mix):
+    batch, _ = mix
+    frames = host_frames(batch)
+    want = oracle.parse_frames(frames)
+    got = engine.parse_to_numpy(batch, out_kind=abi.OUT_RECORD)
+    helpers.records_equal(got, want, frames, "malformed mix record")
+    d = np.zeros(len(frames), abi.DESC_DTYPE)
+    for n in abi.DESC_DTYPE.names:
+        d[n] = want[n]
+    got = engine.parse_to_numpy(batch, out_kind=abi.OUT_SPARSE)
+    helpers.records_equal(got, d, frames, "malformed mix sparse")
+    # the mutations reach the error paths, not only the fast shapes
+    assert ((want["flags"] >> abi.STATUS_SHIFT) != 0).mean() > 0.1
+
+
+def test_tiled_repeats(engine, mix):
+    import torch
+    batch, _ = mix
+    t = workloads.tiled(batch, 3)
+    one = engine.parse(batch, out_kind=abi.OUT_DESC)[: batch.count * 8]
+    three = engine.parse(t, out_kind=abi.OUT_DESC)[: t.count * 8]
+    torch.cuda.synchronize()
+    span = int(batch.offsets[batch.count].item())
+    d1 = one.cpu().numpy().view(abi.DESC_DTYPE)
+    d3 = three.cpu().numpy().view(abi.DESC_DTYPE)
+    for k in range(3):
+        assert (d3[k * batch.count:(k + 1) * batch.count] == d1).all()
+    assert int(t.offsets[-1].item()) == 3 * span
