@@ -191,6 +191,42 @@ struct WinFrame {
     }
 };
 
+// k_parse_span's generic path: frame bytes [0, 64) in a per-lane LDS slot
+// (frame-relative, byte i at slot[i], zero past len), the rest in HBM, and the
+// absolute-parity sum of [80, len) already known from the span prefix scan
+// (tail; only meaningful when len > 80). A checksum range that runs to the
+// frame end (the usual L4 case) costs no HBM reads past byte 80.
+struct SpanFrame {
+    NEXG_NO_DEFER
+    static constexpr uint32_t kSlot = 64;
+    const uint8_t* slot;
+    const uint8_t* g;
+    uint32_t len;
+    uint32_t parity;  // absolute-address parity of byte 0
+    uint32_t tail;
+
+    NEXG_HD uint32_t u8(uint32_t i) const { return i < kSlot ? (uint32_t)slot[i] : (uint32_t)g[i]; }
+    NEXG_HD uint64_t le_sum(uint32_t a, uint32_t b) const {
+        uint64_t acc = 0;
+        const uint32_t lb = b < kSlot ? b : kSlot;
+        if (a < lb) {  // frame-relative LE sum, x256 for an odd frame (congruent, 0 iff 0)
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(slot);
+            uint32_t s = 0;
+            for (uint32_t j = a & ~3u; j < lb; j += 4) s += halves(w[j >> 2] & range_mask(j, a, lb));
+            acc = parity ? (uint64_t)s * 256u : (uint64_t)s;
+        }
+        const uint32_t ga = a > kSlot ? a : kSlot;
+        const bool to_end = b == len && len > 80u && ga <= 80u;
+        const uint32_t gb = to_end ? 80u : b;
+        if (ga < gb) {
+            const uint64_t base = reinterpret_cast<uint64_t>(g);
+            acc += global_le_sum(base + ga, base + gb);
+        }
+        if (to_end) acc += tail;
+        return acc;
+    }
+};
+
 // ---- L4 ------------------------------------------------------------------
 
 // frame.rs:550-568 + udp.rs:197-236 (try_from_bytes) + udp.rs:443-505.
@@ -536,9 +572,11 @@ NEXG_HD bool fast_udp4_64(const uint32_t (&w)[16], uint32_t opt_flags, nexg_reco
 // Canonical-shape fast path for the IMIX mix: {IPv4 IHL 5, IPv6 without
 // extension headers} x {TCP data offset 5, UDP, ICMP/ICMPv6}, with the IP and
 // UDP lengths exactly covering the frame (no padding). w[k] holds bytes
-// 4k..4k+3 of the frame (little-endian), already zero past `len`; the frame
-// starts at an even address; tail_sum is the little-endian sum of bytes
-// [80, len) (0 when len <= 80). One straight-line routine for all six shapes
+// 4k..4k+3 of the frame (little-endian), already zero past `len`; tail_sum
+// is the frame-relative little-endian halfword sum of bytes [80, len) (even
+// frame offsets weigh 1, odd 256; 0 when len <= 80) or any value congruent to
+// it mod 0xFFFF that is 0 only when it is (callers holding an absolute-parity
+// sum of a frame at an odd address pass it x256). One straight-line routine for all six shapes
 // (selects, no per-shape branches) so a mixed wave does not diverge. Returns
 // false when any condition fails; the caller then runs parse_frame, so the
 // result never depends on which path ran. tests/test_core_harness.py checks it.

@@ -9,6 +9,7 @@
 namespace nexg {
 
 constexpr uint32_t kTile = 256;
+constexpr uint32_t kApron = 96;  // k_parse_span: bytes of the previous sub-tile kept in front
 
 // Frame read entirely from HBM (checksum utility path).
 struct GlobalFrame {
@@ -426,17 +427,31 @@ __global__ __launch_bounds__(256) void k_parse_lane80(ParseArgs a) {
     const uint64_t abs = reinterpret_cast<uint64_t>(a.data) + off;
     const uint64_t dend = reinterpret_cast<uint64_t>(a.data) + a.data_bytes;
     bool done = !ext;
-    if (ext && (abs & 3u) == 0 && abs + kLaneWin <= dend) {
+    if (ext && abs + kLaneWin <= dend) {
+        // six 16-B aligned loads cover [abs, abs + 84) at any alignment (the
+        // sixth only while it still overlaps the batch bytes); realigned by
+        // dword selects (q) and v_alignbyte (byte shift)
         const uint32_t tail = len > kLaneWin ? *handoff_slot<OUT>(a, idx) : 0u;
+        const uint64_t a16 = abs & ~15ull;
+        const uint32_t q = (uint32_t)(abs >> 2) & 3u, sh = (uint32_t)abs & 3u;
+        uint32_t u[24];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const uint4 v = (k < 5 || a16 + 80u < dend) ? load16<true>(reinterpret_cast<const void*>(a16 + 16u * k))
+                                                        : make_uint4(0, 0, 0, 0);
+            u[4 * k] = v.x; u[4 * k + 1] = v.y; u[4 * k + 2] = v.z; u[4 * k + 3] = v.w;
+        }
+        uint32_t d[21];
+#pragma unroll
+        for (int j = 0; j < 21; j++) d[j] = q == 0 ? u[j] : q == 1 ? u[j + 1] : q == 2 ? u[j + 2] : u[j + 3];
         uint32_t w[20];
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const uint4 v = load16a4<true>(reinterpret_cast<const void*>(abs + 16u * k));
-            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+        for (int k = 0; k < 20; k++) {
+            const uint32_t v = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+            w[k] = 4u * k < len ? (v & range_mask(4u * k, 0, len)) : 0u;
         }
-#pragma unroll
-        for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
-        done = fast_canonical80(w, len, a.opt_flags, tail, r);
+        // k_tail_sums weights by absolute parity (see k_parse_span)
+        done = fast_canonical80(w, len, a.opt_flags, (uint64_t)tail << (8u * (sh & 1u)), r);
     }
     if (!done) {
         GlobalFrame f{a.data + off};
@@ -493,7 +508,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 // more workgroups per CU).
 template <int OUT, int NB = 1, uint32_t SUB = 16384, int WPE = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_parse_span(ParseArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[NB][SUB];
+    // each stage buffer: [96-B apron | SUB bytes | 96-B pad]; the apron holds
+    // the previous sub-tile's last 96 bytes, so a head window that starts
+    // there is read in the sub-tile where it ends (one gather, no straddle)
+    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[NB][kApron + SUB + kApron];
     __shared__ __attribute__((aligned(16))) uint32_t s_pfx[NB][(SUB / 16u) + 4];  // [1024] = total
     __shared__ uint32_t s_wsum[NB][4];
     __shared__ uint64_t s_span[2];
@@ -532,11 +550,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // span-relative positions: head, tail start (head + 80), end
     const uint32_t hr = (uint32_t)(base + off - A0);
     const bool want_tail = have && len > kLaneWin;
-    const bool fast = have && ((base + off) & 3u) == 0 && !(a.opt_flags & NEXG_PARSE_FROM_IP);
+    // every frame's head window is gathered (any byte alignment: 21 aligned
+    // LDS dwords, realigned by v_alignbyte after the loop); fast_canonical80
+    // itself declines FROM_IP. One generic call site below: a second parse_frame
+    // instance on another branch costs 15 VGPRs (6 -> 5 waves/SIMD).
+    const bool fast = have;
+    const uint32_t sh = (uint32_t)((base + off) & 3u);
     uint32_t qa = 0, qb = 0, run = 0;
-    uint32_t w[20];
+    uint32_t u[21];
 #pragma unroll
-    for (int j = 0; j < 20; j++) w[j] = 0;
+    for (int j = 0; j < 21; j++) u[j] = 0;
 
     constexpr int CPT = SUB / 4096u;  // 16-B chunks per thread per sub-tile
     uint4 cur[CPT];
@@ -550,9 +573,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     fetch(0, cur);
     uint32_t buf = 0;
     for (uint32_t S = 0; S < span; S += SUB, buf = NB == 2 ? buf ^ 1u : 0u) {
-        uint8_t* sb = s_bytes[buf];
+        uint8_t* sb = s_bytes[buf] + kApron;
         uint32_t* sp = s_pfx[buf];
-        // (1) stage bytes + chunk sums, put the next sub-tile in flight
+        // (1) stage bytes + chunk sums, put the next sub-tile in flight. The
+        // threads owning the last 6 chunks first move the previous sub-tile's
+        // (NB = 1: this buffer's, before they overwrite it) into the apron.
+        if (S > 0 && t >= kTile - kApron / 16u) {
+            const uint8_t* prev = s_bytes[NB == 2 ? buf ^ 1u : buf] + kApron + SUB - kApron;
+            *reinterpret_cast<uint4*>(sb - kApron + 16u * (t - (kTile - kApron / 16u))) =
+                *reinterpret_cast<const uint4*>(prev + 16u * (t - (kTile - kApron / 16u)));
+        }
 #pragma unroll
         for (int i = 0; i < CPT; i++) {
             const uint32_t c = t + 256u * i;
@@ -590,40 +620,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const uint32_t da = hr + kLaneWin - S, db = hr + len - S;  // wrap: < 0 -> huge
         if (want_tail && (da < SUB || (last && da == SUB))) qa = q_at(da);
         if (have && (db < SUB || (last && db == SUB))) qb = q_at(db);
-        const uint32_t dh = hr - S;
-        if (fast) {
-            if (dh <= SUB - kLaneWin) {  // whole window in this sub-tile (the usual case)
+        // 84-B dword-aligned head window [dh, dh + 84): gathered exactly once,
+        // in the first sub-tile that holds all of it (apron included: dh >= -80),
+        // or in the last one (bytes past the span end are masked by len)
+        const int dh = (int)((hr & ~3u) - S);
+        if (fast && dh >= -(int)kLaneWin && (dh <= (int)(SUB - kLaneWin - 4u) || (last && dh < (int)SUB))) {
 #pragma unroll
-                for (int j = 0; j < 20; j++) w[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4u * j);
-            } else if (dh < SUB || dh + kLaneWin - 1u < kLaneWin - 1u) {  // straddles a sub-tile edge
-#pragma unroll
-                for (int j = 0; j < 20; j++) {
-                    const uint32_t d = dh + 4u * j;
-                    if (d < SUB) w[j] = *reinterpret_cast<const uint32_t*>(sb + d);
-                }
-            }
+            for (int j = 0; j < 21; j++) u[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4 * j);
         }
         run += total;
         if (NB == 1) __syncthreads();
     }
+    if (NB == 2) __syncthreads();  // the stage buffers become per-lane slots below
     if (have) {
-        bool done = false;
         if (fast) {
+            uint32_t w[20];
 #pragma unroll
-            for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
-            done = fast_canonical80(w, len, a.opt_flags, want_tail ? (uint32_t)(qb - qa) : 0u, r);
-        }
-        if (!done) {
-            GlobalFrame f{a.data + off};
-            parse_frame(f, (uint32_t)((base + off) & 1u), len, a.opt_flags, a.ip_offset, r);
+            for (int k = 0; k < 20; k++) {
+                const uint32_t v = __builtin_amdgcn_alignbyte(u[k + 1], u[k], sh);
+                w[k] = 4u * k < len ? (v & range_mask(4u * k, 0, len)) : 0u;
+            }
+            // Q weights bytes by absolute parity; fast_canonical80 wants the
+            // frame-relative LE sum: x256 (mod 0xFFFF) for a frame at an odd address
+            const uint32_t tq = want_tail ? qb - qa : 0u;
+            const uint64_t tail = (sh & 1u) ? (uint64_t)tq * 256u : (uint64_t)tq;
+            if (!fast_canonical80(w, len, a.opt_flags, tail, r)) {
+                // generic core on the window (64-B LDS slot) + the scanned tail sum
+                uint8_t* slot = &s_bytes[0][0] + 64u * t;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    reinterpret_cast<uint4*>(slot)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+                SpanFrame f{slot, a.data + off, len, sh & 1u, tq};
+                parse_frame(f, sh & 1u, len, a.opt_flags, a.ip_offset, r);
+            }
         }
     }
     if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
     if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the (now idle) byte buffer
         static_assert(OUT != NEXG_OUT_RECORD || NB * SUB >= kTile * 64u, "record staging needs 16 KiB");
         uint8_t* stage = &s_bytes[0][0];
-        if (NB == 2) __syncthreads();
-        if (have) stage_record(stage + 64u * t, r);
+        if (have) stage_record(stage + 64u * t, r);  // this lane's own slot
         __syncthreads();
         copy_out_records<64>(stage, a.out, f0, nf);
     }

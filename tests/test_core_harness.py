@@ -114,6 +114,13 @@ def test_canonical_fast_path_on_imix(oracle):
         want = oracle.parse_packed(buf, offs, lens, flags=flags)
         got = harness.parse_packed(buf, offs, lens, flags=flags, use_fast=4)
         helpers.records_equal(got, want, frames, f"canonical flags={flags}")
+    # k_parse_span's arithmetic at every byte alignment (odd frames: x256
+    # tail for the fast path, SpanFrame for the declined ones)
+    for shift in (1, 2, 3):
+        buf, offs, lens = pack(frames, 1, shift)
+        want = oracle.parse_packed(buf, offs, lens)
+        got = harness.parse_packed(buf, offs, lens, use_fast=5)
+        helpers.records_equal(got, want, frames, f"span arithmetic shift={shift}")
 
 
 @pytest.mark.parametrize("flags,ipo", [(0, 0), (abi.PARSE_FROM_IP, 14), (abi.PARSE_FROM_IP, 0),

@@ -39,8 +39,11 @@ def test_malformed_mix_matches_oracle(engine, oracle, mix):
         d[n] = want[n]
     got = engine.parse_to_numpy(batch, out_kind=abi.OUT_SPARSE)
     helpers.records_equal(got, d, frames, "malformed mix sparse")
-    # the mutations reach the error paths, not only the fast shapes
-    assert ((want["flags"] >> abi.STATUS_SHIFT) != 0).mean() > 0.1
+    # the mutations leave the canonical shapes (exception slots) and reach
+    # the error statuses (lenient parsing turns most into shorter layer stacks)
+    codes = engine.parse(batch, out_kind=abi.OUT_SPARSE)[: batch.count].cpu().numpy()
+    assert (codes == 0).mean() > 0.05
+    assert ((want["flags"] >> abi.STATUS_SHIFT) != 0).sum() > 100
 
 
 def test_tiled_repeats(engine, mix):

@@ -134,3 +134,35 @@ def test_monotone_hint_matches_twopass(engine, oracle):
                    lengths=lt[torch.from_numpy(perm).cuda()], hints=abi.FRAMES_MONOTONE)
     got = engine.parse_to_numpy(b, out_kind=abi.OUT_RECORD)
     helpers.records_equal(got, want[perm], [frames[i] for i in perm], "scattered with hint")
+
+
+@pytest.mark.parametrize("out_kind", [abi.OUT_RECORD, abi.OUT_SPARSE])
+def test_unaligned_frames_take_fast_path_bit_exact(engine, oracle, out_kind):
+    """Canonical IMIX frames at every byte alignment (0-3 byte gaps, offsets +
+    lengths + monotone hint -> span kernel; without the hint -> two-pass), a
+    share with a corrupted payload byte so both checksum verdicts occur, and
+    windows straddling 16-KiB sub-tile edges: records equal the oracle's."""
+    import torch
+    rng = np.random.default_rng(99)
+    frames = [bytearray(oracle.gen_frame(abi.WL_IMIX, i)) for i in range(30000)]
+    for i in rng.choice(len(frames), 3000, replace=False):
+        f = frames[i]
+        f[int(rng.integers(40, len(f)))] ^= 0x5A
+    frames = [bytes(f) for f in frames]
+    gaps = rng.integers(0, 4, len(frames))
+    blob, offs = bytearray(), []
+    for f, g in zip(frames, gaps):
+        blob += bytes(int(g))
+        offs.append(len(blob))
+        blob += f
+    data = torch.frombuffer(bytes(blob) + bytes(16), dtype=torch.uint8).cuda()
+    ot = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    lt = torch.tensor([len(f) for f in frames], dtype=torch.int32, device="cuda")
+    want = oracle.parse_frames(frames)
+    assert ((want["flags"] & abi.C_L4_OK) == 0).sum() > 1000
+    if out_kind == abi.OUT_SPARSE:
+        want = desc_of(want)
+    for hints in (abi.FRAMES_MONOTONE, 0):
+        b = FrameBatch(data=data, count=len(frames), offsets=ot, lengths=lt, hints=hints)
+        got = engine.parse_to_numpy(b, out_kind=out_kind)
+        helpers.records_equal(got, want, frames, f"unaligned hints={hints} out={out_kind}")

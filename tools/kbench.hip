@@ -302,6 +302,7 @@ int main(int argc, char** argv) {
         ivars.push_back({"imix_sparse_span2_8k_nb2", [=]() { hipLaunchKernelGGL((k_parse_span2<NEXG_OUT_SPARSE, 8192, 2>), grid, blk, 0, 0, sa); }, ibytes});
         ivars.push_back({"imix_sparse_span_v1", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1>), grid, blk, 0, 0, sa); }, ibytes});
         ivars.push_back({"imix_sparse_span_v1_w7", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 16384, 7>), grid, blk, 0, 0, sa); }, ibytes});
+        ivars.push_back({"imix_sparse_span_v1_w6", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 16384, 6>), grid, blk, 0, 0, sa); }, ibytes});
     }
     ivars.push_back({"imix_span_nb1_8k", iparse(k_parse_span<NEXG_OUT_DESC, 1, 8192>), ibytes});
     ivars.push_back({"imix_span_nb2_8k", iparse(k_parse_span<NEXG_OUT_DESC, 2, 8192>), ibytes});
