@@ -195,15 +195,31 @@ struct WinFrame {
 // (frame-relative, byte i at slot[i], zero past len), the rest in HBM, and the
 // absolute-parity sum of [80, len) already known from the span prefix scan
 // (tail; only meaningful when len > 80). A checksum range that runs to the
-// frame end (the usual L4 case) costs no HBM reads past byte 80.
+// frame end (the usual L4 case) costs no HBM reads past byte 80. Any other
+// HBM range longer than kDefer bytes (padded frames: the L4 range ends at the
+// IP length) is deferred: le_sum leaves it out and records it, note_mult /
+// note_finish record its multiplier and the checksum it feeds, and the caller
+// adds the range sum afterwards (the kernel: one wave-wide coalesced pass per
+// deferred lane; the host harness: global_le_sum) through span_patch.
+struct SpanDeferred {  // 3 dwords: it is live through the whole generic parse
+    uint32_t rng = 0;   // frame offset of the range | bytes << 16 (0: nothing deferred)
+    uint32_t t = 0;     // the checksum sum without the range, end-around folded
+    uint32_t meta = 0;  // stored checksum | which << 16 (0: no checksum took it) | (mult == 256) << 18
+    NEXG_HD uint32_t which() const { return (meta >> 16) & 3u; }
+    NEXG_HD uint32_t off() const { return rng & 0xFFFFu; }
+    NEXG_HD uint32_t bytes() const { return rng >> 16; }
+};
+
 struct SpanFrame {
-    NEXG_NO_DEFER
     static constexpr uint32_t kSlot = 64;
+    static constexpr uint32_t kDefer = 64;
     const uint8_t* slot;
     const uint8_t* g;
     uint32_t len;
     uint32_t parity;  // absolute-address parity of byte 0
     uint32_t tail;
+    mutable SpanDeferred d{};
+    mutable bool pend = false;
 
     NEXG_HD uint32_t u8(uint32_t i) const { return i < kSlot ? (uint32_t)slot[i] : (uint32_t)g[i]; }
     NEXG_HD uint64_t le_sum(uint32_t a, uint32_t b) const {
@@ -220,12 +236,41 @@ struct SpanFrame {
         const uint32_t gb = to_end ? 80u : b;
         if (ga < gb) {
             const uint64_t base = reinterpret_cast<uint64_t>(g);
-            acc += global_le_sum(base + ga, base + gb);
+            if (gb - ga > kDefer && d.rng == 0) {
+                d.rng = ga | (gb - ga) << 16;
+                pend = true;
+            } else {
+                acc += global_le_sum(base + ga, base + gb);
+            }
         }
         if (to_end) acc += tail;
         return acc;
     }
+    NEXG_HD void note_mult(uint32_t m) const {
+        if (pend) d.meta = (m == 256u ? 1u : 0u) << 18 | 1u << 20;  // bit 20: multiplier known
+        pend = false;
+    }
+    NEXG_HD void note_finish(uint64_t t, uint32_t stored, uint32_t which) const {
+        if ((d.meta >> 20) && !d.which()) {
+            t = (t & 0xFFFFFFFFull) + (t >> 32);  // congruent mod 0xFFFF, 0 iff t == 0
+            d.t = (uint32_t)((t & 0xFFFFFFFFull) + (t >> 32));
+            d.meta = (d.meta & (1u << 18)) | which << 16 | (stored & 0xFFFFu);
+        }
+    }
 };
+
+// finish a deferred checksum: range_sum = le_sum of frame bytes [d.off(), d.off() + d.bytes())
+NEXG_HD void span_patch(const SpanDeferred& d, uint64_t range_sum, nexg_record& r) {
+    const uint32_t calc = fold_complement((uint64_t)d.t + (((d.meta >> 18) & 1u) ? range_sum * 256u : range_sum));
+    const uint32_t stored = d.meta & 0xFFFFu;
+    if (d.which() == kCsumIp) {
+        r.ip_csum_calc = (uint16_t)calc;
+        r.flags = (r.flags & ~NEXG_C_IP_OK) | (calc == stored ? NEXG_C_IP_OK : 0u);
+    } else {
+        r.l4_csum_calc = (uint16_t)calc;
+        r.flags = (r.flags & ~NEXG_C_L4_OK) | (calc == stored ? NEXG_C_L4_OK : 0u);
+    }
+}
 
 // ---- L4 ------------------------------------------------------------------
 

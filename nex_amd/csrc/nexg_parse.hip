@@ -49,8 +49,8 @@ ParseVariant choose_parse_variant(const ParseArgs& a) {
 }
 
 // Span kernel generation: NEXG_SPAN=1 (4 barriers per 16-KiB sub-tile, the
-// default: measured best), 1w6 (the same capped at 80 VGPRs: 6 waves/SIMD,
-// small spill), 2 (2 barriers), 2d (8-KiB double-buffered
+// default: measured best), 1w1 (the same without the 6-waves/SIMD register
+// cap), 2 (2 barriers), 2d (8-KiB double-buffered
 // sub-tiles, 1 barrier). Fewer barriers measured slower (0.66 vs 0.73 of
 // peak, profiles/r02_kbench/): the per-group stream, not the barriers,
 // bounds the loop.
@@ -58,7 +58,7 @@ static int span_variant() {
     static const int v = [] {
         const char* e = getenv("NEXG_SPAN");
         if (!e) return 1;
-        return strcmp(e, "1") == 0 ? 1 : strcmp(e, "2d") == 0 ? 3 : strcmp(e, "1w6") == 0 ? 4 : 2;
+        return strcmp(e, "1") == 0 ? 1 : strcmp(e, "2d") == 0 ? 3 : strcmp(e, "1w1") == 0 ? 4 : 2;
     }();
     return v;
 }
@@ -78,8 +78,10 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             hipLaunchKernelGGL((k_parse<1, OUT, 0, 128>), grid, block, 0, s, a);
             break;
         case ParseVariant::SpanTile:
-            if (span_variant() == 1) hipLaunchKernelGGL((k_parse_span<OUT, 1>), grid, block, 0, s, a);
-            else if (span_variant() == 4) hipLaunchKernelGGL((k_parse_span<OUT, 1, 16384, 6>), grid, block, 0, s, a);
+            // 6 waves/SIMD (80 VGPRs): no spill for desc/flags/verdict, 8 B for
+            // sparse; records (95 VGPRs uncapped) would spill 68 B, so they run at 5
+            if (span_variant() == 1) hipLaunchKernelGGL((k_parse_span<OUT, 1, 16384, OUT == NEXG_OUT_RECORD ? 1 : 6>), grid, block, 0, s, a);
+            else if (span_variant() == 4) hipLaunchKernelGGL((k_parse_span<OUT, 1>), grid, block, 0, s, a);
             else if (span_variant() == 3) hipLaunchKernelGGL((k_parse_span2<OUT, 8192, 2>), grid, block, 0, s, a);
             else hipLaunchKernelGGL((k_parse_span2<OUT, 16384, 1>), grid, block, 0, s, a);
             break;

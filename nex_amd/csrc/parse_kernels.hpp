@@ -84,6 +84,25 @@ __device__ __forceinline__ void store_sparse(const ParseArgs& a, uint64_t idx, b
                                     reinterpret_cast<uint32_t*>(codes + idx));
 }
 
+// store_sparse with the code already known (0: exception) for every lane
+__device__ __forceinline__ void store_sparse_coded(const ParseArgs& a, uint64_t idx, bool valid,
+                                                   const nexg_record& r, uint32_t code) {
+    const bool exc = valid && code == 0u;
+    const uint64_t m = __ballot(exc);
+    uint8_t* codes = reinterpret_cast<uint8_t*>(a.out);
+    if (exc) {
+        uint2* x = reinterpret_cast<uint2*>(codes + NEXG_SPARSE_EXC_OFFSET(a.count));
+        x[(idx & ~63ull) + lanes_below(m)] =
+            make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
+    }
+    const uint32_t c = valid ? code : 0u;
+    const uint32_t c1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x55, 0xF, 0xF, false);  // quad_perm 1111
+    const uint32_t c2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xAA, 0xF, 0xF, false);  // quad_perm 2222
+    const uint32_t c3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xFF, 0xF, 0xF, false);  // quad_perm 3333
+    if ((idx & 3u) == 0u && idx < a.count)
+        __builtin_nontemporal_store(c | (c1 << 8) | (c2 << 16) | (c3 << 24), reinterpret_cast<uint32_t*>(codes + idx));
+}
+
 // every lane of the wave calls this together (see store_sparse)
 template <int OUT>
 __device__ __forceinline__ void store_out(const ParseArgs& a, uint64_t idx, bool valid, const nexg_record& r) {
@@ -632,6 +651,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (NB == 1) __syncthreads();
     }
     if (NB == 2) __syncthreads();  // the stage buffers become per-lane slots below
+    SpanDeferred dfr{};
     if (have) {
         if (fast) {
             uint32_t w[20];
@@ -652,10 +672,52 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     reinterpret_cast<uint4*>(slot)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
                 SpanFrame f{slot, a.data + off, len, sh & 1u, tq};
                 parse_frame(f, sh & 1u, len, a.opt_flags, a.ip_offset, r);
+                dfr = f.d;
             }
         }
     }
-    if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
+    // deferred checksum ranges (SpanFrame): one wave-wide pass of coalesced
+    // 16-B loads (1 KiB per step, L2-hot) per lane that has one
+    // outputs narrower than a record keep only what they store across the pass
+    uint32_t code = 0;
+    if (OUT == NEXG_OUT_SPARSE && have) code = sparse_encode(r, a.opt_flags, a.ip_offset);
+    if (OUT != NEXG_OUT_RECORD) {
+        nexg_record n{};
+        n.flags = r.flags;
+        n.payload_off = r.payload_off;
+        n.payload_len = r.payload_len;
+        r = n;
+    }
+    uint32_t mine = 0;
+    for (uint64_t m = __ballot(dfr.which() != 0u); m; m &= m - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        const uint32_t rg = (uint32_t)__shfl((int)dfr.rng, (int)l, 64);
+        const uint64_t A = __shfl(base + off, (int)l, 64) + (rg & 0xFFFFu), B = A + (rg >> 16);
+        uint32_t s = 0;
+        for (uint64_t c = (A & ~15ull) + 16u * lane; c < B; c += 1024u) {
+            const uint4 v = load16(reinterpret_cast<const void*>(c));
+            if (c >= A && c + 16u <= B) {
+                s += chunk_le_sum(v);
+            } else {
+                if (c + 0 < B) s += halves(v.x & range_mask(c + 0, A, B));
+                if (c + 4 < B) s += halves(v.y & range_mask(c + 4, A, B));
+                if (c + 8 < B) s += halves(v.z & range_mask(c + 8, A, B));
+                if (c + 12 < B) s += halves(v.w & range_mask(c + 12, A, B));
+            }
+        }
+        const uint32_t total = __builtin_amdgcn_readlane(wave_incl_scan_dpp(s), 63);
+        if (lane == l) mine = total;
+    }
+    if (dfr.which()) {
+        span_patch(dfr, mine, r);
+        // a shape code carries the verdict bits: re-derive them (sparse_encode
+        // ignores the OK bits when it matches the shape)
+        if (OUT == NEXG_OUT_SPARSE && code != 0u && (code & 0xFu) < (uint32_t)NEXG_SHAPE_IP_NONE)
+            code = (code & ~(uint32_t)(NEXG_SPARSE_IP_OK | NEXG_SPARSE_L4_OK)) |
+                   ((r.flags & NEXG_C_IP_OK) ? NEXG_SPARSE_IP_OK : 0u) | ((r.flags & NEXG_C_L4_OK) ? NEXG_SPARSE_L4_OK : 0u);
+    }
+    if (OUT == NEXG_OUT_SPARSE) store_sparse_coded(a, idx, have, r, code);
+    else if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
     if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the (now idle) byte buffer
         static_assert(OUT != NEXG_OUT_RECORD || NB * SUB >= kTile * 64u, "record staging needs 16 KiB");
         uint8_t* stage = &s_bytes[0][0];

@@ -67,6 +67,10 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                     memcpy(s64, w80, 64);
                     nexg::SpanFrame f{s64, g, (uint32_t)len, par, tail};
                     nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
+                    if (f.d.which()) {
+                        const uint64_t A = reinterpret_cast<uint64_t>(g) + f.d.off();
+                        nexg::span_patch(f.d, nexg::global_le_sum(A, A + f.d.bytes()), r);
+                    }
                 }
             } else {
                 nexg::WinFrame f{slot, g, o, wlen};
