@@ -191,7 +191,7 @@ struct WinFrame {
     }
 };
 
-// k_parse_span's generic path: frame bytes [0, 64) in a per-lane LDS slot
+// k_parse_span's generic path: frame bytes [0, 80) in a per-lane LDS slot
 // (frame-relative, byte i at slot[i], zero past len), the rest in HBM, and the
 // absolute-parity sum of [80, len) already known from the span prefix scan
 // (tail; only meaningful when len > 80). A checksum range that runs to the
@@ -211,7 +211,7 @@ struct SpanDeferred {  // 3 dwords: it is live through the whole generic parse
 };
 
 struct SpanFrame {
-    static constexpr uint32_t kSlot = 64;
+    static constexpr uint32_t kSlot = 80;
     static constexpr uint32_t kDefer = 64;
     const uint8_t* slot;
     const uint8_t* g;

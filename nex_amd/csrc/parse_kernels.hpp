@@ -530,7 +530,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // each stage buffer: [96-B apron | SUB bytes | 96-B pad]; the apron holds
     // the previous sub-tile's last 96 bytes, so a head window that starts
     // there is read in the sub-tile where it ends (one gather, no straddle)
-    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[NB][kApron + SUB + kApron];
+    // (after the loop the bytes become per-lane 80-B SpanFrame / record slots)
+    constexpr uint32_t kStage = kApron + SUB + kApron > kTile * SpanFrame::kSlot ? kApron + SUB + kApron
+                                                                                 : kTile * SpanFrame::kSlot;
+    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[NB][kStage];
     __shared__ __attribute__((aligned(16))) uint32_t s_pfx[NB][(SUB / 16u) + 4];  // [1024] = total
     __shared__ uint32_t s_wsum[NB][4];
     __shared__ uint64_t s_span[2];
@@ -665,10 +668,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             const uint32_t tq = want_tail ? qb - qa : 0u;
             const uint64_t tail = (sh & 1u) ? (uint64_t)tq * 256u : (uint64_t)tq;
             if (!fast_canonical80(w, len, a.opt_flags, tail, r)) {
-                // generic core on the window (64-B LDS slot) + the scanned tail sum
-                uint8_t* slot = &s_bytes[0][0] + 64u * t;
+                // generic core on the window (80-B LDS slot) + the scanned tail sum
+                uint8_t* slot = &s_bytes[0][0] + SpanFrame::kSlot * t;
 #pragma unroll
-                for (int k = 0; k < 4; k++)
+                for (int k = 0; k < 5; k++)
                     reinterpret_cast<uint4*>(slot)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
                 SpanFrame f{slot, a.data + off, len, sh & 1u, tq};
                 parse_frame(f, sh & 1u, len, a.opt_flags, a.ip_offset, r);
@@ -719,11 +722,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (OUT == NEXG_OUT_SPARSE) store_sparse_coded(a, idx, have, r, code);
     else if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
     if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the (now idle) byte buffer
-        static_assert(OUT != NEXG_OUT_RECORD || NB * SUB >= kTile * 64u, "record staging needs 16 KiB");
+        static_assert(kStage >= kTile * SpanFrame::kSlot, "record staging needs 20 KiB");
         uint8_t* stage = &s_bytes[0][0];
-        if (have) stage_record(stage + 64u * t, r);  // this lane's own slot
+        if (have) stage_record(stage + SpanFrame::kSlot * t, r);  // this lane's own slot
         __syncthreads();
-        copy_out_records<64>(stage, a.out, f0, nf);
+        copy_out_records<SpanFrame::kSlot>(stage, a.out, f0, nf);
     }
 }
 

@@ -45,7 +45,7 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                 // at its own address mod 16 in 16-B chunks; tail sum = Q(end) -
                 // Q(80) from running chunk sums + chunk_prefix_sum, in wrapping
                 // u32 (absolute parity: x256 for the fast path of an odd frame);
-                // declined frames run the generic core on a 64-B slot + that sum
+                // declined frames run the generic core on an 80-B slot + that sum
                 alignas(16) static uint8_t span[65536 + 64];
                 memset(span, 0, sizeof(span));
                 memcpy(span + o, g, len);
@@ -63,8 +63,8 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                 memcpy(w80, g, len < 80 ? len : 80);
                 const uint32_t tail = len > 80 ? Q(o + (uint32_t)len) - Q(o + 80u) : 0u;
                 if (!nexg::fast_canonical80(w80, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, r)) {
-                    alignas(16) uint8_t s64[64];
-                    memcpy(s64, w80, 64);
+                    alignas(16) uint8_t s64[80];
+                    memcpy(s64, w80, 80);
                     nexg::SpanFrame f{s64, g, (uint32_t)len, par, tail};
                     nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
                     if (f.d.which()) {
