@@ -79,7 +79,7 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             break;
         case ParseVariant::SpanTile:
             // 6 waves/SIMD (80 VGPRs): no spill for desc/flags/verdict, 8 B for
-            // sparse; records (95 VGPRs uncapped) would spill 68 B, so they run at 5
+            // sparse/desc; records (about 100 VGPRs) run uncapped: capping them spills 44+ B
             if (span_variant() == 1) hipLaunchKernelGGL((k_parse_span<OUT, 1, 16384, OUT == NEXG_OUT_RECORD ? 1 : 6>), grid, block, 0, s, a);
             else if (span_variant() == 4) hipLaunchKernelGGL((k_parse_span<OUT, 1>), grid, block, 0, s, a);
             else if (span_variant() == 3) hipLaunchKernelGGL((k_parse_span2<OUT, 8192, 2>), grid, block, 0, s, a);

@@ -510,6 +510,18 @@ NEXG_HD uint32_t chunk_prefix_sum(const uint8_t* c, uint32_t m) {
     return halves_acc(v.w & msk(3), halves_acc(v.z & msk(2), halves_acc(v.y & msk(1), halves(v.x & msk(0)))));
 }
 
+// little-endian halfword sum of the bytes of the 16-B chunk v at absolute
+// address c that lie in [A, B)
+NEXG_HD uint32_t chunk_range_sum(const uint4& v, uint64_t c, uint64_t A, uint64_t B) {
+    if (c >= B || c + 16u <= A) return 0u;
+    if (c >= A && c + 16u <= B) return chunk_le_sum(v);
+    uint32_t s = halves(v.x & range_mask(c, A, B));
+    if (c + 4 < B) s += halves(v.y & range_mask(c + 4, A, B));
+    if (c + 8 < B) s += halves(v.z & range_mask(c + 8, A, B));
+    if (c + 12 < B) s += halves(v.w & range_mask(c + 12, A, B));
+    return s;
+}
+
 // inclusive wave64 scan on DPP (row_shr 1/2/4/8, row_bcast 15/31): no LDS traffic
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
@@ -679,8 +691,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
         }
     }
-    // deferred checksum ranges (SpanFrame): one wave-wide pass of coalesced
-    // 16-B loads (1 KiB per step, L2-hot) per lane that has one
+    // deferred checksum ranges (SpanFrame): four at a time, one per 16-lane
+    // group (row), each lane summing up to four 16-B loads in flight per step
+    // (1 KiB per group, L2-hot), rows reduced by xor shuffles
     // outputs narrower than a record keep only what they store across the pass
     uint32_t code = 0;
     if (OUT == NEXG_OUT_SPARSE && have) code = sparse_encode(r, a.opt_flags, a.ip_offset);
@@ -692,24 +705,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         r = n;
     }
     uint32_t mine = 0;
-    for (uint64_t m = __ballot(dfr.which() != 0u); m; m &= m - 1) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(m);
-        const uint32_t rg = (uint32_t)__shfl((int)dfr.rng, (int)l, 64);
-        const uint64_t A = __shfl(base + off, (int)l, 64) + (rg & 0xFFFFu), B = A + (rg >> 16);
-        uint32_t s = 0;
-        for (uint64_t c = (A & ~15ull) + 16u * lane; c < B; c += 1024u) {
-            const uint4 v = load16(reinterpret_cast<const void*>(c));
-            if (c >= A && c + 16u <= B) {
-                s += chunk_le_sum(v);
-            } else {
-                if (c + 0 < B) s += halves(v.x & range_mask(c + 0, A, B));
-                if (c + 4 < B) s += halves(v.y & range_mask(c + 4, A, B));
-                if (c + 8 < B) s += halves(v.z & range_mask(c + 8, A, B));
-                if (c + 12 < B) s += halves(v.w & range_mask(c + 12, A, B));
-            }
+    const uint32_t grp = lane >> 4, gl = lane & 15u;
+    for (uint64_t m = __ballot(dfr.which() != 0u); m;) {
+        const uint64_t cur = m;
+        uint64_t rest = cur;
+        uint32_t pick = 64u;  // this group's deferred lane (64: none)
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t b = rest ? (uint32_t)__builtin_ctzll(rest) : 64u;
+            pick = k == grp ? b : pick;
+            rest &= rest - 1;
         }
-        const uint32_t total = __builtin_amdgcn_readlane(wave_incl_scan_dpp(s), 63);
-        if (lane == l) mine = total;
+        m = rest;
+        const int src = (int)(pick & 63u);
+        const uint32_t rg = (uint32_t)__shfl((int)dfr.rng, src, 64);
+        const uint64_t A = __shfl(base + off, src, 64) + (rg & 0xFFFFu);
+        const uint64_t B = pick < 64u ? A + (rg >> 16) : A;
+        uint32_t s = 0;
+        for (uint64_t c = (A & ~15ull) + 16u * gl; c < B; c += 1024u) {
+            uint4 v[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++)
+                v[k] = c + 256u * k < B ? load16(reinterpret_cast<const void*>(c + 256u * k)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) s += chunk_range_sum(v[k], c + 256u * k, A, B);
+        }
+        s += __shfl_xor(s, 8, 16);
+        s += __shfl_xor(s, 4, 16);
+        s += __shfl_xor(s, 2, 16);
+        s += __shfl_xor(s, 1, 16);
+        const uint32_t rank = (uint32_t)__builtin_popcountll(cur & ((1ull << lane) - 1ull));
+        const uint32_t tot = (uint32_t)__shfl((int)s, (int)((rank & 3u) << 4), 64);
+        if (((cur >> lane) & 1ull) && rank < 4u) mine = tot;
     }
     if (dfr.which()) {
         span_patch(dfr, mine, r);

@@ -17,8 +17,10 @@ from . import abi
 MUTATIONS = ("truncate", "pad", "ip_length", "ver_ihl", "l4_length", "ipv6_hbh", "vlan", "proto200", "random")
 
 
-def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share: float = 0.5):
-    """(FrameBatch on the engine's device, dict of per-mutation counts)."""
+def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share: float = 0.5,
+                  kinds=MUTATIONS):
+    """(FrameBatch on the engine's device, dict of per-mutation counts);
+    `kinds` restricts the mutations drawn (tools/bench_malformed.py)."""
     import torch
 
     from .engine import FrameBatch
@@ -28,7 +30,8 @@ def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share
     data = base.data.cpu().numpy()[: offs[-1]]
     lens = np.diff(offs)
     rng = np.random.default_rng(seed)
-    kind = np.where(rng.random(count) < mutate_share, rng.integers(0, len(MUTATIONS), count), -1)
+    pick = np.array([MUTATIONS.index(k) for k in kinds])
+    kind = np.where(rng.random(count) < mutate_share, pick[rng.integers(0, len(pick), count)], -1)
     # per-frame byte edits on a copy of the frame bytes (lengths unchanged)
     buf = data.copy()
     eth_v4 = (buf[offs[:-1] + 12] == 0x08) & (buf[offs[:-1] + 13] == 0x00)

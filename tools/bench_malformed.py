@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Per-mutation cost of the SURVEY.md App. C malformed mix: for each mutation
+kind, a 1M-frame IMIX batch with every other frame carrying that mutation,
+tiled to 16M frames, parsed with the default span kernel to sparse output.
+Prints one JSON line per kind (kernel ms, Mpkt/s, fraction of 8 TB/s on the
+algorithmic bytes, share of exception slots). The clean IMIX row is the
+baseline; the spread says which fallback costs what.
+
+usage: python tools/bench_malformed.py [--steps K] [--warmup W] [--kinds a,b]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--distinct", type=int, default=1 << 20)
+    ap.add_argument("--tiles", type=int, default=16)
+    ap.add_argument("--kinds", default="")
+    args = ap.parse_args()
+    import torch
+    from nex_amd import abi, workloads
+    from nex_amd.engine import Engine
+    eng = Engine(0)
+    stream = torch.cuda.current_stream()
+    kinds = args.kinds.split(",") if args.kinds else ["clean"] + list(workloads.MUTATIONS) + ["all"]
+    for k in kinds:
+        share = 0.0 if k == "clean" else 0.5
+        sel = workloads.MUTATIONS if k in ("clean", "all") else (k,)
+        mix, counts = workloads.malformed_mix(eng, args.distinct, mutate_share=share, kinds=sel)
+        b = workloads.tiled(mix, args.tiles)
+        out = torch.empty(Engine.out_bytes(abi.OUT_SPARSE, b.count), dtype=torch.uint8, device="cuda")
+        for _ in range(args.warmup):
+            eng.parse(b, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(args.steps):
+            eng.parse(b, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        s = e0.elapsed_time(e1) / 1e3 / args.steps
+        exc = float((out[: b.count] == 0).float().mean().item())
+        print(json.dumps({"kind": k, "frames": b.count, "bytes": b.total_bytes, "kernel_ms": round(s * 1e3, 4),
+                          "mpkt_s": round(b.count / s / 1e6, 1), "frac": round(b.total_bytes / s / 8e12, 4),
+                          "exception_share": round(exc, 4), "mutated": counts.get(k, None)}), flush=True)
+        del b, mix, out
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -22,6 +22,7 @@ for s in ${STEPS:-tests}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench_udp64 500 python bench.py --steps 50 --cpu-seconds 5 ;;
     benchw1) step bench_w1 400 env NEXG_SPAN=1w1 python bench.py --steps 50 --no-cpu-baseline ;;
+    malformed) step bench_malformed 500 python tools/bench_malformed.py ;;
     benchimix) step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5 ;;
     spanvar) for v in 1 2 2d; do step bench_imix_span$v 300 env NEXG_SPAN=$v python bench.py --workload imix --steps 20 --warmup 20 --no-cpu-baseline; done ;;
     pmc) step pmc 900 bash tools/pmc.sh ;;
