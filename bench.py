@@ -57,6 +57,12 @@ def cpu_baseline(batch, workload, count, seconds, nthreads=1):
         data = batch.data[: n * batch.stride].cpu().numpy()
         offs, lens, stride = None, None, batch.stride
         nbytes = n * batch.stride
+    elif batch.lengths is not None:  # offsets + lengths (capture-record shape)
+        offs = batch.offsets[:n].cpu().numpy().astype(np.uint64)
+        lens = batch.lengths[:n].cpu().numpy().astype(np.uint32)
+        data = batch.data[: int(offs[-1]) + int(lens[-1])].cpu().numpy()
+        stride = 0
+        nbytes = int(lens.sum())
     else:
         offs = batch.offsets[: n + 1].cpu().numpy().astype(np.uint64)
         data = batch.data[: int(offs[n])].cpu().numpy()
@@ -209,7 +215,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=25,
                     help="untimed steps; a freshly generated batch runs its first launches "
                          "slow (clock ramp), profiles/r01_staging/imix_ramp.txt")
-    ap.add_argument("--workload", choices=["udp64", "imix", "ser"], default="udp64")
+    ap.add_argument("--workload", choices=["udp64", "imix", "imix_pcap", "ser"], default="udp64")
     ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
     ap.add_argument("--out", choices=list(OUT_KINDS), default="sparse",
                     help="output kind (default: lossless sparse descriptors, NEXG_OUT_SPARSE)")
@@ -242,9 +248,9 @@ def main():
     out_kind = OUT_KINDS[args.out]
     width = {"desc": 8, "record": 64, "flags": 4, "verdict": 2, "sparse": 1}[args.out]
 
-    if args.workload in ("udp64", "imix"):
+    if args.workload in ("udp64", "imix", "imix_pcap"):
         wl = abi.WL_UDP64 if args.workload == "udp64" else abi.WL_IMIX
-        batch = eng.gen_batch(wl, F, first_index=first)
+        batch = eng.gen_batch(wl, F, first_index=first, record_gap=16 if args.workload == "imix_pcap" else 0)
         torch.cuda.synchronize(device)
         alg_bytes = batch.total_bytes  # Σ frame_len: every byte is read (L4 checksum)
         out = torch.empty(Engine.out_bytes(out_kind, F), dtype=torch.uint8, device=device)
@@ -256,9 +262,13 @@ def main():
                                "stride, device-resident; Frame parse (L2/L3/L4) + IPv4 header and "
                                "UDP checksum verify -> " + OUT_NOTE[args.out] if F == 16 << 20
                                else f"{F} x 64-B Eth/IPv4/UDP frames per GPU; " + OUT_NOTE[args.out]}
-        else:
+        elif args.workload == "imix":
             cfg = {"workload": f"configs[2]: {F} IMIX frames per GPU (64/576/1500 at 7:4:1, "
                                "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table; " + OUT_NOTE[args.out]}
+        else:
+            cfg = {"workload": f"configs[4] ingest shape: {F} IMIX frames per GPU, each after a 16-B "
+                               "capture record header (nexg_pcap_read_raw layout: offsets + lengths + "
+                               "monotone hint, headers read through, not counted); " + OUT_NOTE[args.out]}
     else:
         p = eng.gen_udp4_params(F, first_index=first)
         out = torch.empty(F * 42, dtype=torch.uint8, device=device)
@@ -276,7 +286,7 @@ def main():
                 "seed": hex(abi.DEFAULT_SEED)})
 
     if args.e2e:
-        assert args.workload in ("udp64", "imix"), "--e2e covers the parse path"
+        assert args.workload in ("udp64", "imix"), "--e2e covers the packed parse path"
         # host-resident copy of the same frames (pinned), chunked pipeline:
         # copy stream: H2D chunk i; compute stream: parse chunk i; D2H descs
         host = torch.empty(batch.data.numel(), dtype=torch.uint8, pin_memory=True)
@@ -316,7 +326,7 @@ def main():
         cfg["workload"] += "; END-TO-END: frames in pinned host memory, chunked H2D/parse/D2H"
         cfg["e2e_chunk_frames"] = C
 
-    warm = max(args.warmup, 20) if args.workload == "imix" and not args.e2e else args.warmup  # see imix_line
+    warm = max(args.warmup, 20) if args.workload.startswith("imix") and not args.e2e else args.warmup  # see imix_line
     elapsed, kernel_s = timed(step, args.steps, warm, stream, device, host_clock=args.e2e)
     tp = dist.throughput(F, alg_bytes, args.steps, elapsed, device)
     ceilings = None

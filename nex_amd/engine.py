@@ -406,9 +406,12 @@ class Engine:
 
     # --- synthetic workloads ----------------------------------------------
     def gen_batch(self, workload: int, count: int, seed: int = abi.DEFAULT_SEED,
-                  first_index: int = 0, stream=None) -> FrameBatch:
+                  first_index: int = 0, stream=None, record_gap: int = 0) -> FrameBatch:
         """Device-generated SURVEY.md App. C workload (UDP64: fixed 64-B
-        stride; IMIX: packed with an int64 offset table of count+1 entries)."""
+        stride; IMIX: packed with an int64 offset table of count+1 entries).
+        record_gap > 0 (IMIX): each frame preceded by that many zero bytes and
+        described by offsets + lengths + the monotone hint, the shape
+        nexg_pcap_read_raw hands over (16 = classic pcap record headers)."""
         torch = _torch()
         dev = self.torch_device
         s = self._stream(stream)
@@ -422,11 +425,18 @@ class Engine:
                                               _ptr(lengths), s))
         offsets = torch.zeros(count + 1, dtype=torch.int64, device=dev)
         if count:
-            torch.cumsum(lengths[:count].to(torch.int64), 0, out=offsets[1:])
+            torch.cumsum(lengths[:count].to(torch.int64) + record_gap, 0, out=offsets[1:])
         total = int(offsets[count].item()) if count else 0
-        data = torch.empty(max(total, 16) + 16, dtype=torch.uint8, device=dev)
+        if record_gap:
+            offsets = offsets + record_gap  # frame i starts after its record header
+            data = torch.zeros(max(total, 16) + 16, dtype=torch.uint8, device=dev)
+        else:
+            data = torch.empty(max(total, 16) + 16, dtype=torch.uint8, device=dev)
         self._check(self.lib.nexg_gen_frames(self.ctx, workload, seed, first_index, count,
                                              _ptr(data), _ptr(offsets), 0, s))
+        if record_gap:
+            return FrameBatch(data=data[:max(total, 16)], count=count, offsets=offsets,
+                              lengths=lengths, hints=abi.FRAMES_MONOTONE)
         return FrameBatch(data=data, count=count, offsets=offsets)
 
     def gen_udp4_params(self, count, seed=abi.DEFAULT_SEED, first_index=0, stream=None):

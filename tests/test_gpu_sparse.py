@@ -166,3 +166,18 @@ def test_unaligned_frames_take_fast_path_bit_exact(engine, oracle, out_kind):
         b = FrameBatch(data=data, count=len(frames), offsets=ot, lengths=lt, hints=hints)
         got = engine.parse_to_numpy(b, out_kind=out_kind)
         helpers.records_equal(got, want, frames, f"unaligned hints={hints} out={out_kind}")
+
+
+def test_record_gap_batches_match_oracle(engine, oracle):
+    """gen_batch(record_gap=16): the capture-record layout bench.py's
+    imix_pcap line times; every frame parses to the oracle's record of the
+    generator's frame, through the span kernel (monotone hint)."""
+    n = 20000
+    b = engine.gen_batch(abi.WL_IMIX, n, record_gap=16)
+    assert b.hints == abi.FRAMES_MONOTONE and b.lengths is not None
+    frames = [oracle.gen_frame(abi.WL_IMIX, i) for i in range(n)]
+    offs = b.offsets[:n].cpu().numpy()
+    assert (np.diff(offs) == np.array([len(f) + 16 for f in frames[:-1]])).all() and offs[0] == 16
+    want = oracle.parse_frames(frames)
+    helpers.records_equal(engine.parse_to_numpy(b, out_kind=abi.OUT_RECORD), want, frames, "record gap")
+    helpers.records_equal(engine.parse_to_numpy(b, out_kind=abi.OUT_SPARSE), desc_of(want), frames, "gap sparse")

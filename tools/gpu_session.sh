@@ -23,11 +23,16 @@ for s in ${STEPS:-tests}; do
     bench) step bench_udp64 500 python bench.py --steps 50 --cpu-seconds 5 ;;
     benchw1) step bench_w1 400 env NEXG_SPAN=1w1 python bench.py --steps 50 --no-cpu-baseline ;;
     malformed) step bench_malformed 500 python tools/bench_malformed.py ;;
+    benchpcap) step bench_pcap 400 python bench.py --workload imix_pcap --steps 20 --cpu-seconds 5 ;;
+    ser) step bench_ser 300 python bench.py --workload ser --steps 50 --no-cpu-baseline ;;
+    e2e) step bench_e2e 400 python bench.py --e2e --steps 5 --warmup 2 --no-cpu-baseline
+         step bench_e2e_imix 400 python bench.py --e2e --workload imix --steps 3 --warmup 1 --no-cpu-baseline ;;
     benchimix) step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5 ;;
     spanvar) for v in 1 2 2d; do step bench_imix_span$v 300 env NEXG_SPAN=$v python bench.py --workload imix --steps 20 --warmup 20 --no-cpu-baseline; done ;;
     pmc) step pmc 900 bash tools/pmc.sh ;;
-    prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-imix
-          step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 10 --warmup 20 --no-cpu-baseline ;;
+    prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed
+          step prof_pcap 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pcap -o run -- python3 bench.py --workload imix_pcap --steps 60 --warmup 25 --no-cpu-baseline
+          step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 60 --warmup 25 --no-cpu-baseline ;;
   esac
 done
 echo done

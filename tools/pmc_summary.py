@@ -23,7 +23,9 @@ def main():
     rows = []
     per_wl = defaultdict(lambda: {"read_bytes": 0.0, "write_bytes": 0.0, "kernels": []})
     for path in sorted(glob.glob(os.path.join(src, "*_*_SIZE", "*counter_collection.csv"))):
-        wl, counter = os.path.basename(os.path.dirname(path)).split("_", 1)  # <wl>[.<out>]_<COUNTER>
+        name = os.path.basename(os.path.dirname(path))  # <wl>[.<out>]_<COUNTER>
+        counter = "FETCH_SIZE" if name.endswith("_FETCH_SIZE") else "WRITE_SIZE"
+        wl = name[: -len(counter) - 1]
         vals = defaultdict(list)
         with open(path) as f:
             for r in csv.DictReader(f):
