@@ -553,14 +553,35 @@ using EchoReplyPacket = EchoPacket<129>;
 
 /* ---- the engine --------------------------------------------------------- */
 
+// The calling thread's current device switched for a scope and restored after
+// (Engine methods: scratch hipMalloc, copies and launches on the engine's device
+// whatever device the caller has current).
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) {
+            const hipError_t e = hipSetDevice(d);
+            if (e != hipSuccess) throw Error(std::string("hipSetDevice: ") + hipGetErrorString(e));
+        }
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
 class Engine {  // one nexg context on one gfx950 device, one stream
    public:
-    explicit Engine(int device = 0) {
-        check_hip(hipSetDevice(device), "hipSetDevice");
+    explicit Engine(int device = 0) : device_(device) {
+        DeviceScope ds(device);
         check(nexg_ctx_create(device, &ctx_), "nexg_ctx_create");
         check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
     }
     ~Engine() {
+        DeviceScope ds(device_);
         for (auto& b : scratch_) (void)hipFree(b.p);
         if (stream_) (void)hipStreamDestroy(stream_);
         if (ctx_) nexg_ctx_destroy(ctx_);
@@ -569,10 +590,12 @@ class Engine {  // one nexg context on one gfx950 device, one stream
     Engine& operator=(const Engine&) = delete;
 
     nexg_ctx* ctx() const { return ctx_; }
+    int device() const { return device_; }
     hipStream_t stream() const { return stream_; }
 
     // Device-resident batch (frames / out are device pointers), stream-ordered
     void parse(const nexg_frames& frames, ParseOption option, ParseMode mode, int out_kind, void* out) {
+        DeviceScope ds(device_);
         const nexg_parse_option o{option.flags(mode), (uint32_t)option.offset};
         check(nexg_parse_batch(ctx_, &frames, &o, out_kind, out, stream_), "nexg_parse_batch");
     }
@@ -582,6 +605,7 @@ class Engine {  // one nexg context on one gfx950 device, one stream
     // option lists decoded, and each Frame materialised from its record.
     std::vector<Result<Frame>> try_from_bufs(const std::vector<std::vector<uint8_t>>& frames,
                                              ParseOption option = {}, ParseMode mode = ParseMode::Lenient) {
+        DeviceScope ds(device_);
         const uint64_t n = frames.size();
         std::vector<Result<Frame>> out;
         if (n == 0) return out;
@@ -607,6 +631,7 @@ class Engine {  // one nexg context on one gfx950 device, one stream
     // borrow `frames`, which must outlive them
     std::vector<Result<FrameSlice>> frame_slices(const std::vector<std::vector<uint8_t>>& frames,
                                                  ParseOption option = {}) {
+        DeviceScope ds(device_);
         const uint64_t n = frames.size();
         std::vector<Result<FrameSlice>> out;
         if (n == 0) return out;
@@ -626,6 +651,7 @@ class Engine {  // one nexg context on one gfx950 device, one stream
     // 65535 (builder/udp.rs:83, builder/ipv4.rs:153)
     Result<std::vector<std::vector<uint8_t>>, BuildError> build_udp_ping(const std::vector<UdpPingTuple>& t,
                                                                          const UdpPingShape& shape) {
+        DeviceScope ds(device_);
         if (28ull + shape.payload.size() > 65535ull) return BuildError::LengthOverflow;
         const uint64_t n = t.size();
         const uint32_t L = 42u + (uint32_t)shape.payload.size();
@@ -683,6 +709,7 @@ class Engine {  // one nexg context on one gfx950 device, one stream
     // BuildError::AddressFamilyMismatch otherwise, builder/error.rs)
     Result<std::vector<std::vector<uint8_t>>, BuildError> build_tcp_ping(const std::vector<TcpPingTuple>& t,
                                                                          const TcpPingShape& shape) {
+        DeviceScope ds(device_);
         std::vector<std::vector<uint8_t>> frames;
         if (t.empty()) return frames;
         if (shape.options.size() > 40) return BuildError::LengthOverflow;
@@ -725,6 +752,7 @@ class Engine {  // one nexg context on one gfx950 device, one stream
     // icmp_ping's echo request for every tuple (EchoRequest 8 / ICMPv6 128, code 0)
     Result<std::vector<std::vector<uint8_t>>, BuildError> build_icmp_ping(const std::vector<IcmpPingTuple>& t,
                                                                           const IcmpPingShape& shape) {
+        DeviceScope ds(device_);
         std::vector<std::vector<uint8_t>> frames;
         if (t.empty()) return frames;
         const uint8_t fam = t[0].source.family;
@@ -799,6 +827,7 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         size_t size = 0;
     };
     std::vector<Scratch> scratch_;
+    int device_ = 0;
     void* scratch(size_t slot, size_t n) {
         if (slot >= scratch_.size()) scratch_.resize(slot + 1);
         Scratch& b = scratch_[slot];
