@@ -81,6 +81,21 @@ __device__ __forceinline__ void build_copy_out(const uint8_t* smem, uint8_t* T, 
     if (tid < bytes - tail) T[tail + tid] = smem[tail + tid];
 }
 
+// BE word sum of the shared payload (it starts at an even L4 offset), once
+// per workgroup: all threads call it together; 0 without a barrier when the
+// payload is empty (udp_ping's case), so the empty build pays nothing
+__device__ __forceinline__ uint32_t shared_payload_sum(const uint8_t* pl, uint32_t n, uint32_t* s) {
+    if (n == 0) return 0u;  // kernel argument: uniform over the workgroup
+    if (threadIdx.x == 0) *s = 0;
+    __syncthreads();
+    uint32_t ps = 0;
+    for (uint32_t k = 2u * threadIdx.x; k < n; k += 2u * kBuildTile)
+        ps += ((uint32_t)pl[k] << 8) | (k + 1 < n ? (uint32_t)pl[k + 1] : 0u);
+    if (ps) atomicAdd(s, ps);
+    __syncthreads();
+    return *s;
+}
+
 // MAXS = largest stride the LDS tile holds (0: direct global writes).
 // FULL: per-tuple port and id arrays present, MACs from the defaults — every
 // parameter load is unconditional, so a lane issues all five before its first
@@ -96,16 +111,14 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     const uint32_t tid = threadIdx.x;
     const uint64_t i = first + tid;
     const uint32_t flen = 42u + p.payload_len;
+    __shared__ uint32_t s_pay;
+    const uint64_t pw = shared_payload_sum(p.payload, p.payload_len, &s_pay);
     if (tid < nf) {
         const uint32_t src = p.src_ip[i], dst = p.dst_ip[i];
         const uint32_t sp = FULL ? p.src_port[i] : (p.src_port ? p.src_port[i] : p.def_src_port);
         const uint32_t dp = FULL ? p.dst_port[i] : (p.dst_port ? p.dst_port[i] : p.def_dst_port);
         const uint32_t id = FULL ? p.ip_id[i] : (p.ip_id ? p.ip_id[i] : p.def_ip_id);
         const uint32_t ulen = 8u + p.payload_len, total = 20u + ulen;
-        // BE word sum of the shared payload (even UDP offset 8); L2-resident
-        uint64_t pw = 0;
-        for (uint32_t k = 0; k < p.payload_len; k += 2)
-            pw += ((uint32_t)p.payload[k] << 8) | (k + 1 < p.payload_len ? (uint32_t)p.payload[k + 1] : 0u);
         const uint64_t addr = (uint64_t)(src >> 16) + (src & 0xFFFFu) + (dst >> 16) + (dst & 0xFFFFu);
         // udp.rs:443-477 on to_bytes(): pseudo + sport + dport + length (+ payload)
         const uint32_t ucs = fold_complement(addr + 17u + ulen + sp + dp + ulen + pw);
@@ -178,6 +191,8 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
     const uint32_t tid = threadIdx.x;
     const uint64_t i = first + tid;
     const uint32_t flen = 62u + p.payload_len;
+    __shared__ uint32_t s_pay;
+    const uint64_t pw = shared_payload_sum(p.payload, p.payload_len, &s_pay);
     if (tid < nf) {
         const uint32_t* s4 = reinterpret_cast<const uint32_t*>(p.src_ip + 16u * i);
         const uint32_t* d4 = reinterpret_cast<const uint32_t*>(p.dst_ip + 16u * i);
@@ -187,9 +202,6 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
         const uint32_t sp = p.src_port ? p.src_port[i] : p.def_src_port;
         const uint32_t dp = p.dst_port ? p.dst_port[i] : p.def_dst_port;
         const uint32_t ulen = 8u + p.payload_len;
-        uint64_t pw = 0;  // BE word sum of the shared payload (UDP offset 8 is even)
-        for (uint32_t k = 0; k < p.payload_len; k += 2)
-            pw += ((uint32_t)p.payload[k] << 8) | (k + 1 < p.payload_len ? (uint32_t)p.payload[k + 1] : 0u);
         // util.rs:111-133 pseudo-header: address segments (as LE halves x 256),
         // next header 17, length; then sport, dport, length, payload (skipword 3)
         uint32_t addr_le = 0;
@@ -302,16 +314,7 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
     const uint64_t left = a.count - first;
     const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
     const uint64_t i = first + tid;
-    // shared payload: BE word sum (payload starts at an even L4 offset)
-    if (tid == 0) s_pay = 0;
-    __syncthreads();
-    {
-        uint32_t ps = 0;
-        for (uint32_t k = 2u * tid; k < a.payload_len; k += 2u * kBuildTile)
-            ps += ((uint32_t)a.payload[k] << 8) | (k + 1 < a.payload_len ? (uint32_t)a.payload[k + 1] : 0u);
-        if (ps) atomicAdd(&s_pay, ps);
-    }
-    __syncthreads();
+    const uint32_t pay_sum = shared_payload_sum(a.payload, a.payload_len, &s_pay);
     const uint32_t l4_hdr = KIND == kL4Tcp ? 20u + a.opt_padded : 8u;
     const uint32_t l4_len = l4_hdr + a.payload_len;
     const uint32_t flen = 14u + 2u * NIP + l4_len;
@@ -347,7 +350,7 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
             const uint32_t ak = a.ack ? a.ack[i] : a.def_ack;
             const uint32_t w6 = ((l4_hdr / 4u) << 12) | (a.flags & 0xFFu);
             t = sp + dp + (sq >> 16) + (sq & 0xFFFFu) + (ak >> 16) + (ak & 0xFFFFu) + w6 + a.window + a.urg +
-                a.opt_sum + s_pay;
+                a.opt_sum + pay_sum;
             hw[L + 0] = bswap16(sp); hw[L + 1] = bswap16(dp);
             hw[L + 2] = bswap16(sq >> 16); hw[L + 3] = bswap16(sq & 0xFFFFu);
             hw[L + 4] = bswap16(ak >> 16); hw[L + 5] = bswap16(ak & 0xFFFFu);
@@ -357,7 +360,7 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
             const uint32_t id = a.ident ? a.ident[i] : a.def_ident;
             const uint32_t sq = a.seqno ? a.seqno[i] : a.def_seqno;
             const uint32_t w0 = (a.icmp_type << 8) | a.icmp_code;
-            t = w0 + id + sq + s_pay;
+            t = w0 + id + sq + pay_sum;
             hw[L + 0] = bswap16(w0);
             hw[L + 2] = bswap16(id); hw[L + 3] = bswap16(sq);
         }
