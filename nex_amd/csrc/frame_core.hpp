@@ -194,8 +194,9 @@ struct WinFrame {
 // k_parse_span's generic path: frame bytes [0, 80) in a per-lane LDS slot
 // (frame-relative, byte i at slot[i], zero past len), the rest in HBM, and the
 // absolute-parity sum of [80, len) already known from the span prefix scan
-// (tail; only meaningful when len > 80). A checksum range that runs to the
-// frame end (the usual L4 case) costs no HBM reads past byte 80. Any other
+// (tail; only meaningful when len > 80), or of [80, IP end) for a padded
+// frame (span_tail_end). A checksum range that runs to that end (the usual L4
+// case) costs no HBM reads past byte 80. Any other
 // HBM range longer than kDefer bytes (padded frames: the L4 range ends at the
 // IP length) is deferred: le_sum leaves it out and records it, note_mult /
 // note_finish record its multiplier and the checksum it feeds, and the caller
@@ -210,14 +211,26 @@ struct SpanDeferred {  // 3 dwords: it is live through the whole generic parse
     NEXG_HD uint32_t bytes() const { return rng >> 16; }
 };
 
+// Where k_parse_span takes its second prefix value: the IP end of an
+// untagged Ethernet frame whose IPv4 total length / IPv6 payload length ends
+// it before the frame end (padding) and at or past byte 84, else the frame
+// end. b12 / b16 = little-endian dwords of frame bytes 12..15 / 16..19.
+NEXG_HD uint32_t span_tail_end(uint32_t b12, uint32_t b16, uint32_t len, uint32_t opt_flags) {
+    if (opt_flags & (NEXG_PARSE_FROM_IP | NEXG_PARSE_VLAN)) return len;
+    const uint32_t et = ((b12 & 0xFFu) << 8) | ((b12 >> 8) & 0xFFu);
+    const uint32_t e = et == 0x0800u ? 14u + (((b16 & 0xFFu) << 8) | ((b16 >> 8) & 0xFFu))
+                     : et == 0x86DDu ? 54u + ((((b16 >> 16) & 0xFFu) << 8) | (b16 >> 24)) : 0u;
+    return (e >= 84u && e < len) ? e : len;
+}
+
 struct SpanFrame {
     static constexpr uint32_t kSlot = 80;
     static constexpr uint32_t kDefer = 64;
     const uint8_t* slot;
     const uint8_t* g;
-    uint32_t len;
-    uint32_t parity;  // absolute-address parity of byte 0
-    uint32_t tail;
+    uint32_t tail_end;  // span_tail_end(): the frame end or the IP end of a padded frame
+    uint32_t parity;    // absolute-address parity of byte 0
+    uint32_t tail;      // absolute-parity sum of [80, tail_end) (when tail_end > 80)
     mutable SpanDeferred d{};
     mutable bool pend = false;
 
@@ -232,7 +245,7 @@ struct SpanFrame {
             acc = parity ? (uint64_t)s * 256u : (uint64_t)s;
         }
         const uint32_t ga = a > kSlot ? a : kSlot;
-        const bool to_end = b == len && len > 80u && ga <= 80u;
+        const bool to_end = b == tail_end && tail_end > 80u && ga <= 80u;
         const uint32_t gb = to_end ? 80u : b;
         if (ga < gb) {
             const uint64_t base = reinterpret_cast<uint64_t>(g);

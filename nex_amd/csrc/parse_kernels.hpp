@@ -591,6 +591,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const bool fast = have;
     const uint32_t sh = (uint32_t)((base + off) & 3u);
     uint32_t qa = 0, qb = 0, run = 0;
+    uint32_t qend = len;  // frame-relative position of the second prefix value
     uint32_t u[21];
 #pragma unroll
     for (int j = 0; j < 21; j++) u[j] = 0;
@@ -651,9 +652,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             const uint32_t c = d >> 4, m = d & 15u;
             return run + sp[c] + (m ? chunk_prefix_sum(sb + 16u * c, m) : 0u);
         };
-        const uint32_t da = hr + kLaneWin - S, db = hr + len - S;  // wrap: < 0 -> huge
-        if (want_tail && (da < SUB || (last && da == SUB))) qa = q_at(da);
-        if (have && (db < SUB || (last && db == SUB))) qb = q_at(db);
         // 84-B dword-aligned head window [dh, dh + 84): gathered exactly once,
         // in the first sub-tile that holds all of it (apron included: dh >= -80),
         // or in the last one (bytes past the span end are masked by len)
@@ -661,7 +659,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (fast && dh >= -(int)kLaneWin && (dh <= (int)(SUB - kLaneWin - 4u) || (last && dh < (int)SUB))) {
 #pragma unroll
             for (int j = 0; j < 21; j++) u[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4 * j);
+            // A padded frame's L4 range ends at the IP end, not the frame end:
+            // take the second prefix value there instead (at or past the window
+            // end, so in this sub-tile or a later one), so SpanFrame sums that
+            // range from the scan too (untagged Ethernet only).
+            qend = span_tail_end(__builtin_amdgcn_alignbyte(u[4], u[3], sh),
+                                 __builtin_amdgcn_alignbyte(u[5], u[4], sh), len, a.opt_flags);
         }
+        const uint32_t da = hr + kLaneWin - S, db = hr + qend - S;  // wrap: < 0 -> huge
+        if (want_tail && (da < SUB || (last && da == SUB))) qa = q_at(da);
+        if (have && (db < SUB || (last && db == SUB))) qb = q_at(db);
         run += total;
         if (NB == 1) __syncthreads();
     }
@@ -685,7 +692,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
                 for (int k = 0; k < 5; k++)
                     reinterpret_cast<uint4*>(slot)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-                SpanFrame f{slot, a.data + off, len, sh & 1u, tq};
+                SpanFrame f{slot, a.data + off, qend, sh & 1u, tq};
                 parse_frame(f, sh & 1u, len, a.opt_flags, a.ip_offset, r);
                 dfr = f.d;
             }

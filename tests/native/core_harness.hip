@@ -65,7 +65,9 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                 if (!nexg::fast_canonical80(w80, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, r)) {
                     alignas(16) uint8_t s64[80];
                     memcpy(s64, w80, 80);
-                    nexg::SpanFrame f{s64, g, (uint32_t)len, par, tail};
+                    const uint32_t te = nexg::span_tail_end(w80[3], w80[4], (uint32_t)len, flags);
+                    const uint32_t tail2 = te > 80 ? Q(o + te) - Q(o + 80u) : 0u;
+                    nexg::SpanFrame f{s64, g, te, par, tail2};
                     nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
                     if (f.d.which()) {
                         const uint64_t A = reinterpret_cast<uint64_t>(g) + f.d.off();
