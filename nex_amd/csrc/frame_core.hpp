@@ -234,7 +234,11 @@ struct SpanFrame {
     mutable SpanDeferred d{};
     mutable bool pend = false;
 
-    NEXG_HD uint32_t u8(uint32_t i) const { return i < kSlot ? (uint32_t)slot[i] : (uint32_t)g[i]; }
+    // one generic (flat) byte load from the slot or HBM: no divergent branch
+    NEXG_HD uint32_t u8(uint32_t i) const {
+        const uint8_t* p = i < kSlot ? slot + i : g + i;
+        return *p;
+    }
     NEXG_HD uint64_t le_sum(uint32_t a, uint32_t b) const {
         uint64_t acc = 0;
         const uint32_t lb = b < kSlot ? b : kSlot;
