@@ -522,6 +522,24 @@ NEXG_HD uint32_t chunk_range_sum(const uint4& v, uint64_t c, uint64_t A, uint64_
     return s;
 }
 
+// k_parse_span's generic-pass bucket of a declined frame, from its head
+// window dwords 3 (bytes 12..15) and 5 (bytes 20..23): IPv4 TCP / UDP / ICMP /
+// other, IPv6 TCP / UDP / ICMPv6 / other, anything else (FROM_IP included)
+constexpr uint32_t kBuckets = 9;
+NEXG_HD uint32_t span_bucket(uint32_t w3, uint32_t w5, uint32_t opt_flags) {
+    if (opt_flags & NEXG_PARSE_FROM_IP) return 8u;
+    const uint32_t et = ((w3 & 0xFFu) << 8) | ((w3 >> 8) & 0xFFu);
+    if (et == 0x0800u) {
+        const uint32_t p = w5 >> 24;
+        return p == 6u ? 0u : p == 17u ? 1u : p == 1u ? 2u : 3u;
+    }
+    if (et == 0x86DDu) {
+        const uint32_t p = w5 & 0xFFu;
+        return p == 6u ? 4u : p == 17u ? 5u : p == 58u ? 6u : 7u;
+    }
+    return 8u;
+}
+
 // inclusive wave64 scan on DPP (row_shr 1/2/4/8, row_bcast 15/31): no LDS traffic
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
@@ -549,6 +567,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     __shared__ __attribute__((aligned(16))) uint32_t s_pfx[NB][(SUB / 16u) + 4];  // [1024] = total
     __shared__ uint32_t s_wsum[NB][4];
     __shared__ uint64_t s_span[2];
+    __shared__ uint32_t s_hist[2 * kBuckets + 1];  // generic-pass bucket counts, bases, total
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint64_t f0 = (uint64_t)blockIdx.x * kTile;  // grid order: XCD order measured slower here
     const uint64_t idx = f0 + t;
@@ -673,94 +692,134 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (NB == 1) __syncthreads();
     }
     if (NB == 2) __syncthreads();  // the stage buffers become per-lane slots below
-    SpanDeferred dfr{};
+    uint8_t* const slots = &s_bytes[0][0];  // 80 B per lane from here on
+    // (A) every lane: the canonical fast path on its head window
+    uint32_t code = 0, key = 0;
+    bool gen = false;
+    const uint32_t tq = want_tail ? qb - qa : 0u;
     if (have) {
-        if (fast) {
-            uint32_t w[20];
+        uint32_t w[20];
 #pragma unroll
-            for (int k = 0; k < 20; k++) {
-                const uint32_t v = __builtin_amdgcn_alignbyte(u[k + 1], u[k], sh);
-                w[k] = 4u * k < len ? (v & range_mask(4u * k, 0, len)) : 0u;
+        for (int k = 0; k < 20; k++) {
+            const uint32_t v = __builtin_amdgcn_alignbyte(u[k + 1], u[k], sh);
+            w[k] = 4u * k < len ? (v & range_mask(4u * k, 0, len)) : 0u;
+        }
+        // Q weights bytes by absolute parity; fast_canonical80 wants the
+        // frame-relative LE sum: x256 (mod 0xFFFF) for a frame at an odd address
+        const uint64_t tail = (sh & 1u) ? (uint64_t)tq * 256u : (uint64_t)tq;
+        if (fast_canonical80(w, len, a.opt_flags, tail, r)) {
+            if (OUT == NEXG_OUT_SPARSE) code = sparse_encode(r, a.opt_flags, a.ip_offset);
+            if (OUT == NEXG_OUT_RECORD) stage_record(slots + SpanFrame::kSlot * t, r);
+        } else {  // declined: the window goes to this lane's slot for pass (B)
+            gen = true;
+            key = span_bucket(w[3], w[5], a.opt_flags);
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+                reinterpret_cast<uint4*>(slots + SpanFrame::kSlot * t)[k] =
+                    make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        }
+    }
+    // (B) the declined frames of the workgroup, bucketed by (family, L4
+    // protocol) and handed out densely in bucket order, so a wave runs one or
+    // two generic parse paths for 64 frames instead of the union of every
+    // path for the few declined lanes of each wave. Items: {span position,
+    // len | tail end << 16, tail sum, owner lane} in the idle prefix buffer;
+    // results go back through the owner's slot.
+    if (__syncthreads_or(gen)) {
+        if (t < kBuckets) s_hist[t] = 0;
+        __syncthreads();
+        const uint32_t rank = gen ? atomicAdd(&s_hist[key], 1u) : 0u;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t acc = 0;
+            for (uint32_t k = 0; k < kBuckets; k++) {
+                const uint32_t c = s_hist[k];
+                s_hist[kBuckets + k] = acc;
+                acc += c;
             }
-            // Q weights bytes by absolute parity; fast_canonical80 wants the
-            // frame-relative LE sum: x256 (mod 0xFFFF) for a frame at an odd address
-            const uint32_t tq = want_tail ? qb - qa : 0u;
-            const uint64_t tail = (sh & 1u) ? (uint64_t)tq * 256u : (uint64_t)tq;
-            if (!fast_canonical80(w, len, a.opt_flags, tail, r)) {
-                // generic core on the window (80-B LDS slot) + the scanned tail sum
-                uint8_t* slot = &s_bytes[0][0] + SpanFrame::kSlot * t;
+            s_hist[2 * kBuckets] = acc;
+        }
+        __syncthreads();
+        uint4* const items = reinterpret_cast<uint4*>(&s_pfx[0][0]);
+        if (gen) items[s_hist[kBuckets + key] + rank] = make_uint4(hr, len | qend << 16, tq, t);
+        const uint32_t ngen = s_hist[2 * kBuckets];
+        __syncthreads();
+        const bool work = t < ngen;
+        nexg_record rr{};
+        SpanDeferred dfr{};
+        uint32_t owner = 0, ghr = 0;
+        if (work) {
+            const uint4 it = items[t];
+            ghr = it.x;
+            owner = it.w;
+            SpanFrame f{slots + SpanFrame::kSlot * owner, reinterpret_cast<const uint8_t*>(A0 + ghr), it.y >> 16,
+                        ghr & 1u, it.z};
+            parse_frame(f, ghr & 1u, it.y & 0xFFFFu, a.opt_flags, a.ip_offset, rr);
+            dfr = f.d;
+        }
+        // deferred checksum ranges (SpanFrame): four at a time, one per 16-lane
+        // group (row), each lane summing up to four 16-B loads in flight per
+        // step (1 KiB per group, L2-hot), rows reduced by xor shuffles
+        uint32_t mine = 0;
+        const uint32_t grp = lane >> 4, gl = lane & 15u;
+        for (uint64_t m = __ballot(dfr.which() != 0u); m;) {
+            const uint64_t cur = m;
+            uint64_t rest = cur;
+            uint32_t pick = 64u;  // this group's deferred lane (64: none)
 #pragma unroll
-                for (int k = 0; k < 5; k++)
-                    reinterpret_cast<uint4*>(slot)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-                SpanFrame f{slot, a.data + off, qend, sh & 1u, tq};
-                parse_frame(f, sh & 1u, len, a.opt_flags, a.ip_offset, r);
-                dfr = f.d;
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint32_t b = rest ? (uint32_t)__builtin_ctzll(rest) : 64u;
+                pick = k == grp ? b : pick;
+                rest &= rest - 1;
+            }
+            m = rest;
+            const int src = (int)(pick & 63u);
+            const uint32_t rg = (uint32_t)__shfl((int)dfr.rng, src, 64);
+            const uint64_t A = A0 + (uint32_t)__shfl((int)ghr, src, 64) + (rg & 0xFFFFu);
+            const uint64_t B = pick < 64u ? A + (rg >> 16) : A;
+            uint32_t s = 0;
+            for (uint64_t c = (A & ~15ull) + 16u * gl; c < B; c += 1024u) {
+                uint4 v[4];
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++)
+                    v[k] = c + 256u * k < B ? load16(reinterpret_cast<const void*>(c + 256u * k)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) s += chunk_range_sum(v[k], c + 256u * k, A, B);
+            }
+            s += __shfl_xor(s, 8, 16);
+            s += __shfl_xor(s, 4, 16);
+            s += __shfl_xor(s, 2, 16);
+            s += __shfl_xor(s, 1, 16);
+            const uint32_t rk = (uint32_t)__builtin_popcountll(cur & ((1ull << lane) - 1ull));
+            const uint32_t tot = (uint32_t)__shfl((int)s, (int)((rk & 3u) << 4), 64);
+            if (((cur >> lane) & 1ull) && rk < 4u) mine = tot;
+        }
+        if (dfr.which()) span_patch(dfr, mine, rr);
+        if (work) {  // each slot is read and written by its one worker only
+            uint8_t* os = slots + SpanFrame::kSlot * owner;
+            if (OUT == NEXG_OUT_RECORD) {
+                stage_record(os, rr);
+            } else {
+                const uint32_t c = OUT == NEXG_OUT_SPARSE ? sparse_encode(rr, a.opt_flags, a.ip_offset) : 0u;
+                *reinterpret_cast<uint4*>(os) =
+                    make_uint4(rr.flags, (uint32_t)rr.payload_off | ((uint32_t)rr.payload_len << 16), c, 0u);
             }
         }
-    }
-    // deferred checksum ranges (SpanFrame): four at a time, one per 16-lane
-    // group (row), each lane summing up to four 16-B loads in flight per step
-    // (1 KiB per group, L2-hot), rows reduced by xor shuffles
-    // outputs narrower than a record keep only what they store across the pass
-    uint32_t code = 0;
-    if (OUT == NEXG_OUT_SPARSE && have) code = sparse_encode(r, a.opt_flags, a.ip_offset);
-    if (OUT != NEXG_OUT_RECORD) {
-        nexg_record n{};
-        n.flags = r.flags;
-        n.payload_off = r.payload_off;
-        n.payload_len = r.payload_len;
-        r = n;
-    }
-    uint32_t mine = 0;
-    const uint32_t grp = lane >> 4, gl = lane & 15u;
-    for (uint64_t m = __ballot(dfr.which() != 0u); m;) {
-        const uint64_t cur = m;
-        uint64_t rest = cur;
-        uint32_t pick = 64u;  // this group's deferred lane (64: none)
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            const uint32_t b = rest ? (uint32_t)__builtin_ctzll(rest) : 64u;
-            pick = k == grp ? b : pick;
-            rest &= rest - 1;
+        __syncthreads();
+        if (gen && OUT != NEXG_OUT_RECORD) {
+            const uint4 v = *reinterpret_cast<const uint4*>(slots + SpanFrame::kSlot * t);
+            r.flags = v.x;
+            r.payload_off = (uint16_t)v.y;
+            r.payload_len = (uint16_t)(v.y >> 16);
+            code = v.z;
         }
-        m = rest;
-        const int src = (int)(pick & 63u);
-        const uint32_t rg = (uint32_t)__shfl((int)dfr.rng, src, 64);
-        const uint64_t A = __shfl(base + off, src, 64) + (rg & 0xFFFFu);
-        const uint64_t B = pick < 64u ? A + (rg >> 16) : A;
-        uint32_t s = 0;
-        for (uint64_t c = (A & ~15ull) + 16u * gl; c < B; c += 1024u) {
-            uint4 v[4];
-#pragma unroll
-            for (uint32_t k = 0; k < 4; k++)
-                v[k] = c + 256u * k < B ? load16(reinterpret_cast<const void*>(c + 256u * k)) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (uint32_t k = 0; k < 4; k++) s += chunk_range_sum(v[k], c + 256u * k, A, B);
-        }
-        s += __shfl_xor(s, 8, 16);
-        s += __shfl_xor(s, 4, 16);
-        s += __shfl_xor(s, 2, 16);
-        s += __shfl_xor(s, 1, 16);
-        const uint32_t rank = (uint32_t)__builtin_popcountll(cur & ((1ull << lane) - 1ull));
-        const uint32_t tot = (uint32_t)__shfl((int)s, (int)((rank & 3u) << 4), 64);
-        if (((cur >> lane) & 1ull) && rank < 4u) mine = tot;
-    }
-    if (dfr.which()) {
-        span_patch(dfr, mine, r);
-        // a shape code carries the verdict bits: re-derive them (sparse_encode
-        // ignores the OK bits when it matches the shape)
-        if (OUT == NEXG_OUT_SPARSE && code != 0u && (code & 0xFu) < (uint32_t)NEXG_SHAPE_IP_NONE)
-            code = (code & ~(uint32_t)(NEXG_SPARSE_IP_OK | NEXG_SPARSE_L4_OK)) |
-                   ((r.flags & NEXG_C_IP_OK) ? NEXG_SPARSE_IP_OK : 0u) | ((r.flags & NEXG_C_L4_OK) ? NEXG_SPARSE_L4_OK : 0u);
     }
     if (OUT == NEXG_OUT_SPARSE) store_sparse_coded(a, idx, have, r, code);
     else if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
-    if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the (now idle) byte buffer
+    if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the slots (pitch 80 B)
         static_assert(kStage >= kTile * SpanFrame::kSlot, "record staging needs 20 KiB");
-        uint8_t* stage = &s_bytes[0][0];
-        if (have) stage_record(stage + SpanFrame::kSlot * t, r);  // this lane's own slot
         __syncthreads();
-        copy_out_records<SpanFrame::kSlot>(stage, a.out, f0, nf);
+        copy_out_records<SpanFrame::kSlot>(slots, a.out, f0, nf);
     }
 }
 
