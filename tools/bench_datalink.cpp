@@ -207,5 +207,61 @@ int main(int argc, char** argv) {
                (unsigned long long)dr);
         fflush(stdout);
     }
+    // rx scale-out: K TPACKET_V3 receivers in one PACKET_FANOUT (hash) group,
+    // one drain thread each (one receiver per GPU); the
+    // burst's frames differ in their IPv4 source so the hash spreads them
+    for (uint32_t K : {2u, 4u}) {
+        auto fr = frames;
+        for (uint64_t i = 0; i < n; i++) memcpy(fr.data() + i * len + 26, &i, 4);  // IPv4 source address
+        std::vector<nexg_rx*> rxv(K, nullptr);
+        for (uint32_t k = 0; k < K; k++) {
+            nexg_rx_config c;
+            nexg_rx_config_default(&c);
+            c.read_timeout_ms = 200;
+            c.promiscuous = 0;
+            c.ring_blocks = 256;
+            c.fanout = 1;
+            c.fanout_type = NEXG_FANOUT_HASH;
+            c.fanout_group = 0x4E40u + K;
+            if (nexg_rx_open("lo", &c, &rxv[k])) { fprintf(stderr, "nexg_rx_open (fanout) failed\n"); return 1; }
+        }
+        double best = 0;
+        uint64_t got = 0, sent = 0;
+        for (int round = 0; round < 2; round++) {
+            sent = send_batch(fr, n, len);
+            usleep(200000);
+            std::vector<RxResult> rr(K);
+            std::vector<std::atomic<bool>> stops(K);
+            std::vector<std::vector<uint8_t>> bufs(K, std::vector<uint8_t>(kMaxBatch * 2048, 1));
+            std::vector<std::vector<uint64_t>> offv(K, std::vector<uint64_t>(kMaxBatch + 1, 0));
+            std::vector<std::thread> th;
+            const double t0 = now_s();
+            for (uint32_t k = 0; k < K; k++)
+                th.emplace_back([&, k] {  // drain until the receiver's queue stays empty for a timeout
+                    for (;;) {
+                        uint64_t m = 0;
+                        if (nexg_rx_next_batch(rxv[k], bufs[k].data(), bufs[k].size(), offv[k].data(), kMaxBatch,
+                                               nullptr, &m) || m == 0)
+                            break;
+                        for (uint64_t j = 0; j < m; j++)
+                            rr[k].frames += tagged(bufs[k].data() + offv[k][j], (uint32_t)(offv[k][j + 1] - offv[k][j]));
+                        rr[k].last = now_s();
+                    }
+                });
+            for (auto& x : th) x.join();
+            got = 0;
+            double last = t0;
+            for (auto& x : rr) {
+                got += x.frames;
+                last = x.last > last ? x.last : last;
+            }
+            best = got / (last - t0) / 1e6;
+        }
+        for (auto* x : rxv) nexg_rx_close(x);
+        printf("{\"side\": \"rx\", \"mode\": \"%u x tpacket_v3_ring in one PACKET_FANOUT hash group, one thread each\", "
+               "\"frame_bytes\": %u, \"copies\": %llu, \"expected\": %llu, \"drain_mpps\": %.3f}\n",
+               K, len, (unsigned long long)got, (unsigned long long)(2 * sent), best);
+        fflush(stdout);
+    }
     return 0;
 }
