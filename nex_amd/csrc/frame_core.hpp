@@ -762,6 +762,15 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w)[20], uint32_t len, uint32_t op
     return true;
 }
 
+// NEXG_OUT_SPARSE code of a record fast_canonical80 produced: its six shapes
+// are exactly NEXG_SHAPE_V4_UDP..NEXG_SHAPE_V6_ICMP with the payload after the
+// fixed headers (no VLAN), so the code needs no shape search
+NEXG_HD uint32_t canonical80_code(const nexg_record& r) {
+    const uint32_t f = r.flags;
+    const uint32_t shape = ((f & NEXG_L_IPV6) ? 4u : 1u) + ((f & NEXG_L_UDP) ? 0u : (f & NEXG_L_TCP) ? 1u : 2u);
+    return shape | ((f & NEXG_C_IP_OK) ? NEXG_SPARSE_IP_OK : 0u) | ((f & NEXG_C_L4_OK) ? NEXG_SPARSE_L4_OK : 0u);
+}
+
 // nexg_sparse_decode (include/nexg.h) on the device: the same table macros
 NEXG_HD bool sparse_decode(uint32_t code, uint32_t len, uint32_t opt_flags, uint32_t ip_offset, nexg_desc& d) {
     const uint32_t shape = code & 0xFu, tags = (code >> NEXG_SPARSE_TAG_SHIFT) & 3u;

@@ -62,7 +62,10 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                 uint32_t w80[20] = {0};
                 memcpy(w80, g, len < 80 ? len : 80);
                 const uint32_t tail = len > 80 ? Q(o + (uint32_t)len) - Q(o + 80u) : 0u;
-                if (!nexg::fast_canonical80(w80, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, r)) {
+                if (nexg::fast_canonical80(w80, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, r)) {
+                    // the span kernel stores canonical80_code for these: it must be the encoder's code
+                    if (nexg::canonical80_code(r) != nexg::sparse_encode(r, flags, ip_offset)) return -2;
+                } else {
                     alignas(16) uint8_t s64[80];
                     memcpy(s64, w80, 80);
                     const uint32_t te = nexg::span_tail_end(w80[3], w80[4], (uint32_t)len, flags);

@@ -38,10 +38,11 @@ def parse_packed(data, offsets=None, lengths=None, stride=0, flags=0, ip_offset=
     offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
     lens = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.uint32)
     recs = np.zeros(count, dtype=abi.RECORD_DTYPE)
-    lib().harness_parse(data.ctypes.data, data.nbytes,
-                        None if offs is None else offs.ctypes.data,
-                        None if lens is None else lens.ctypes.data, stride, count, flags,
-                        ip_offset, window, int(use_fast), recs.ctypes.data)
+    rc = lib().harness_parse(data.ctypes.data, data.nbytes,
+                             None if offs is None else offs.ctypes.data,
+                             None if lens is None else lens.ctypes.data, stride, count, flags,
+                             ip_offset, window, int(use_fast), recs.ctypes.data)
+    assert rc == 0, f"harness_parse: {rc} (-2: canonical80_code differs from sparse_encode)"
     return recs
 
 
