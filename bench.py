@@ -204,7 +204,7 @@ def malformed_line(eng, args, F, first, out_kind, stream, device, rank, world):
             "value": tp["value"], "unit": "Mpkt/s", "steps": steps, "ms_per_step": tp["ms_per_step"],
             "gib_s": tp["gib_s"], "bytes_per_gpu": alg, "sparse_shape_share": canonical,
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("malformed", args.out),
                          "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg}}
 
 
@@ -215,7 +215,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=25,
                     help="untimed steps; a freshly generated batch runs its first launches "
                          "slow (clock ramp), profiles/r01_staging/imix_ramp.txt")
-    ap.add_argument("--workload", choices=["udp64", "imix", "imix_pcap", "ser"], default="udp64")
+    ap.add_argument("--workload", choices=["udp64", "imix", "imix_pcap", "malformed", "ser"], default="udp64")
     ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
     ap.add_argument("--out", choices=list(OUT_KINDS), default="sparse",
                     help="output kind (default: lossless sparse descriptors, NEXG_OUT_SPARSE)")
@@ -248,9 +248,16 @@ def main():
     out_kind = OUT_KINDS[args.out]
     width = {"desc": 8, "record": 64, "flags": 4, "verdict": 2, "sparse": 1}[args.out]
 
-    if args.workload in ("udp64", "imix", "imix_pcap"):
+    if args.workload in ("udp64", "imix", "imix_pcap", "malformed"):
         wl = abi.WL_UDP64 if args.workload == "udp64" else abi.WL_IMIX
-        batch = eng.gen_batch(wl, F, first_index=first, record_gap=16 if args.workload == "imix_pcap" else 0)
+        if args.workload == "malformed":  # the malformed object's batch as the main workload (PMC / rocprof)
+            from nex_amd import workloads
+            distinct = min(F, 1 << 20)
+            mix, mcounts = workloads.malformed_mix(eng, distinct, seed=abi.DEFAULT_SEED + first)
+            batch = workloads.tiled(mix, max(1, F // distinct))
+            F = batch.count
+        else:
+            batch = eng.gen_batch(wl, F, first_index=first, record_gap=16 if args.workload == "imix_pcap" else 0)
         torch.cuda.synchronize(device)
         alg_bytes = batch.total_bytes  # Σ frame_len: every byte is read (L4 checksum)
         out = torch.empty(Engine.out_bytes(out_kind, F), dtype=torch.uint8, device=device)
@@ -262,6 +269,9 @@ def main():
                                "stride, device-resident; Frame parse (L2/L3/L4) + IPv4 header and "
                                "UDP checksum verify -> " + OUT_NOTE[args.out] if F == 16 << 20
                                else f"{F} x 64-B Eth/IPv4/UDP frames per GPU; " + OUT_NOTE[args.out]}
+        elif args.workload == "malformed":
+            cfg = {"workload": f"SURVEY App. C malformed mix: {F} frames per GPU ({distinct} distinct, tiled), "
+                               f"IMIX with half the frames mutated {mcounts}; " + OUT_NOTE[args.out]}
         elif args.workload == "imix":
             cfg = {"workload": f"configs[2]: {F} IMIX frames per GPU (64/576/1500 at 7:4:1, "
                                "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table; " + OUT_NOTE[args.out]}
@@ -326,7 +336,7 @@ def main():
         cfg["workload"] += "; END-TO-END: frames in pinned host memory, chunked H2D/parse/D2H"
         cfg["e2e_chunk_frames"] = C
 
-    warm = max(args.warmup, 20) if args.workload.startswith("imix") and not args.e2e else args.warmup  # see imix_line
+    warm = max(args.warmup, 20) if args.workload in ("imix", "imix_pcap", "malformed") and not args.e2e else args.warmup  # see imix_line
     elapsed, kernel_s = timed(step, args.steps, warm, stream, device, host_clock=args.e2e)
     tp = dist.throughput(F, alg_bytes, args.steps, elapsed, device)
     ceilings = None

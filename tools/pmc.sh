@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 run() { local name=$1 secs=$2; shift 2
   timeout -s KILL "$secs" "$@" > "gpurun_out/pmc/$name.log" 2>&1; local rc=$?
   echo "$name rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
-CONFIGS=${CONFIGS:-"udp64.sparse imix.sparse udp64.desc imix.desc ser.desc"}
+CONFIGS=${CONFIGS:-"udp64.sparse imix.sparse imix_pcap.sparse malformed.sparse udp64.desc imix.desc ser.desc"}
 for cfg in $CONFIGS; do
   wl=${cfg%.*}; out=${cfg#*.}
   for c in FETCH_SIZE WRITE_SIZE; do
