@@ -581,10 +581,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (t == nf - 1) s_span[1] = off + len;
     __syncthreads();
     const uint64_t lo = s_span[0], hi = s_span[1];
+    const uint64_t A0 = (base + lo) & ~15ull;
+    const uint32_t span = (uint32_t)(((base + hi + 15u) & ~15ull) - A0);
+    // the first sub-tile goes in flight before the group's packed check (one
+    // barrier less of start-up latency); only when [lo, hi] is a plausible
+    // range of the batch, so every load stays inside its 16-B blocks
+    constexpr int CPT = SUB / 4096u;  // 16-B chunks per thread per sub-tile
+    uint4 cur[CPT];
+    auto fetch = [&](uint32_t S, uint4 (&v)[CPT]) {
+#pragma unroll
+        for (int i = 0; i < CPT; i++) {
+            const uint32_t c = S + 16u * (t + 256u * i);
+            v[i] = c < span ? load16<true>(reinterpret_cast<const void*>(A0 + c)) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    const bool plausible = hi >= lo && hi <= a.data_bytes && hi - lo <= (1ull << 30);
+    if (plausible) fetch(0, cur);
     // packed contract: every frame of the group lies inside [lo, hi], and the
     // span is small enough for 32-bit span-relative arithmetic
     const bool inside = !have || (ok && off >= lo && off + len <= hi);
-    const bool span_ok = __syncthreads_and(inside) && hi >= lo && hi - lo <= (1ull << 30);
+    const bool span_ok = __syncthreads_and(inside) && plausible;
     nexg_record r{};
     if (!span_ok) {  // not packed here: every lane parses its own frame from HBM
         if (have) {
@@ -598,8 +614,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         store_out<OUT>(a, idx, have, r);
         return;
     }
-    const uint64_t A0 = (base + lo) & ~15ull;
-    const uint32_t span = (uint32_t)(((base + hi + 15u) & ~15ull) - A0);
     // span-relative positions: head, tail start (head + 80), end
     const uint32_t hr = (uint32_t)(base + off - A0);
     const bool want_tail = have && len > kLaneWin;
@@ -615,16 +629,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
     for (int j = 0; j < 21; j++) u[j] = 0;
 
-    constexpr int CPT = SUB / 4096u;  // 16-B chunks per thread per sub-tile
-    uint4 cur[CPT];
-    auto fetch = [&](uint32_t S, uint4 (&v)[CPT]) {
-#pragma unroll
-        for (int i = 0; i < CPT; i++) {
-            const uint32_t c = S + 16u * (t + 256u * i);
-            v[i] = c < span ? load16<true>(reinterpret_cast<const void*>(A0 + c)) : make_uint4(0, 0, 0, 0);
-        }
-    };
-    fetch(0, cur);
     uint32_t buf = 0;
     for (uint32_t S = 0; S < span; S += SUB, buf = NB == 2 ? buf ^ 1u : 0u) {
         uint8_t* sb = s_bytes[buf] + kApron;
