@@ -782,6 +782,32 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         return download_frames(d_out, n, L);
     }
 
+    // Mutable{Ipv4,Udp,Tcp,Icmp,Icmpv6}Packet::recompute_checksum over every
+    // frame's raw buffer (ipv4.rs:669-679, udp.rs:338-369, tcp.rs:1009-1040,
+    // icmp.rs:372-377, icmpv6.rs:450-470), chained as mutable_chaining.rs:
+    // the frames are rewritten in place; one nexg_fixup per frame says which
+    // fields were written (which = NEXG_FIX_IP | NEXG_FIX_L4)
+    std::vector<nexg_fixup> recompute_checksums(std::vector<std::vector<uint8_t>>& frames, ParseOption option = {},
+                                                uint32_t which = NEXG_FIX_IP | NEXG_FIX_L4) {
+        DeviceScope ds(device_);
+        const uint64_t n = frames.size();
+        std::vector<nexg_fixup> fx(n);
+        if (n == 0) return fx;
+        HostBatch hb(*this, frames);
+        void* d_fx = scratch(3, n * sizeof(nexg_fixup));
+        const nexg_parse_option o{option.flags(ParseMode::Lenient), (uint32_t)option.offset};
+        check(nexg_recompute_checksums_batch(ctx_, &hb.fb, &o, which, static_cast<nexg_fixup*>(d_fx), stream_),
+              "nexg_recompute_checksums_batch");
+        std::vector<uint8_t> data(hb.data.size());
+        check_hip(hipMemcpyAsync(data.data(), const_cast<uint8_t*>(hb.fb.data), data.size(), hipMemcpyDeviceToHost,
+                                 stream_), "D2H");
+        check_hip(hipMemcpyAsync(fx.data(), d_fx, n * sizeof(nexg_fixup), hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+        for (uint64_t i = 0; i < n; i++)
+            std::copy(data.begin() + hb.offs[i], data.begin() + hb.offs[i] + hb.lens[i], frames[i].begin());
+        return fx;
+    }
+
    private:
     void* upload(size_t slot, const void* src, size_t n) {
         void* d = scratch(slot, n);
@@ -927,6 +953,107 @@ class PcapReader {  // classic pcap / pcapng, a batch of records per call
     std::vector<uint8_t> buf_;
     std::vector<uint64_t> offs_;
 };
+
+/* ---- live datalink (nexg_rx_* / nexg_tx_*; nex-datalink's Linux channel) -- */
+
+namespace datalink {
+
+enum class FanoutType : uint32_t {  // lib.rs:70-90
+    HASH = NEXG_FANOUT_HASH, LB = NEXG_FANOUT_LB, CPU = NEXG_FANOUT_CPU,
+    ROLLOVER = NEXG_FANOUT_ROLLOVER, RND = NEXG_FANOUT_RND, QM = NEXG_FANOUT_QM
+};
+struct FanoutOption {  // lib.rs:92-131
+    uint16_t group_id = 0;
+    FanoutType fanout_type = FanoutType::HASH;
+    bool defrag = false, rollover = false;
+};
+struct Config {  // lib.rs:229-240 (the Linux knobs) + the batch ring
+    uint32_t read_buffer_size = 4096;
+    int32_t read_timeout_ms = -1;  // read_timeout: None
+    bool promiscuous = true;
+    bool has_fanout = false;
+    FanoutOption linux_fanout{};
+    uint32_t mode = NEXG_RX_RING;  // or NEXG_RX_MMSG
+    uint32_t ring_block_size = 1u << 20, ring_blocks = 64, ring_block_tov_ms = 2;
+    bool skip_outgoing = false;
+};
+
+// RawReceiver::next (linux.rs:356-397), a batch of frames per call
+class RawReceiver {
+   public:
+    RawReceiver(const std::string& ifname, const Config& c = {}) {
+        nexg_rx_config k;
+        nexg_rx_config_default(&k);
+        k.read_buffer_size = c.read_buffer_size;
+        k.read_timeout_ms = c.read_timeout_ms;
+        k.promiscuous = c.promiscuous;
+        k.fanout = c.has_fanout;
+        k.fanout_type = (uint32_t)c.linux_fanout.fanout_type | (c.linux_fanout.defrag ? NEXG_FANOUT_FLAG_DEFRAG : 0u) |
+                        (c.linux_fanout.rollover ? NEXG_FANOUT_FLAG_ROLLOVER : 0u);
+        k.fanout_group = c.linux_fanout.group_id;
+        k.mode = c.mode;
+        k.ring_block_size = c.ring_block_size;
+        k.ring_blocks = c.ring_blocks;
+        k.ring_block_tov_ms = c.ring_block_tov_ms;
+        k.flags = c.skip_outgoing ? NEXG_RX_SKIP_OUTGOING : 0u;
+        const int rc = nexg_rx_open(ifname.c_str(), &k, &rx_);
+        if (rc != NEXG_OK) throw Error("nexg_rx_open(" + ifname + "): " + nexg_strerror(rc));
+    }
+    ~RawReceiver() {
+        if (rx_) nexg_rx_close(rx_);
+    }
+    RawReceiver(const RawReceiver&) = delete;
+    RawReceiver& operator=(const RawReceiver&) = delete;
+    // frames already received (waits up to the read timeout for the first)
+    std::vector<std::vector<uint8_t>> next_batch(uint64_t max_frames = 4096, uint64_t data_cap = 16u << 20) {
+        buf_.resize(data_cap);
+        offs_.resize(max_frames + 1);
+        uint64_t n = 0;
+        const int rc = nexg_rx_next_batch(rx_, buf_.data(), buf_.size(), offs_.data(), max_frames, nullptr, &n);
+        if (rc != NEXG_OK) throw Error(std::string("nexg_rx_next_batch: ") + nexg_strerror(rc));
+        std::vector<std::vector<uint8_t>> frames(n);
+        for (uint64_t i = 0; i < n; i++) frames[i].assign(buf_.begin() + offs_[i], buf_.begin() + offs_[i + 1]);
+        return frames;
+    }
+    nexg_rx* handle() const { return rx_; }
+
+   private:
+    nexg_rx* rx_ = nullptr;
+    std::vector<uint8_t> buf_;
+    std::vector<uint64_t> offs_;
+};
+
+// RawSender::send (linux.rs:302-346), a batch per call (sendmmsg)
+class RawSender {
+   public:
+    explicit RawSender(const std::string& ifname) {
+        const int rc = nexg_tx_open(ifname.c_str(), &tx_);
+        if (rc != NEXG_OK) throw Error("nexg_tx_open(" + ifname + "): " + nexg_strerror(rc));
+    }
+    ~RawSender() {
+        if (tx_) nexg_tx_close(tx_);
+    }
+    RawSender(const RawSender&) = delete;
+    RawSender& operator=(const RawSender&) = delete;
+    // frames the kernel accepted
+    uint64_t send_batch(const std::vector<std::vector<uint8_t>>& frames) {
+        std::vector<uint8_t> data;
+        std::vector<uint64_t> offs(frames.size() + 1, 0);
+        for (size_t i = 0; i < frames.size(); i++) {
+            data.insert(data.end(), frames[i].begin(), frames[i].end());
+            offs[i + 1] = data.size();
+        }
+        uint64_t sent = 0;
+        const int rc = nexg_tx_send_batch(tx_, data.data(), offs.data(), nullptr, 0, frames.size(), &sent);
+        if (rc != NEXG_OK) throw Error(std::string("nexg_tx_send_batch: ") + nexg_strerror(rc));
+        return sent;
+    }
+
+   private:
+    nexg_tx* tx_ = nullptr;
+};
+
+}  // namespace datalink
 
 }  // namespace nexg
 

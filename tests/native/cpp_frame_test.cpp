@@ -10,6 +10,7 @@
 //                    a GPU; the oracle is test infrastructure)
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <fstream>
 #include <map>
@@ -322,6 +323,21 @@ int main(int argc, char** argv) {
             CHECK(e.is_ok() && e.value()[0] == wante);
             auto fe = eng->try_from_bufs(e.value());
             CHECK(fe[0].is_ok() && fe[0].value().checksums.l4_ok);
+            // examples/mutable_chaining.rs: clear the checksum fields, recompute
+            // them over the raw buffers (Mutable*Packet::recompute_checksum)
+            // -> the builders' bytes again
+            std::vector<std::vector<uint8_t>> fix = {b.value()[0], e.value()[0]};
+            const size_t ip = 14, l4 = 14 + (fam == 4 ? 20 : 40);
+            for (auto& x : fix) {
+                if (fam == 4) x[ip + 10] = x[ip + 11] = 0;
+            }
+            fix[0][l4 + 16] = fix[0][l4 + 17] = 0xEE;  // TCP checksum
+            fix[1][l4 + 2] = fix[1][l4 + 3] = 0x11;    // ICMP / ICMPv6 checksum
+            auto fx = eng->recompute_checksums(fix);
+            CHECK(fix[0] == b.value()[0] && fix[1] == e.value()[0]);
+            CHECK((fx[0].done & NEXG_FIX_L4) && fx[0].proto == 6 && fx[0].l4_off == l4);
+            CHECK((fx[1].done & NEXG_FIX_L4) && fx[1].proto == (fam == 4 ? 1 : 58));
+            CHECK(((fx[0].done & NEXG_FIX_IP) != 0) == (fam == 4));
         }
         TcpPingTuple a, b6;
         a.source = a.destination = IpAddr::from(Ipv4Addr{{10, 0, 0, 1}});
@@ -332,6 +348,34 @@ int main(int argc, char** argv) {
         big.options.assign(50, 0x01);  // builder/tcp.rs:211-228: options past 40 B
         auto over = eng->build_tcp_ping({a}, big);
         CHECK(over.is_err() && over.error() == BuildError::LengthOverflow);
+    }
+    if (!gpu) {  // datalink::RawSender / RawReceiver over loopback where CAP_NET_RAW is held
+        try {
+            datalink::Config c;
+            c.read_timeout_ms = 300;
+            c.skip_outgoing = true;
+            datalink::RawReceiver rx("lo", c);
+            datalink::RawSender tx("lo");
+            std::vector<std::vector<uint8_t>> out;
+            for (int i = 0; i < 32; i++) {
+                std::vector<uint8_t> f(64 + 8 * i, 0);
+                for (int k = 0; k < 6; k++) f[k] = 0xFF;
+                const uint8_t src[6] = {0x02, 0x6E, 0x65, 0x78, 0x43, (uint8_t)i};
+                memcpy(f.data() + 6, src, 6);
+                f[12] = 0x88;
+                f[13] = 0xB5;  // local experimental EtherType
+                f[20] = (uint8_t)i;
+                out.push_back(f);
+            }
+            CHECK(tx.send_batch(out) == out.size());
+            std::vector<std::vector<uint8_t>> in;
+            for (int tries = 0; tries < 10 && in.size() < out.size(); tries++)
+                for (auto& f : rx.next_batch())
+                    if (f.size() >= 12 && f[6] == 0x02 && f[7] == 0x6E && f[10] == 0x43) in.push_back(f);
+            CHECK(in == out);
+        } catch (const Error& e) {
+            printf("datalink checks skipped: %s\n", e.what());
+        }
     }
     // every fixture: Frame fields == the record the oracle writes (device == oracle in --gpu)
     for (const auto& n : names) {
