@@ -493,9 +493,11 @@ namespace nexg {
 // LE-halfword sums are prefix-scanned; a frame's L4 tail sum is then the
 // difference of two prefix values Q(p) = Σ_{i<p} byte_i·256^(i mod 2) taken at
 // p = start+80 and p = end (ones-complement sums are linear, and 2^32 wrapping
-// is exact for a ≤64-KiB frame). The 80-B head window is copied from LDS into
-// registers and finished by fast_canonical80; anything it declines is parsed
-// by the generic core straight from HBM (L2-hot: the workgroup just read it).
+// is exact for a ≤64-KiB frame). Each frame's head window is copied from LDS
+// into registers at any byte alignment and finished by fast_canonical80; the
+// frames it declines are bucketed by (family, L4 protocol) across the
+// workgroup and parsed densely by the generic core on 80-B LDS slots
+// (SpanFrame), their L4 sums taken from the same prefix scan.
 
 NEXG_HD uint32_t chunk_le_sum(const uint4& v) {
     return halves_acc(v.w, halves_acc(v.z, halves_acc(v.y, halves_acc(v.x, 0u))));
@@ -553,8 +555,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 
 // NB = 2: sub-tile k stages into buffer k&1, so the barrier that publishes
 // sub-tile k also retires every lookup into sub-tile k-2's buffer (3 barriers
-// per sub-tile, 41 KB LDS); NB = 1: one buffer and a 4th barrier (21 KB LDS,
-// more workgroups per CU).
+// per sub-tile, ~42 KB LDS); NB = 1 (the library's): one buffer and a 4th
+// barrier (~25 KB LDS, 6 workgroups per CU).
 template <int OUT, int NB = 1, uint32_t SUB = 16384, int WPE = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_parse_span(ParseArgs a) {
     // each stage buffer: [96-B apron | SUB bytes | 96-B pad]; the apron holds
@@ -621,7 +623,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // LDS dwords, realigned by v_alignbyte after the loop); fast_canonical80
     // itself declines FROM_IP. One generic call site below: a second parse_frame
     // instance on another branch costs 15 VGPRs (6 -> 5 waves/SIMD).
-    const bool fast = have;
     const uint32_t sh = (uint32_t)((base + off) & 3u);
     uint32_t qa = 0, qb = 0, run = 0;
     uint32_t qend = len;  // frame-relative position of the second prefix value
@@ -679,7 +680,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // in the first sub-tile that holds all of it (apron included: dh >= -80),
         // or in the last one (bytes past the span end are masked by len)
         const int dh = (int)((hr & ~3u) - S);
-        if (fast && dh >= -(int)kLaneWin && (dh <= (int)(SUB - kLaneWin - 4u) || (last && dh < (int)SUB))) {
+        if (have && dh >= -(int)kLaneWin && (dh <= (int)(SUB - kLaneWin - 4u) || (last && dh < (int)SUB))) {
 #pragma unroll
             for (int j = 0; j < 21; j++) u[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4 * j);
             // A padded frame's L4 range ends at the IP end, not the frame end:
