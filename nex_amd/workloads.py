@@ -67,11 +67,13 @@ def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share
     new_offs = np.zeros(count + 1, np.int64)
     np.cumsum(new_len, out=new_offs[1:])
     out = np.zeros(int(new_offs[-1]), np.uint8)
-    plain = (ins == 0) & (pad == 0)
-    # frames without inserts: one gather of their (possibly truncated) bytes
-    src = np.repeat(offs[:-1][plain], new_len[plain]) + _ramp(new_len[plain])
-    dst = np.repeat(new_offs[:-1][plain], new_len[plain]) + _ramp(new_len[plain])
-    out[dst] = buf[src]
+    plain = np.nonzero((ins == 0) & (pad == 0))[0]
+    # frames without inserts: gathers of their (possibly truncated) bytes, in
+    # chunks so the index arrays stay small (one rank per GPU builds its mix)
+    for c0 in range(0, len(plain), 1 << 16):
+        sel = plain[c0:c0 + (1 << 16)]
+        ramp = _ramp(new_len[sel])
+        out[np.repeat(new_offs[:-1][sel], new_len[sel]) + ramp] = buf[np.repeat(offs[:-1][sel], new_len[sel]) + ramp]
     for j in np.nonzero(~plain)[0]:
         f = buf[offs[j]:offs[j + 1]]
         if pad[j]:
