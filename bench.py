@@ -238,9 +238,10 @@ def main():
     rank, world, local = dist.env_rank_world()
     if world != args.gpus and rank == 0:
         log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
+    local = dist.device_index(local)  # 1:1 on a full node; folded for a shared-GPU rehearsal
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    dist.init()  # RCCL when this process has a GPU, gloo otherwise
+    dist.init()  # RCCL when this process has a GPU, gloo otherwise (NEXG_DIST_BACKEND overrides)
     eng = Engine(local)
     F = args.frames
     first = rank * F

@@ -19,13 +19,26 @@ def shard(total: int, rank: int, world: int):
 
 
 def pick_backend() -> str:
-    """RCCL ("nccl" on ROCm) when this process has a GPU, gloo otherwise.
-    Only the timing barrier and two scalar reductions ever use it."""
+    """RCCL ("nccl" on ROCm) when this process has a GPU, gloo otherwise;
+    NEXG_DIST_BACKEND overrides (gloo lets several ranks share one GPU for a
+    rehearsal of the multi-rank path, which RCCL refuses). Only the timing
+    barrier and two scalar reductions ever use it."""
     import torch
     import torch.distributed as dist
+    forced = os.environ.get("NEXG_DIST_BACKEND")
+    if forced:
+        return forced
     if torch.cuda.is_available() and dist.is_nccl_available():
         return "nccl"
     return "gloo"
+
+
+def device_index(local: int) -> int:
+    """GPU of a rank: its LOCAL_RANK, folded onto the visible devices when
+    there are fewer (the shared-GPU rehearsal; the 8-GPU run maps 1:1)."""
+    import torch
+    n = torch.cuda.device_count()
+    return local % n if n else local
 
 
 def init(backend: str = None):
