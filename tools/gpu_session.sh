@@ -28,6 +28,7 @@ for s in ${STEPS:-tests}; do
     e2e) step bench_e2e 400 python bench.py --e2e --steps 5 --warmup 2 --no-cpu-baseline
          step bench_e2e_imix 400 python bench.py --e2e --workload imix --steps 3 --warmup 1 --no-cpu-baseline ;;
     rehearse2) step rehearse2 600 env NEXG_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 2 ;;
+    rehearse8) step rehearse8 900 env NEXG_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 8 --steps 10 --warmup 3 --cpu-seconds 2 ;;
     benchimix) step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5 ;;
     spanvar) for v in 1 2 2d; do step bench_imix_span$v 300 env NEXG_SPAN=$v python bench.py --workload imix --steps 20 --warmup 20 --no-cpu-baseline; done ;;
     pmc) step pmc 900 bash tools/pmc.sh ;;
