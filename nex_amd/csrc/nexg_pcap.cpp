@@ -236,6 +236,108 @@ void refill(nexg_pcap* p, size_t need) {
     }
 }
 
+// Classic-pcap record walk of buf[0, have) split over `threads` threads.
+// Chunk k > 0 starts at the first position whose header is plausible
+// (caplen <= snaplen, orig_len >= caplen, sub-second field in range) and
+// chains to further plausible headers; each thread walks its chunk to the
+// first record that starts at or past the chunk end. The chunks are stitched
+// where the previous walk ended exactly where the next one began; any
+// disagreement (a header look-alike inside a payload) re-walks that chunk
+// from the previous end, so the result always equals the sequential walk.
+// Returns records found (<= max_frames) and *end = bytes described, or -1
+// when a malformed record needs the sequential walk's error path.
+struct WalkPart {
+    std::vector<uint64_t> offs;
+    std::vector<uint32_t> lens;
+    std::vector<uint64_t> ts;
+    size_t begin = 0, end = 0;  // first record start, first start past the chunk (or the incomplete tail)
+    bool bad = false;
+};
+
+bool classic_plausible(const nexg_pcap* p, const uint8_t* b, size_t avail) {
+    if (avail < 16) return false;
+    const uint32_t frac = rd32(p, b + 4), caplen = rd32(p, b + 8), orig = rd32(p, b + 12);
+    const uint32_t snap = p->snaplen ? p->snaplen : 262144u;
+    return caplen <= snap && orig >= caplen && frac < (p->nsec ? 1000000000u : 1000000u);
+}
+
+void walk_classic(const nexg_pcap* p, const uint8_t* buf, size_t have, size_t from, size_t stop, bool want_ts,
+                  WalkPart& w) {
+    size_t pos = from;
+    w.begin = from;
+    while (pos < stop) {
+        if (have - pos < 16) break;
+        const uint32_t caplen = rd32(p, buf + pos + 8);
+        if (caplen > (1u << 26)) { w.bad = true; break; }
+        if (have - pos < 16 + (size_t)caplen) break;
+        w.offs.push_back(pos + 16);
+        w.lens.push_back(caplen);
+        if (want_ts)
+            w.ts.push_back((uint64_t)rd32(p, buf + pos) * 1000000000ull +
+                           (uint64_t)rd32(p, buf + pos + 4) * (p->nsec ? 1u : 1000u));
+        pos += 16 + caplen;
+    }
+    w.end = pos;
+}
+
+int64_t parallel_walk(nexg_pcap* p, const uint8_t* buf, size_t have, uint64_t max_frames, uint64_t* offsets,
+                      uint32_t* lengths, uint64_t* ts_ns, size_t* end) {
+    const size_t T = p->threads;
+    const size_t per = (have + T - 1) / T;
+    std::vector<WalkPart> parts(T);
+    auto work = [&](size_t k) {
+        const size_t a = k * per, b = a + per < have ? a + per : have;
+        if (a >= have) { parts[k].begin = parts[k].end = have; return; }
+        size_t s = a;
+        if (k > 0) {  // first plausible header that chains 4 deep (or to the buffer end)
+            for (; s < b; s++) {
+                size_t q = s;
+                int depth = 0;
+                while (depth < 4 && classic_plausible(p, buf + q, have - q)) {
+                    q += 16 + (size_t)rd32(p, buf + q + 8);
+                    depth++;
+                    if (q >= have) break;
+                }
+                if (depth == 4 || (depth > 0 && q >= have)) break;
+            }
+        }
+        walk_classic(p, buf, have, s, b, ts_ns != nullptr, parts[k]);
+    };
+    std::vector<std::thread> pool;
+    for (size_t k = 1; k < T; k++) pool.emplace_back(work, k);
+    work(0);
+    for (auto& t : pool) t.join();
+    // stitch; re-walk a chunk whose start disagrees with the previous end
+    for (size_t k = 1; k < T; k++) {
+        if (parts[k - 1].bad) return -1;
+        if (parts[k].begin != parts[k - 1].end) {
+            const size_t stop = (k + 1) * per < have ? (k + 1) * per : have;
+            parts[k] = WalkPart{};
+            walk_classic(p, buf, have, parts[k - 1].end, stop > parts[k - 1].end ? stop : parts[k - 1].end,
+                         ts_ns != nullptr, parts[k]);
+        }
+    }
+    if (parts[T - 1].bad) return -1;
+    // concatenate (up to max_frames), in parallel
+    std::vector<uint64_t> first(T + 1, 0);
+    for (size_t k = 0; k < T; k++) first[k + 1] = first[k] + parts[k].offs.size();
+    const uint64_t n = first[T] < max_frames ? first[T] : max_frames;
+    auto copy = [&](size_t k) {
+        if (first[k] >= n) return;
+        const uint64_t m = (first[k + 1] < n ? first[k + 1] : n) - first[k];
+        memcpy(offsets + first[k], parts[k].offs.data(), m * 8);
+        memcpy(lengths + first[k], parts[k].lens.data(), m * 4);
+        if (ts_ns) memcpy(ts_ns + first[k], parts[k].ts.data(), m * 8);
+    };
+    pool.clear();
+    for (size_t k = 1; k < T; k++) pool.emplace_back(copy, k);
+    copy(0);
+    for (auto& t : pool) t.join();
+    *end = n < first[T] ? (size_t)(offsets[n - 1] + lengths[n - 1]) : parts[T - 1].end;
+    if (n == 0) *end = 0;
+    return (int64_t)n;
+}
+
 }  // namespace
 
 extern "C" {
@@ -374,7 +476,17 @@ int nexg_pcap_read_raw(nexg_pcap* p, uint8_t* buf, uint64_t cap, uint64_t* offse
     }
     uint64_t n = 0;
     size_t pos = 0;
-    while (n < max_frames) {
+    bool walked = false;
+    if (!p->ng && p->threads > 1 && have >= (8u << 20)) {  // classic pcap: the record walk in parallel
+        size_t end = 0;
+        const int64_t got = parallel_walk(p, buf, have, max_frames, offsets, lengths, ts_ns, &end);
+        if (got >= 0) {
+            n = (uint64_t)got;
+            pos = end;
+            walked = true;
+        }  // else: a malformed record; the sequential walk below reports it
+    }
+    while (!walked && n < max_frames) {
         size_t used = 0;
         Rec r;
         const int rc = scan_one(p, buf + pos, have - pos, &used, &r);

@@ -257,3 +257,36 @@ def test_raw_retry_after_erange_resumes(tmp_path, frames):
             got += [bytes(buf[int(offs[k]):int(offs[k]) + int(lens[k])]) for k in range(n)]
         assert errors >= 1
     assert got == fr
+
+
+@pytest.mark.parametrize("threads", [3, 8])
+def test_raw_parallel_walk_against_lookalike_headers(tmp_path, threads):
+    """read_raw's parallel record walk (classic pcap, >= 8 MiB read) starts
+    chunks at speculated record boundaries; payloads made of chained,
+    plausible-looking 16-B record headers must not fool it: the frames, their
+    lengths and the bytes consumed equal the sequential walk's, in both byte
+    orders and with the frame limit cutting inside a chunk."""
+    import struct
+
+    from nex_amd.ingest import raw_frames
+    rng = np.random.default_rng(5)
+    fr = []
+    for i in range(60000):
+        n = int(rng.integers(20, 400))
+        if i % 3 == 0:  # a payload of fake headers, each "caplen" pointing at the next
+            fake = b""
+            while len(fake) + 16 + 24 <= n:
+                fake += struct.pack("<IIII", 1_700_000_000, 123456, 24, 24) + bytes(24)
+            fr.append(fake + bytes(n - len(fake)))
+        else:
+            fr.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    for big_endian in (False, True):
+        path = _write(tmp_path, f"look{int(big_endian)}.pcap", pcapfile.classic(fr, big_endian=big_endian))
+        with PcapReader(path) as r:
+            want = list(raw_frames(r, cap=10 << 20, max_frames=1 << 15))
+        assert want == fr
+        for cap, maxf in ((10 << 20, 1 << 15), (12 << 20 | 3, 1 << 20)):
+            with PcapReader(path) as r:
+                r.set_read_threads(threads)
+                got = list(raw_frames(r, cap=cap, max_frames=maxf))
+            assert got == want, (big_endian, cap, maxf)
