@@ -609,7 +609,10 @@ int nexg_pcap_read_raw(nexg_pcap* p, uint8_t* buf, uint64_t cap, uint64_t* offse
                        uint32_t* lengths, uint64_t max_frames, uint64_t* ts_ns,
                        uint64_t* n_frames, uint64_t* bytes_used);
 /* read_raw's file reads split over up to `threads` (1..64) parallel preads
- * of >= 4-MiB pieces (default 1). Results are identical for any count.
+ * of >= 4-MiB pieces (default 1), and for classic pcap the record walk of a
+ * read of >= 8 MiB split over as many threads (speculative chunk starts,
+ * stitched; a disagreement re-walks that chunk). Results are identical for
+ * any count.
  * (read_batch stays single-threaded: parallel record copies into pinned
  * staging measured 2.5-4x slower on the GPU boxes, profiles/r01_ingest/threads.) */
 int nexg_pcap_set_read_threads(nexg_pcap* p, uint32_t threads);
