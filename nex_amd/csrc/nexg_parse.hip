@@ -78,9 +78,15 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             hipLaunchKernelGGL((k_parse<1, OUT, 0, 128>), grid, block, 0, s, a);
             break;
         case ParseVariant::SpanTile:
-            // 6 waves/SIMD (80 VGPRs): no spill for desc/flags/verdict, 8 B for
-            // sparse/desc; records (about 100 VGPRs) run uncapped: capping them spills 44+ B
-            if (span_variant() == 1) hipLaunchKernelGGL((k_parse_span<OUT, 1, 16384, OUT == NEXG_OUT_RECORD ? 1 : 6>), grid, block, 0, s, a);
+            // 20-KiB sub-tiles at 6 waves/SIMD (80 VGPRs, 26 KB LDS, 6 workgroups
+            // per CU: 120 KB in flight per CU): +2.6 % over 16 KiB on IMIX in the
+            // same process, 24 KiB at 5 waves equal, 28-32 KiB slower
+            // (profiles/r02_kbench/kbench_subtile.log). Records (about 100
+            // VGPRs) run uncapped on 16 KiB: capping them spills 44+ B.
+            if (span_variant() == 1) {
+                if (OUT == NEXG_OUT_RECORD) hipLaunchKernelGGL((k_parse_span<OUT, 1, 16384, 1>), grid, block, 0, s, a);
+                else hipLaunchKernelGGL((k_parse_span<OUT, 1, 20480, 6>), grid, block, 0, s, a);
+            }
             else if (span_variant() == 4) hipLaunchKernelGGL((k_parse_span<OUT, 1>), grid, block, 0, s, a);
             else if (span_variant() == 3) hipLaunchKernelGGL((k_parse_span2<OUT, 8192, 2>), grid, block, 0, s, a);
             else hipLaunchKernelGGL((k_parse_span2<OUT, 16384, 1>), grid, block, 0, s, a);

@@ -303,6 +303,16 @@ int main(int argc, char** argv) {
         ivars.push_back({"imix_sparse_span_v1", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1>), grid, blk, 0, 0, sa); }, ibytes});
         ivars.push_back({"imix_sparse_span_v1_w7", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 16384, 7>), grid, blk, 0, 0, sa); }, ibytes});
         ivars.push_back({"imix_sparse_span_v1_w6", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 16384, 6>), grid, blk, 0, 0, sa); }, ibytes});
+        // larger sub-tiles: more bytes in flight per workgroup, fewer workgroups per CU
+        ivars.push_back({"imix_sparse_span_20k_w6", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 20480, 6>), grid, blk, 0, 0, sa); }, ibytes});
+        ivars.push_back({"imix_sparse_span_20k_w5", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 20480, 5>), grid, blk, 0, 0, sa); }, ibytes});
+        ivars.push_back({"imix_sparse_span_24k_w5", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 24576, 5>), grid, blk, 0, 0, sa); }, ibytes});
+        ivars.push_back({"imix_sparse_span_24k_w4", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 24576, 4>), grid, blk, 0, 0, sa); }, ibytes});
+        ivars.push_back({"imix_sparse_span_28k_w5", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 28672, 5>), grid, blk, 0, 0, sa); }, ibytes});
+        ivars.push_back({"imix_sparse_span_32k_w4", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 32768, 4>), grid, blk, 0, 0, sa); }, ibytes});
+        ivars.push_back({"imix_sparse_span_32k_w5", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, 32768, 5>), grid, blk, 0, 0, sa); }, ibytes});
+        ivars.push_back({"imix_desc_span_20k_w6", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_DESC, 1, 20480, 6>), grid, blk, 0, 0, ia); }, ibytes});
+        ivars.push_back({"imix_desc_span_16k_w6", [=]() { hipLaunchKernelGGL((k_parse_span<NEXG_OUT_DESC, 1, 16384, 6>), grid, blk, 0, 0, ia); }, ibytes});
     }
     ivars.push_back({"imix_span_nb1_8k", iparse(k_parse_span<NEXG_OUT_DESC, 1, 8192>), ibytes});
     ivars.push_back({"imix_span_nb2_8k", iparse(k_parse_span<NEXG_OUT_DESC, 2, 8192>), ibytes});
