@@ -83,6 +83,77 @@ def cpu_baseline(batch, workload, count, seconds, nthreads=1):
                       "not buildable here)"}
 
 
+SER_MACS = (b"\x02\0\0\0\0\1", b"\x02\0\0\0\0\2")  # udp_ping's interface MACs (synthetic)
+
+
+def cpu_baseline_ser(params, count, seconds, nthreads=1):
+    """Oracle udp_ping builds (nexo_build_udp4_batch: the restatement of
+    UdpPacketBuilder -> Ipv4PacketBuilder -> EthernetPacketBuilder, one tuple
+    at a time) over the first `count` tuples of the same parameter batch."""
+    import numpy as np
+    from oracle import oracle
+    n = min(count, params[0].numel())
+    host = [t[:n].cpu().numpy().view(np.uint32 if t.element_size() == 4 else np.uint16) for t in params]
+    out = np.empty((n, 42), np.uint8)
+    reps, t = 0, 0.0
+    while t < seconds and reps < 1000:
+        t0 = time.perf_counter()
+        oracle.build_udp4_batch(SER_MACS[0], SER_MACS[1], *host, 64, 2, nthreads=nthreads, out=out)
+        t += time.perf_counter() - t0
+        reps += 1
+    return {"value": round(n * reps / t / 1e6, 3), "unit": "Mpkt/s", "cores": nthreads, "kind": "port",
+            "gib_s": round(42 * n * reps / t / 2**30, 3),
+            "sample": f"{nthreads} thread(s), first {n} tuples of the same parameter batch, {reps} passes "
+                      f"({t:.1f} s), oracle/nex_oracle.c nexo_build_udp4 (literal restatement of the "
+                      "udp_ping.rs:68-109 builder chain; Rust reference not buildable here)"}
+
+
+def write_ceiling(eng, out, args, stream, device):
+    """Write-only HBM stream on the serialize path's own output buffer
+    (nexg_probe_stream out_per_64 = 64: the builders' 16-B non-temporal
+    copy-out shape), same steps / warmup / HIP-event timing."""
+    nbytes = out.numel() // 16384 * 16384
+    _, ks = timed(lambda: eng.probe_write(out, stream=stream), args.steps, args.warmup, stream, device)
+    return {"write_only_gbs": round(nbytes / ks / 1e9, 1),
+            "source": "nexg_probe_stream(out_per_64=64) over the build output buffer, same steps/warmup"}
+
+
+def ser_line(eng, args, F, first, stream, device, rank, world):
+    """configs[3] beside the default run: build+checksum F udp_ping-shape
+    frames (42 B) per GPU from device-resident tuples, with the write-only
+    stream ceiling of the same buffer and the oracle builder on the host."""
+    import torch
+    from nex_amd import dist
+    p = eng.gen_udp4_params(F, first_index=first)
+    out = torch.empty(F * 42, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize(device)
+    alg = F * 42
+    step = lambda: eng.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=SER_MACS[0], dst_mac=SER_MACS[1],
+                                  ip_flags=2, out=out, stream=stream)
+    elapsed, kernel_s = timed(step, args.steps, args.warmup, stream, device)
+    tp = dist.throughput(F, alg, args.steps, elapsed, device)
+    ceil = write_ceiling(eng, out, args, stream, device)
+    if rank != 0:
+        return None
+    ach = alg / kernel_s / 1e9
+    ceil["frac_of_write_only"] = round(ach / ceil["write_only_gbs"], 4)
+    r = {"workload": f"configs[3]: build+checksum {F} udp_ping-shape Eth/IPv4/UDP frames (42 B) per GPU "
+                     "from device-resident parameter tuples (src/dst IPv4, ports, IPv4 id: 14 B read)",
+         "value": tp["value"], "unit": "Mpkt/s", "steps": args.steps, "ms_per_step": tp["ms_per_step"],
+         "gib_s": tp["gib_s"], "bytes_per_gpu": alg,
+         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("ser", "desc"),
+                      "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg,
+                      "basis": "bytes written (SURVEY.md 8(d) SER); parameter reads (14 B/frame) not counted",
+                      "stream_ceilings": ceil}}
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            r["cpu_baseline"] = cpu_baseline_ser(p, 1 << 20, args.cpu_seconds / 2, host_threads())
+        except Exception as e:
+            r["cpu_baseline"] = {"value": None, "error": repr(e)}
+    return r
+
+
 def load_traffic(workload, out_kind):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (FETCH_SIZE
     doubled per the gfx950 correction + WRITE_SIZE), if one exists."""
@@ -223,6 +294,8 @@ def main():
                     help="skip the configs[2] IMIX line reported beside the default UDP64 run")
     ap.add_argument("--no-malformed", action="store_true",
                     help="skip the malformed-mix line (fallback cost) reported beside the default run")
+    ap.add_argument("--no-ser", action="store_true",
+                    help="skip the configs[3] serialize line reported beside the default run")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true",
@@ -287,8 +360,8 @@ def main():
         batch = None
 
         def step():
-            eng.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=b"\x02\0\0\0\0\1",
-                           dst_mac=b"\x02\0\0\0\0\2", ip_flags=2, out=out, stream=stream)
+            eng.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=SER_MACS[0], dst_mac=SER_MACS[1],
+                           ip_flags=2, out=out, stream=stream)
         cfg = {"workload": f"configs[3]: build+checksum {F} udp_ping-shape Eth/IPv4/UDP frames "
                            "(42 B) per GPU from device-resident parameter tuples"}
 
@@ -343,12 +416,17 @@ def main():
     ceilings = None
     if args.workload == "udp64" and not args.e2e and not args.no_imix:
         ceilings = stream_ceilings(eng, batch, args, stream, device)
+    elif args.workload == "ser":
+        ceilings = write_ceiling(eng, out, args, stream, device)
     imix = None
     if args.workload == "udp64" and not args.e2e and not args.no_imix and F == 16 << 20:
         imix = imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
     malformed = None
     if args.workload == "udp64" and not args.e2e and not args.no_malformed and F == 16 << 20:
         malformed = malformed_line(eng, args, F, first, out_kind, stream, device, rank, world)
+    ser = None
+    if args.workload == "udp64" and not args.e2e and not args.no_ser and F == 16 << 20:
+        ser = ser_line(eng, args, F, first, stream, device, rank, world)
 
     if rank != 0:
         return
@@ -375,6 +453,15 @@ def main():
                      "kernel_ms": round(kernel_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": alg_bytes},
     }
+    if args.workload == "ser":
+        res["roofline"]["basis"] = "bytes written (SURVEY.md 8(d) SER); parameter reads (14 B/frame) not counted"
+        res["roofline"]["traffic"] = load_traffic("ser", "desc")  # the build has no output kind; tools/pmc.sh records it as ser.desc
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                res["cpu_baseline"] = cpu_baseline_ser(p, 1 << 20, args.cpu_seconds / 2, host_threads())
+                res["cpu_baseline"]["single_thread"] = cpu_baseline_ser(p, 1 << 20, args.cpu_seconds / 2, 1)
+            except Exception as e:
+                res["cpu_baseline"] = {"value": None, "error": repr(e)}
     if world == 1 and not args.no_cpu_baseline and batch is not None:
         try:
             res["cpu_baseline"] = cpu_baseline(batch, args.workload, 1 << 20, args.cpu_seconds / 2,
@@ -383,7 +470,10 @@ def main():
                                                                 args.cpu_seconds / 2, 1)
         except Exception as e:  # reported, never fatal to the GPU measurement
             res["cpu_baseline"] = {"value": None, "error": repr(e)}
-    if ceilings is not None:
+    if ceilings is not None and args.workload == "ser":
+        res["roofline"]["stream_ceilings"] = dict(
+            ceilings, frac_of_write_only=round(achieved / ceilings["write_only_gbs"], 4))
+    elif ceilings is not None:
         res["roofline"]["stream_ceilings"] = dict(
             ceilings, frac_of_read_only=round(achieved / ceilings["read_only_gbs"], 4),
             frac_of_read64_write8=round(achieved / ceilings["read64_write8_gbs"], 4))
@@ -391,6 +481,8 @@ def main():
         res["imix"] = imix
     if malformed is not None:
         res["malformed"] = malformed
+    if ser is not None:
+        res["ser"] = ser
     print(json.dumps(res), flush=True)
 
 

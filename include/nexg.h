@@ -456,7 +456,11 @@ int nexg_decode_options(nexg_ctx* ctx, const nexg_frames* frames, const nexg_rec
  * (the nexg_desc stream shape): out[i] = {x, i} with x the XOR of the four
  * 16-B chunks lane i % 256 of tile i / 256 loaded (chunks i%256 + 256k).
  * out_per_64 = 0: read only; out[tile] = XOR of the tile's dwords (4 B per
- * 16 KiB). bench.py reports the headline kernel against both. */
+ * 16 KiB). bench.py reports the headline kernel against both.
+ * out_per_64 = 64: write only (the builders' copy-out shape: 16-B
+ * non-temporal stores, 16 KiB per workgroup); `data` is not read (may be
+ * NULL), `out` (16-B aligned) receives `bytes` bytes: dwords {tile, chunk, 0, 0}
+ * per 16-B chunk. bench.py reports the serialize path against it. */
 int nexg_probe_stream(nexg_ctx* ctx, const void* data, uint64_t bytes, uint32_t out_per_64,
                       void* out, void* stream);
 

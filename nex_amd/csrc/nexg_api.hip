@@ -215,13 +215,15 @@ int nexg_decode_options(nexg_ctx* ctx, const nexg_frames* frames, const nexg_rec
 int nexg_probe_stream(nexg_ctx* ctx, const void* data, uint64_t bytes, uint32_t out_per_64,
                       void* out, void* stream) {
     if (!ctx) return NEXG_EINVAL;
-    if (bytes % 16384u != 0 || (bytes && (!data || !out)) || (out_per_64 != 0 && out_per_64 != 8) ||
-        (reinterpret_cast<uint64_t>(data) & 15u) != 0 || (reinterpret_cast<uint64_t>(out) & 7u) != 0)
+    const bool wo = out_per_64 == 64;  // write-only: data unused
+    if (bytes % 16384u != 0 || (bytes && ((!wo && !data) || !out)) ||
+        (out_per_64 != 0 && out_per_64 != 8 && !wo) || (reinterpret_cast<uint64_t>(data) & 15u) != 0 ||
+        (reinterpret_cast<uint64_t>(out) & (wo ? 15u : 7u)) != 0)
         return fail(ctx, NEXG_EINVAL, "probe: bytes must be a multiple of 16384, buffers aligned%s", nullptr);
     if (bytes / 16384u > 0x7FFFFFFFull) return fail(ctx, NEXG_ERANGE, "probe: too many tiles%s", nullptr);
     DeviceGuard g(ctx);
     return hip_status(ctx, nexg::launch_probe_stream(static_cast<const uint8_t*>(data), bytes / 16384u,
-                                                     out_per_64 == 8, out, static_cast<hipStream_t>(stream)),
+                                                     out_per_64, out, static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
 }
 

@@ -250,9 +250,22 @@ __global__ __launch_bounds__(256) void k_probe_stream(const uint8_t* data, void*
     }
 }
 
-hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, bool write8, void* out, hipStream_t s) {
+// write-only calibration stream: the builders' copy-out shape (16-B
+// non-temporal stores, 16 KiB per 256-lane workgroup); out[tile][c] = {tile, c, 0, 0}
+__global__ __launch_bounds__(256) void k_probe_write(uint8_t* out) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u* T = reinterpret_cast<v4u*>(out + (uint64_t)blockIdx.x * 16384u);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t c = threadIdx.x + 256u * k;
+        __builtin_nontemporal_store(v4u{blockIdx.x, c, 0u, 0u}, T + c);
+    }
+}
+
+hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, uint32_t mode, void* out, hipStream_t s) {
     if (tiles == 0) return hipSuccess;
-    if (write8) hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out);
+    if (mode == 64) hipLaunchKernelGGL(k_probe_write, dim3((uint32_t)tiles), dim3(kTile), 0, s, static_cast<uint8_t*>(out));
+    else if (mode == 8) hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out);
     else hipLaunchKernelGGL(k_probe_stream<false>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out);
     return hipGetLastError();
 }

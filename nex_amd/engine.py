@@ -260,6 +260,14 @@ class Engine:
                                                _ptr(out), self._stream(stream)))
         return out
 
+    def probe_write(self, out, stream=None):
+        """Write-only calibration stream (nexg_probe_stream, out_per_64 = 64):
+        the builders' copy-out shape over a uint8 device tensor (whole 16-KiB
+        tiles). Not a reference entry point."""
+        nbytes = out.numel() // 16384 * 16384
+        self._check(self.lib.nexg_probe_stream(self.ctx, None, nbytes, 64, _ptr(out), self._stream(stream)))
+        return out
+
     def checksum(self, batch: FrameBatch, skipword: int, stream=None):
         """util::checksum(buf, skipword) per buffer (util.rs:65)."""
         torch = _torch()

@@ -817,6 +817,40 @@ int nexo_parse_batch(const nexg_frames* frames, uint32_t flags, uint32_t ip_offs
     return 0;
 }
 
+/* udp_ping.rs:68-109 over a tuple batch (the serialize path's CPU baseline:
+ * one nexo_build_udp4 per tuple, static index-range split over nthreads) */
+typedef struct {
+    const nexo_udp4_tuples* p;
+    uint8_t* out;
+    uint64_t begin, end;
+} build_job;
+
+static void* build_worker(void* arg) {
+    build_job* j = (build_job*)arg;
+    const nexo_udp4_tuples* p = j->p;
+    for (uint64_t i = j->begin; i < j->end; i++)
+        nexo_build_udp4(p->src_mac, p->dst_mac, p->src_ip[i], p->dst_ip[i], p->src_port[i], p->dst_port[i],
+                        p->ip_id[i], p->ttl, p->ip_flags, 0, NULL, 0, j->out + 42u * i);
+    return NULL;
+}
+
+int nexo_build_udp4_batch(const nexo_udp4_tuples* p, uint8_t* out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    build_job jobs[256];
+    for (int t = 0; t < nthreads; t++)
+        jobs[t] = (build_job){p, out, p->count * (uint64_t)t / (uint64_t)nthreads,
+                              p->count * (uint64_t)(t + 1) / (uint64_t)nthreads};
+    if (nthreads == 1) {
+        build_worker(&jobs[0]);
+        return 0;
+    }
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, build_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    return 0;
+}
+
 /* ======================= FrameSlice (frame.rs:84-287) =================== */
 
 typedef struct {

@@ -94,6 +94,20 @@ int nexo_build_udp4(const uint8_t src_mac[6], const uint8_t dst_mac[6],
                     uint16_t dport, uint16_t ip_id, uint8_t ttl,
                     uint8_t ip_flags, uint8_t dscp_ecn, const uint8_t* payload,
                     uint32_t payload_len, uint8_t* out);
+/* a batch of udp_ping IPv4 builds with empty payloads, 42 B per tuple at
+ * out + 42 i (the serialize bench's CPU baseline) */
+typedef struct {
+    const uint8_t* src_mac;
+    const uint8_t* dst_mac;
+    const uint32_t* src_ip;
+    const uint32_t* dst_ip;
+    const uint16_t* src_port;
+    const uint16_t* dst_port;
+    const uint16_t* ip_id;
+    uint64_t count;
+    uint8_t ttl, ip_flags;
+} nexo_udp4_tuples;
+int nexo_build_udp4_batch(const nexo_udp4_tuples* p, uint8_t* out, int nthreads);
 int nexo_build_udp6(const uint8_t src_mac[6], const uint8_t dst_mac[6],
                     const uint8_t src_ip[16], const uint8_t dst_ip[16], uint16_t sport,
                     uint16_t dport, uint8_t hop_limit, uint8_t traffic_class,

@@ -47,6 +47,8 @@ def lib():
         L.nexo_build_udp4.restype = I
         L.nexo_build_udp4.argtypes = [P, P, U32, U32, U16, U16, U16, ctypes.c_uint8, ctypes.c_uint8,
                                       ctypes.c_uint8, P, U32, P]
+        L.nexo_build_udp4_batch.restype = I
+        L.nexo_build_udp4_batch.argtypes = [ctypes.POINTER(Udp4Tuples), P, I]
         L.nexo_slice_frame.restype = None
         L.nexo_decode_options.argtypes = [P, ctypes.c_size_t, U32, U32, P]
         L.nexo_decode_options.restype = None
@@ -173,6 +175,32 @@ def build_udp4(src_mac, dst_mac, src_ip, dst_ip, sport, dport, ip_id=0, ttl=64, 
     if n < 0:
         raise ValueError("BuildError::LengthOverflow")
     return out.raw[:n]
+
+
+class Udp4Tuples(ctypes.Structure):
+    _fields_ = [("src_mac", ctypes.c_void_p), ("dst_mac", ctypes.c_void_p), ("src_ip", ctypes.c_void_p),
+                ("dst_ip", ctypes.c_void_p), ("src_port", ctypes.c_void_p), ("dst_port", ctypes.c_void_p),
+                ("ip_id", ctypes.c_void_p), ("count", ctypes.c_uint64), ("ttl", ctypes.c_uint8),
+                ("ip_flags", ctypes.c_uint8)]
+
+
+def build_udp4_batch(src_mac, dst_mac, src_ip, dst_ip, sport, dport, ip_id, ttl=64, ip_flags=0,
+                     nthreads=1, out=None):
+    """udp_ping IPv4 builds (empty payload) over numpy tuple arrays: a
+    (count, 42) uint8 array; `nthreads` static index-range shards."""
+    src_ip = np.ascontiguousarray(src_ip, np.uint32)
+    dst_ip = np.ascontiguousarray(dst_ip, np.uint32)
+    sport = np.ascontiguousarray(sport, np.uint16)
+    dport = np.ascontiguousarray(dport, np.uint16)
+    ip_id = np.ascontiguousarray(ip_id, np.uint16)
+    n = len(src_ip)
+    if out is None:
+        out = np.empty((n, 42), np.uint8)
+    sm, dm = _buf(src_mac)[0], _buf(dst_mac)[0]
+    t = Udp4Tuples(ctypes.cast(sm, ctypes.c_void_p), ctypes.cast(dm, ctypes.c_void_p), src_ip.ctypes.data,
+                   dst_ip.ctypes.data, sport.ctypes.data, dport.ctypes.data, ip_id.ctypes.data, n, ttl, ip_flags)
+    lib().nexo_build_udp4_batch(ctypes.byref(t), out.ctypes.data, nthreads)
+    return out
 
 
 def build_udp6(src_mac, dst_mac, src_ip: bytes, dst_ip: bytes, sport, dport, hop_limit=64,

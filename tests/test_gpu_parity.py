@@ -389,6 +389,14 @@ def test_probe_stream(engine):
     o0 = engine.probe_stream(data, False)
     torch.cuda.synchronize()
     assert (o0.cpu().numpy().view("<u4")[:3] == np.bitwise_xor.reduce(lane_x, axis=1)).all()
+    ow = torch.full((3 * 16384 + 16,), 0xAB, dtype=torch.uint8, device="cuda")
+    engine.probe_write(ow)
+    torch.cuda.synchronize()
+    got = ow.cpu().numpy()
+    want = np.zeros((3, 1024, 4), np.uint32)
+    want[:, :, 0] = np.arange(3)[:, None]
+    want[:, :, 1] = np.arange(1024)[None, :]
+    assert (got[: 3 * 16384].view("<u4") == want.reshape(-1)).all() and (got[3 * 16384:] == 0xAB).all()
 
 
 @pytest.mark.parametrize("workload", [abi.WL_UDP64, abi.WL_IMIX])

@@ -77,6 +77,21 @@ def test_udp_ping_build_golden(oracle):
         oracle.build_udp4(bytes(6), bytes(6), 1, 2, 3, 4, payload=bytes(65535 - 28 + 1))
 
 
+def test_udp4_batch_build_equals_single(oracle):
+    """The serialize bench's CPU baseline (nexo_build_udp4_batch, threaded)
+    builds exactly what the per-tuple restatement builds."""
+    rng = np.random.default_rng(3)
+    n = 1000
+    src, dst = rng.integers(0, 1 << 32, n, dtype=np.uint32), rng.integers(0, 1 << 32, n, dtype=np.uint32)
+    sp, dp, ids = (rng.integers(0, 1 << 16, n, dtype=np.uint16) for _ in range(3))
+    sm, dm = bytes([2, 0, 0, 0, 0, 1]), bytes([2, 0, 0, 0, 0, 2])
+    for th in (1, 3):
+        got = oracle.build_udp4_batch(sm, dm, src, dst, sp, dp, ids, 64, 2, nthreads=th)
+        for i in range(0, n, 7):
+            want = oracle.build_udp4(sm, dm, int(src[i]), int(dst[i]), int(sp[i]), int(dp[i]), int(ids[i]), 64, 2)
+            assert bytes(got[i]) == want
+
+
 # ---- quirks (SURVEY.md Appendix A) -------------------------------------------
 
 def _rec(oracle, fr, flags=0, off=0):
