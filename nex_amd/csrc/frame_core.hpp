@@ -632,42 +632,61 @@ NEXG_HD bool fast_udp4_64(const uint32_t (&w)[16], uint32_t opt_flags, nexg_reco
 }
 
 // Canonical-shape fast path for the IMIX mix: {IPv4 IHL 5, IPv6 without
-// extension headers} x {TCP data offset 5, UDP, ICMP/ICMPv6}, with the IP and
-// UDP lengths exactly covering the frame (no padding). w[k] holds bytes
-// 4k..4k+3 of the frame (little-endian), already zero past `len`; tail_sum
-// is the frame-relative little-endian halfword sum of bytes [80, len) (even
-// frame offsets weigh 1, odd 256; 0 when len <= 80) or any value congruent to
-// it mod 0xFFFF that is 0 only when it is (callers holding an absolute-parity
-// sum of a frame at an odd address pass it x256). One straight-line routine for all six shapes
-// (selects, no per-shape branches) so a mixed wave does not diverge. Returns
-// false when any condition fails; the caller then runs parse_frame, so the
-// result never depends on which path ran. tests/test_core_harness.py checks it.
+// extension headers} x {TCP data offset 5, UDP, ICMP/ICMPv6}. w0[k] holds
+// bytes 4k..4k+3 of the frame (little-endian), already zero past `len`;
+// tail_sum is the frame-relative little-endian halfword sum of bytes
+// [80, tail_end) (even frame offsets weigh 1, odd 256; 0 when tail_end <= 80)
+// or any value congruent to it mod 0xFFFF that is 0 only when it is (callers
+// holding an absolute-parity sum of a frame at an odd address pass it x256).
+// The IP layer ends where the reference's parse ends it (ipv4.rs:372-529: the
+// declared total length, 0 = the whole buffer, clamped to the frame unless
+// strict; ipv6.rs:217-384: 40 + payload length, clamped likewise), so
+// Ethernet padding and over-long declared lengths stay on the fast path when
+// the L4 sum can be formed: the IP end is the frame end, or tail_end (the
+// span kernel's second prefix value sits there), or inside the window (bytes
+// past it masked, no tail). A UDP length word that does not fit the IP
+// payload gives the reference's transport-only layer (udp.rs:197-236, Q14).
+// One straight-line routine for all shapes (selects, no per-shape branches)
+// so a mixed wave does not diverge. Returns false when any condition fails;
+// the caller then runs parse_frame, so the result never depends on which path
+// ran. tests/test_core_harness.py checks it.
 NEXG_HD uint32_t wbyte(const uint32_t (&w)[20], uint32_t i) { return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFu; }
 NEXG_HD uint32_t wbe16(const uint32_t (&w)[20], uint32_t i) { return (wbyte(w, i) << 8) | wbyte(w, i + 1); }
 NEXG_HD uint32_t wle16(const uint32_t (&w)[20], uint32_t i) { return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFFFu; }
 
-NEXG_HD bool fast_canonical80(const uint32_t (&w)[20], uint32_t len, uint32_t opt_flags,
-                              uint64_t tail_sum, nexg_record& r) {
+NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t opt_flags,
+                              uint64_t tail_sum, uint32_t tail_end, nexg_record& r) {
     if (opt_flags & NEXG_PARSE_FROM_IP) return false;
-    const uint32_t et = wbe16(w, 12);
+    const uint32_t et = wbe16(w0, 12);
     const bool v6 = et == 0x86DDu;
     if (!(et == 0x0800u || v6)) return false;
     const uint32_t l4 = v6 ? 54u : 34u;
     if (len < l4 + 8u) return false;
-    const uint32_t n = len - l4;
-    // L3 checks
-    const uint32_t b14 = wbyte(w, 14);
-    const uint32_t proto = v6 ? wbyte(w, 20) : wbyte(w, 23);
-    const uint32_t decl4 = wbe16(w, 16);
-    const bool l3ok = v6 ? ((b14 >> 4) == 6u && wbe16(w, 18) == n)
-                         : (b14 == 0x45u && (decl4 == len - 14u || decl4 == 0u));
+    // L3 checks and the IP end e
+    const bool strict = (opt_flags & NEXG_PARSE_STRICT) != 0;
+    const uint32_t b14 = wbyte(w0, 14);
+    const uint32_t proto = v6 ? wbyte(w0, 20) : wbyte(w0, 23);
+    const uint32_t avail = len - 14u;
+    const uint32_t decl = v6 ? 40u + wbe16(w0, 18) : (wbe16(w0, 16) ? wbe16(w0, 16) : avail);
+    const bool l3ok = (v6 ? (b14 >> 4) == 6u : (b14 == 0x45u && decl >= 20u)) && !(strict && decl > avail);
+    const uint32_t ipl = decl < avail ? decl : avail;  // IP bytes parsed (v4: total_length)
+    const uint32_t e = 14u + ipl;
     const bool tcp = proto == 6u, udp = proto == 17u, icmp = proto == (v6 ? 58u : 1u);
-    if (!l3ok || !(tcp || udp || icmp)) return false;
+    if (!l3ok || !(tcp || udp || icmp) || e < l4 + 8u) return false;
+    const bool inwin = e <= 80u;  // checksummed bytes all in the window
+    if (e != len && e != tail_end && !inwin) return false;
+    const uint32_t n = e - l4;
+    uint32_t w[20];
+#pragma unroll
+    for (int k = 0; k < 20; k++) w[k] = 4u * k >= e ? 0u : (w0[k] & range_mask(4u * k, 0, e));
+    if (inwin) tail_sum = 0;
     // L4 header words at l4 + k (compile-time extraction for both offsets + select)
     auto L = [&](uint32_t k) { return v6 ? wbe16(w, 54u + k) : wbe16(w, 34u + k); };
     auto LE = [&](uint32_t k) { return v6 ? wle16(w, 54u + k) : wle16(w, 34u + k); };
     if (tcp && (n < 20u || (L(12) >> 12) != 5u)) return false;
-    if (udp && L(4) != n) return false;
+    const uint32_t ulen = L(4);
+    const bool q14 = udp && (ulen < 8u || ulen > n);  // no UdpPacket: payload = the L4 bytes
+    if (udp && !q14 && ulen != n) return false;
     // little-endian suffix sums of the window (bytes >= 4k), for the payload starts
     uint32_t suf[21];
     suf[20] = 0;
@@ -705,19 +724,18 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w)[20], uint32_t len, uint32_t op
     const uint32_t l4_calc = fold_complement(t4);
     const uint32_t l4_cs = tcp ? L(16) : (udp ? L(6) : L(2));
     r = nexg_record{};
-    uint32_t fl = NEXG_L_ETHERNET | NEXG_L_IP | (v6 ? NEXG_L_IPV6 : NEXG_L_IPV4) | NEXG_C_L4_CHECKED |
-                  (l4_calc == l4_cs ? NEXG_C_L4_OK : 0u);
+    uint32_t fl = NEXG_L_ETHERNET | NEXG_L_IP | (v6 ? NEXG_L_IPV6 : NEXG_L_IPV4) |
+                  (q14 ? 0u : NEXG_C_L4_CHECKED | (l4_calc == l4_cs ? NEXG_C_L4_OK : 0u));
     fl |= tcp ? (NEXG_L_TRANSPORT | NEXG_L_TCP)
-              : (udp ? (NEXG_L_TRANSPORT | NEXG_L_UDP) : (v6 ? NEXG_L_ICMPV6 : NEXG_L_ICMP));
+              : (udp ? (q14 ? NEXG_L_TRANSPORT : NEXG_L_TRANSPORT | NEXG_L_UDP) : (v6 ? NEXG_L_ICMPV6 : NEXG_L_ICMP));
     if (!v6) {
-        const uint64_t tip = 256ull * (wle16(w, 14) + wle16(w, 18) + wle16(w, 20) + wle16(w, 22) + p4) +
-                             (len - 14u);
+        const uint64_t tip = 256ull * (wle16(w, 14) + wle16(w, 18) + wle16(w, 20) + wle16(w, 22) + p4) + ipl;
         const uint32_t ip_calc = fold_complement(tip);
         const uint32_t ip_cs = wbe16(w, 24);
         fl |= NEXG_C_IP_CHECKED | (ip_calc == ip_cs ? NEXG_C_IP_OK : 0u);
         r.ip_ver_ihl = 0x45;
         r.ip_tos = (uint8_t)wbyte(w, 15);
-        r.ip_length = (uint16_t)(len - 14u);
+        r.ip_length = (uint16_t)ipl;
         r.ip_word = (wbe16(w, 18) << 16) | wbe16(w, 20);
         r.ip_ttl = (uint8_t)wbyte(w, 22);
         r.ip_src = (wbe16(w, 26) << 16) | wbe16(w, 28);
@@ -728,7 +746,7 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w)[20], uint32_t len, uint32_t op
         const uint32_t w0 = (wbe16(w, 14) << 16) | wbe16(w, 16);
         r.ip_ver_ihl = 0x60;
         r.ip_tos = (uint8_t)(w0 >> 20);
-        r.ip_length = (uint16_t)n;
+        r.ip_length = (uint16_t)(decl - 40u);
         r.ip_word = w0 & 0xFFFFFu;
         r.ip_ttl = (uint8_t)wbyte(w, 21);
     }
@@ -737,6 +755,11 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w)[20], uint32_t len, uint32_t op
     r.packet_len = (uint16_t)len;
     r.ethertype = (uint16_t)et;
     r.l3_off = 14;
+    if (q14) {  // frame.rs:550-568: transport layer without a UdpPacket
+        r.payload_off = (uint16_t)l4;
+        r.payload_len = (uint16_t)n;
+        return true;
+    }
     r.l4_off = (uint16_t)l4;
     r.l4_csum = (uint16_t)l4_cs;
     r.l4_csum_calc = (uint16_t)l4_calc;
@@ -762,13 +785,18 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w)[20], uint32_t len, uint32_t op
     return true;
 }
 
-// NEXG_OUT_SPARSE code of a record fast_canonical80 produced: its six shapes
-// are exactly NEXG_SHAPE_V4_UDP..NEXG_SHAPE_V6_ICMP with the payload after the
-// fixed headers (no VLAN), so the code needs no shape search
+// NEXG_OUT_SPARSE code of a record fast_canonical80 produced: its six
+// L4 shapes are exactly NEXG_SHAPE_V4_UDP..NEXG_SHAPE_V6_ICMP when the payload
+// runs from the fixed headers to the frame end (no VLAN), so the code needs no
+// shape search; a padded frame or a transport-only (Q14) layer is an
+// exception (0), as sparse_encode would make it
 NEXG_HD uint32_t canonical80_code(const nexg_record& r) {
     const uint32_t f = r.flags;
     const uint32_t shape = ((f & NEXG_L_IPV6) ? 4u : 1u) + ((f & NEXG_L_UDP) ? 0u : (f & NEXG_L_TCP) ? 1u : 2u);
-    return shape | ((f & NEXG_C_IP_OK) ? NEXG_SPARSE_IP_OK : 0u) | ((f & NEXG_C_L4_OK) ? NEXG_SPARSE_L4_OK : 0u);
+    const uint32_t h = (f & NEXG_L_UDP) ? 8u : (f & NEXG_L_TCP) ? 20u : 4u;
+    const bool coded = (f & NEXG_C_L4_CHECKED) && r.l4_off + h + r.payload_len == r.packet_len;
+    return coded ? shape | ((f & NEXG_C_IP_OK) ? NEXG_SPARSE_IP_OK : 0u) | ((f & NEXG_C_L4_OK) ? NEXG_SPARSE_L4_OK : 0u)
+                 : 0u;
 }
 
 // nexg_sparse_decode (include/nexg.h) on the device: the same table macros

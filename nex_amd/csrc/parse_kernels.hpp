@@ -470,7 +470,7 @@ __global__ __launch_bounds__(256) void k_parse_lane80(ParseArgs a) {
             w[k] = 4u * k < len ? (v & range_mask(4u * k, 0, len)) : 0u;
         }
         // k_tail_sums weights by absolute parity (see k_parse_span)
-        done = fast_canonical80(w, len, a.opt_flags, (uint64_t)tail << (8u * (sh & 1u)), r);
+        done = fast_canonical80(w, len, a.opt_flags, (uint64_t)tail << (8u * (sh & 1u)), len, r);
     }
     if (!done) {
         GlobalFrame f{a.data + off};
@@ -712,7 +712,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // Q weights bytes by absolute parity; fast_canonical80 wants the
         // frame-relative LE sum: x256 (mod 0xFFFF) for a frame at an odd address
         const uint64_t tail = (sh & 1u) ? (uint64_t)tq * 256u : (uint64_t)tq;
-        if (fast_canonical80(w, len, a.opt_flags, tail, r)) {
+        if (fast_canonical80(w, len, a.opt_flags, tail, qend, r)) {
             if (OUT == NEXG_OUT_SPARSE) code = canonical80_code(r);
             if (OUT == NEXG_OUT_RECORD) stage_record(slots + SpanFrame::kSlot * t, r);
         } else {  // declined: the window goes to this lane's slot for pass (B)
@@ -954,7 +954,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (fast) {
 #pragma unroll
             for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
-            done = fast_canonical80(w, len, a.opt_flags, want_tail ? (uint32_t)(qb - qa) : 0u, r);
+            done = fast_canonical80(w, len, a.opt_flags, want_tail ? (uint32_t)(qb - qa) : 0u, len, r);
         }
         if (!done) {
             GlobalFrame f{a.data + off};

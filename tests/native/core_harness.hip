@@ -36,7 +36,7 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                 memcpy(w80, g, len < 80 ? len : 80);
                 const uint64_t base = reinterpret_cast<uint64_t>(g);
                 const uint64_t tail = len > 80 ? nexg::global_le_sum(base + 80, base + len) : 0;
-                if (!nexg::fast_canonical80(w80, (uint32_t)len, flags, tail, r)) {
+                if (!nexg::fast_canonical80(w80, (uint32_t)len, flags, tail, (uint32_t)len, r)) {
                     nexg::WinFrame f{slot, g, o, wlen};
                     nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
                 }
@@ -61,16 +61,16 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                 };
                 uint32_t w80[20] = {0};
                 memcpy(w80, g, len < 80 ? len : 80);
-                const uint32_t tail = len > 80 ? Q(o + (uint32_t)len) - Q(o + 80u) : 0u;
-                if (nexg::fast_canonical80(w80, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, r)) {
+                // the second prefix value at span_tail_end (the IP end of a padded frame)
+                const uint32_t te = nexg::span_tail_end(w80[3], w80[4], (uint32_t)len, flags);
+                const uint32_t tail = len > 80 ? Q(o + te) - Q(o + 80u) : 0u;
+                if (nexg::fast_canonical80(w80, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, te, r)) {
                     // the span kernel stores canonical80_code for these: it must be the encoder's code
                     if (nexg::canonical80_code(r) != nexg::sparse_encode(r, flags, ip_offset)) return -2;
                 } else {
                     alignas(16) uint8_t s64[80];
                     memcpy(s64, w80, 80);
-                    const uint32_t te = nexg::span_tail_end(w80[3], w80[4], (uint32_t)len, flags);
-                    const uint32_t tail2 = te > 80 ? Q(o + te) - Q(o + 80u) : 0u;
-                    nexg::SpanFrame f{s64, g, te, par, tail2};
+                    nexg::SpanFrame f{s64, g, te, par, tail};
                     nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
                     if (f.d.which()) {
                         const uint64_t A = reinterpret_cast<uint64_t>(g) + f.d.off();

@@ -109,6 +109,27 @@ def test_canonical_fast_path_on_imix(oracle):
         fr[min(j, len(fr) - 1)] = int(rng.choice([0, 0x45, 0x60, 6, 17, 58, 1, 0x50, int(rng.integers(256))]))
         frames.append(bytes(fr))
         frames.append(f[: int(rng.integers(30, len(f) + 1))])
+    # the App. C kinds the fast path now keeps: Ethernet padding (IP end at
+    # the frame end, inside the window, at the span's second prefix value, or
+    # in 80..83 where it must decline), declared IP lengths past the frame
+    # (clamped unless strict) or 0, UDP length words that do not fit (Q14)
+    for f in base[:1500]:
+        v4 = f[12:14] == b"\x08\x00"
+        frames.append(f + bytes(rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8)))
+        fr = bytearray(f)
+        j = 16 if v4 else 18
+        fr[j:j + 2] = int(rng.choice([0, int(rng.integers(0, 1 << 16)), len(f) - (14 if v4 else 54) + 1])
+                          ).to_bytes(2, "big")
+        frames.append(bytes(fr))
+        fr = bytearray(f)
+        l4 = 34 if v4 else 54
+        fr[l4 + 4] = int(rng.integers(256))
+        frames.append(bytes(fr))
+    for e in (64, 79, 80, 81, 83, 84, 85, 100):  # IPv4/UDP of IP end e, padded by 1..40
+        for pad in (1, 3, 4, 17, 40):
+            body = bytes(rng.integers(0, 256, e - 42, dtype=np.uint8))
+            frames.append(helpers._eth(helpers._ipv4(helpers._udp(body), 17)) + bytes(pad))
+            frames.append(helpers._eth(helpers._ipv6(helpers._udp(bytes(max(0, e - 62))), 17), 0x86DD) + bytes(pad))
     buf, offs, lens = pack(frames, 4)
     for flags in (0, abi.PARSE_STRICT):
         want = oracle.parse_packed(buf, offs, lens, flags=flags)
