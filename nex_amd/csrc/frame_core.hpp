@@ -631,48 +631,72 @@ NEXG_HD bool fast_udp4_64(const uint32_t (&w)[16], uint32_t opt_flags, nexg_reco
     return true;
 }
 
-// Canonical-shape fast path for the IMIX mix: {IPv4 IHL 5, IPv6 without
-// extension headers} x {TCP data offset 5, UDP, ICMP/ICMPv6}. w0[k] holds
-// bytes 4k..4k+3 of the frame (little-endian), already zero past `len`;
-// tail_sum is the frame-relative little-endian halfword sum of bytes
-// [80, tail_end) (even frame offsets weigh 1, odd 256; 0 when tail_end <= 80)
-// or any value congruent to it mod 0xFFFF that is 0 only when it is (callers
-// holding an absolute-parity sum of a frame at an odd address pass it x256).
-// The IP layer ends where the reference's parse ends it (ipv4.rs:372-529: the
-// declared total length, 0 = the whole buffer, clamped to the frame unless
-// strict; ipv6.rs:217-384: 40 + payload length, clamped likewise), so
-// Ethernet padding and over-long declared lengths stay on the fast path when
-// the L4 sum can be formed: the IP end is the frame end, or tail_end (the
-// span kernel's second prefix value sits there), or inside the window (bytes
-// past it masked, no tail). A UDP length word that does not fit the IP
-// payload gives the reference's transport-only layer (udp.rs:197-236, Q14).
-// One straight-line routine for all shapes (selects, no per-shape branches)
-// so a mixed wave does not diverge. Returns false when any condition fails;
-// the caller then runs parse_frame, so the result never depends on which path
-// ran. tests/test_core_harness.py checks it.
+// Register fast path over a frame's first 80 bytes: every frame whose Frame
+// (frame.rs:570-658) is decided by those bytes plus one L4 tail sum, i.e. the
+// canonical IMIX shapes {IPv4 IHL 5, IPv6 without extension headers} x {TCP
+// data offset 5, UDP, ICMP/ICMPv6} and the common ways real traffic leaves
+// them: other EtherTypes (Ethernet only, Q3), an IP header that does not parse
+// (non-strict: ip = Some(all None), Q4/Q12), other IP protocols and short
+// ICMP (no transport layer, Q9/Q15), a UDP length word that does not fit or a
+// TCP header that does not parse (transport layer only, Q14), and IP lengths
+// that end the layer before the frame end (Ethernet padding) or past it
+// (clamped unless strict). w0[k] holds bytes 4k..4k+3 of the frame
+// (little-endian), already zero past `len`; tail_sum is the frame-relative
+// little-endian halfword sum of bytes [80, tail_end) (even frame offsets weigh
+// 1, odd 256; 0 when tail_end <= 80) or any value congruent to it mod 0xFFFF
+// that is 0 only when it is (callers holding an absolute-parity sum of a frame
+// at an odd address pass it x256). The IP layer ends where the reference's
+// parse ends it (ipv4.rs:372-529: the declared total length, 0 = the whole
+// buffer, clamped to the frame unless strict; ipv6.rs:217-384: 40 + payload
+// length, clamped likewise); its checksummed bytes must end at the frame end,
+// at tail_end (the span kernel's second prefix value sits there) or inside the
+// window (bytes past it masked, no tail). Declined (false, the caller runs
+// parse_frame, so the result never depends on which path ran): FROM_IP,
+// ARP, VLAN tags under NEXG_PARSE_VLAN, IPv4 options, TCP options, IPv6
+// extension headers, a UDP datagram shorter than its IP payload, strict-mode
+// errors, frames under 14 B. Straight-line selects across the shapes, so a
+// mixed wave does not diverge. tests/test_core_harness.py checks it.
 NEXG_HD uint32_t wbyte(const uint32_t (&w)[20], uint32_t i) { return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFu; }
 NEXG_HD uint32_t wbe16(const uint32_t (&w)[20], uint32_t i) { return (wbyte(w, i) << 8) | wbyte(w, i + 1); }
 NEXG_HD uint32_t wle16(const uint32_t (&w)[20], uint32_t i) { return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFFFu; }
 
 NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t opt_flags,
                               uint64_t tail_sum, uint32_t tail_end, nexg_record& r) {
-    if (opt_flags & NEXG_PARSE_FROM_IP) return false;
+    if ((opt_flags & NEXG_PARSE_FROM_IP) || len < 14u) return false;
     const uint32_t et = wbe16(w0, 12);
-    const bool v6 = et == 0x86DDu;
-    if (!(et == 0x0800u || v6)) return false;
-    const uint32_t l4 = v6 ? 54u : 34u;
-    if (len < l4 + 8u) return false;
-    // L3 checks and the IP end e
+    const bool v6 = et == 0x86DDu, v4 = et == 0x0800u;
     const bool strict = (opt_flags & NEXG_PARSE_STRICT) != 0;
-    const uint32_t b14 = wbyte(w0, 14);
-    const uint32_t proto = v6 ? wbyte(w0, 20) : wbyte(w0, 23);
     const uint32_t avail = len - 14u;
-    const uint32_t decl = v6 ? 40u + wbe16(w0, 18) : (wbe16(w0, 16) ? wbe16(w0, 16) : avail);
-    const bool l3ok = (v6 ? (b14 >> 4) == 6u : (b14 == 0x45u && decl >= 20u)) && !(strict && decl > avail);
+    const uint32_t b14 = wbyte(w0, 14), hl = b14 & 15u, decl16 = wbe16(w0, 16);
+    // parse_ipv4 / parse_ipv6 failures before the options / extension walk
+    const bool bad_ip = v4 ? (avail < 20u || (b14 >> 4) != 4u || hl < 5u || 4u * hl > avail ||
+                              (decl16 != 0u && decl16 < 4u * hl))
+                           : (avail < 40u || (b14 >> 4) != 6u);
+    if (!(v4 || v6) || bad_ip) {
+        if ((v4 || v6) ? strict
+                       : (et == 0x0806u ||
+                          ((opt_flags & NEXG_PARSE_VLAN) && (et == 0x8100u || et == 0x88A8u || et == 0x9100u))))
+            return false;
+        r = nexg_record{};  // Ethernet only (payload = the rest) or ip = Some(all None) (no payload)
+        r.flags = NEXG_L_ETHERNET | ((v4 || v6) ? NEXG_L_IP : 0u);
+        r.packet_len = (uint16_t)len;
+        r.ethertype = (uint16_t)et;
+        r.l3_off = 14;
+        if (!(v4 || v6)) {
+            r.payload_off = (uint16_t)(avail ? 14u : 0u);
+            r.payload_len = (uint16_t)avail;
+        }
+        return true;
+    }
+    if (v4 && hl != 5u) return false;  // options
+    const uint32_t l4 = v6 ? 54u : 34u;
+    const uint32_t decl = v6 ? 40u + wbe16(w0, 18) : (decl16 ? decl16 : avail);
+    if (strict && decl > avail) return false;
     const uint32_t ipl = decl < avail ? decl : avail;  // IP bytes parsed (v4: total_length)
-    const uint32_t e = 14u + ipl;
-    const bool tcp = proto == 6u, udp = proto == 17u, icmp = proto == (v6 ? 58u : 1u);
-    if (!l3ok || !(tcp || udp || icmp) || e < l4 + 8u) return false;
+    const uint32_t e = 14u + ipl;                      // >= l4
+    const uint32_t raw = v6 ? wbyte(w0, 20) : wbyte(w0, 23);
+    const uint32_t pv = ip_next_protocol_value(raw);
+    if (v6 && (pv == 0u || pv == 43u || pv == 44u || pv == 60u)) return false;  // extension headers
     const bool inwin = e <= 80u;  // checksummed bytes all in the window
     if (e != len && e != tail_end && !inwin) return false;
     const uint32_t n = e - l4;
@@ -683,10 +707,14 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     // L4 header words at l4 + k (compile-time extraction for both offsets + select)
     auto L = [&](uint32_t k) { return v6 ? wbe16(w, 54u + k) : wbe16(w, 34u + k); };
     auto LE = [&](uint32_t k) { return v6 ? wle16(w, 54u + k) : wle16(w, 34u + k); };
-    if (tcp && (n < 20u || (L(12) >> 12) != 5u)) return false;
-    const uint32_t ulen = L(4);
-    const bool q14 = udp && (ulen < 8u || ulen > n);  // no UdpPacket: payload = the L4 bytes
-    if (udp && !q14 && ulen != n) return false;
+    const bool tcp = pv == 6u, udp = pv == 17u, icmp = pv == (v6 ? 58u : 1u);
+    const uint32_t doff = L(12) >> 12, ulen = L(4);
+    const bool tfail = tcp && (n < 20u || doff < 5u || 4u * doff > n);  // no TcpPacket
+    const bool q14 = udp && (n < 8u || ulen < 8u || ulen > n);          // no UdpPacket
+    if ((tcp && !tfail && doff != 5u) || (udp && !q14 && ulen != n)) return false;
+    const bool tonly = tfail || q14;                                  // transport layer, no packet
+    const bool none = !(tcp || udp || icmp) || (icmp && n < 8u);      // no transport layer
+    const bool l4ok = !(tonly || none);
     // little-endian suffix sums of the window (bytes >= 4k), for the payload starts
     uint32_t suf[21];
     suf[20] = 0;
@@ -719,17 +747,18 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     else if (udp) hdr = LE(0) + LE(2);
     else hdr = LE(0);
     uint64_t t4 = 256ull * ((icmp && !v6 ? 0u : pseudo) + hdr + restsum);
-    t4 += (icmp && !v6) ? 0u : (proto + n);  // pseudo proto + length (BE constants)
-    if (udp) t4 += n;                       // UDP length word as serialised
+    t4 += (icmp && !v6) ? 0u : (pv + n);  // pseudo proto + length (BE constants)
+    if (udp) t4 += n;                     // UDP length word as serialised
     const uint32_t l4_calc = fold_complement(t4);
     const uint32_t l4_cs = tcp ? L(16) : (udp ? L(6) : L(2));
     r = nexg_record{};
-    uint32_t fl = NEXG_L_ETHERNET | NEXG_L_IP | (v6 ? NEXG_L_IPV6 : NEXG_L_IPV4) |
-                  (q14 ? 0u : NEXG_C_L4_CHECKED | (l4_calc == l4_cs ? NEXG_C_L4_OK : 0u));
-    fl |= tcp ? (NEXG_L_TRANSPORT | NEXG_L_TCP)
-              : (udp ? (q14 ? NEXG_L_TRANSPORT : NEXG_L_TRANSPORT | NEXG_L_UDP) : (v6 ? NEXG_L_ICMPV6 : NEXG_L_ICMP));
-    if (!v6) {
-        const uint64_t tip = 256ull * (wle16(w, 14) + wle16(w, 18) + wle16(w, 20) + wle16(w, 22) + p4) + ipl;
+    uint32_t fl = NEXG_L_ETHERNET | NEXG_L_IP | (v6 ? NEXG_L_IPV6 : NEXG_L_IPV4) | ((tcp || udp) ? NEXG_L_TRANSPORT : 0u);
+    if (l4ok)
+        fl |= NEXG_C_L4_CHECKED | (l4_calc == l4_cs ? NEXG_C_L4_OK : 0u) |
+              (tcp ? NEXG_L_TCP : udp ? NEXG_L_UDP : v6 ? NEXG_L_ICMPV6 : NEXG_L_ICMP);
+    if (!v6) {  // ipv4.rs:932-938 over to_bytes(): total_length = 20 + payload, protocol value()
+        const uint64_t tip =
+            256ull * (wle16(w, 14) + wle16(w, 18) + wle16(w, 20) + (wbyte(w, 22) | pv << 8) + p4) + ipl;
         const uint32_t ip_calc = fold_complement(tip);
         const uint32_t ip_cs = wbe16(w, 24);
         fl |= NEXG_C_IP_CHECKED | (ip_calc == ip_cs ? NEXG_C_IP_OK : 0u);
@@ -743,20 +772,20 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
         r.ip_csum = (uint16_t)ip_cs;
         r.ip_csum_calc = (uint16_t)ip_calc;
     } else {
-        const uint32_t w0 = (wbe16(w, 14) << 16) | wbe16(w, 16);
+        const uint32_t w6 = (wbe16(w, 14) << 16) | wbe16(w, 16);
         r.ip_ver_ihl = 0x60;
-        r.ip_tos = (uint8_t)(w0 >> 20);
+        r.ip_tos = (uint8_t)(w6 >> 20);
         r.ip_length = (uint16_t)(decl - 40u);
-        r.ip_word = w0 & 0xFFFFFu;
+        r.ip_word = w6 & 0xFFFFFu;
         r.ip_ttl = (uint8_t)wbyte(w, 21);
     }
     r.flags = fl;
-    r.ip_proto = (uint8_t)proto;
+    r.ip_proto = (uint8_t)pv;
     r.packet_len = (uint16_t)len;
     r.ethertype = (uint16_t)et;
     r.l3_off = 14;
-    if (q14) {  // frame.rs:550-568: transport layer without a UdpPacket
-        r.payload_off = (uint16_t)l4;
+    if (!l4ok) {  // frame.rs:530-568 / 624-658: the IP payload is the Frame's payload
+        r.payload_off = (uint16_t)(n ? l4 : 0u);
         r.payload_len = (uint16_t)n;
         return true;
     }
@@ -785,16 +814,20 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     return true;
 }
 
-// NEXG_OUT_SPARSE code of a record fast_canonical80 produced: its six
-// L4 shapes are exactly NEXG_SHAPE_V4_UDP..NEXG_SHAPE_V6_ICMP when the payload
-// runs from the fixed headers to the frame end (no VLAN), so the code needs no
-// shape search; a padded frame or a transport-only (Q14) layer is an
-// exception (0), as sparse_encode would make it
+// NEXG_OUT_SPARSE code of a record fast_canonical80 produced, without the
+// encoder's shape search: its L4 records are exactly NEXG_SHAPE_V4_UDP ..
+// NEXG_SHAPE_V6_ICMP and its records without a transport layer
+// NEXG_SHAPE_V4_OTHER / V6_OTHER when the payload runs from the fixed
+// headers to the frame end (no VLAN), Ethernet-only and all-None IP records
+// are NEXG_SHAPE_ETH_ONLY / IP_NONE; a padded frame or a transport layer
+// without a packet (Q14) is an exception (0), as sparse_encode would make it
 NEXG_HD uint32_t canonical80_code(const nexg_record& r) {
     const uint32_t f = r.flags;
-    const uint32_t shape = ((f & NEXG_L_IPV6) ? 4u : 1u) + ((f & NEXG_L_UDP) ? 0u : (f & NEXG_L_TCP) ? 1u : 2u);
-    const uint32_t h = (f & NEXG_L_UDP) ? 8u : (f & NEXG_L_TCP) ? 20u : 4u;
-    const bool coded = (f & NEXG_C_L4_CHECKED) && r.l4_off + h + r.payload_len == r.packet_len;
+    if (!(f & (NEXG_L_IPV4 | NEXG_L_IPV6))) return (f & NEXG_L_IP) ? (uint32_t)NEXG_SHAPE_IP_NONE : (uint32_t)NEXG_SHAPE_ETH_ONLY;
+    const bool v6 = (f & NEXG_L_IPV6) != 0, l4 = (f & NEXG_C_L4_CHECKED) != 0;
+    const uint32_t shape = !l4 ? (v6 ? 9u : 8u) : ((v6 ? 4u : 1u) + ((f & NEXG_L_UDP) ? 0u : (f & NEXG_L_TCP) ? 1u : 2u));
+    const uint32_t end = !l4 ? (v6 ? 54u : 34u) : r.l4_off + ((f & NEXG_L_UDP) ? 8u : (f & NEXG_L_TCP) ? 20u : 4u);
+    const bool coded = (l4 || !(f & NEXG_L_TRANSPORT)) && end + r.payload_len == r.packet_len;
     return coded ? shape | ((f & NEXG_C_IP_OK) ? NEXG_SPARSE_IP_OK : 0u) | ((f & NEXG_C_L4_OK) ? NEXG_SPARSE_L4_OK : 0u)
                  : 0u;
 }
