@@ -32,9 +32,11 @@ for s in ${STEPS:-tests}; do
     benchimix) step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5 ;;
     spanvar) for v in 1 2 2d; do step bench_imix_span$v 300 env NEXG_SPAN=$v python bench.py --workload imix --steps 20 --warmup 20 --no-cpu-baseline; done ;;
     pmc) step pmc 900 bash tools/pmc.sh ;;
-    prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed
+    prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed --no-ser
           step prof_pcap 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pcap -o run -- python3 bench.py --workload imix_pcap --steps 60 --warmup 25 --no-cpu-baseline
-          step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 60 --warmup 25 --no-cpu-baseline ;;
+          step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 60 --warmup 25 --no-cpu-baseline
+          step prof_malformed 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_malformed -o run -- python3 bench.py --workload malformed --steps 60 --warmup 25 --no-cpu-baseline
+          step prof_ser 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser -o run -- python3 bench.py --workload ser --steps 60 --warmup 25 --no-cpu-baseline ;;
   esac
 done
 echo done

@@ -12,7 +12,7 @@ CONFIGS=${CONFIGS:-"udp64.sparse imix.sparse imix_pcap.sparse malformed.sparse u
 for cfg in $CONFIGS; do
   wl=${cfg%.*}; out=${cfg#*.}
   for c in FETCH_SIZE WRITE_SIZE; do
-    run ${cfg}_$c 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc/${cfg}_$c -o run -- python3 bench.py --workload $wl --out $out --steps 5 --warmup 1 --no-cpu-baseline --no-imix --no-malformed
+    run ${cfg}_$c 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc/${cfg}_$c -o run -- python3 bench.py --workload $wl --out $out --steps 5 --warmup 1 --no-cpu-baseline --no-imix --no-malformed --no-ser
   done
 done
 echo done
