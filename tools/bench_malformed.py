@@ -7,6 +7,8 @@ algorithmic bytes, share of exception slots). The clean IMIX row is the
 baseline; the spread says which fallback costs what.
 
 usage: python tools/bench_malformed.py [--steps K] [--warmup W] [--kinds a,b]
+       [--libs A.so,B.so]   (A/B: the same batches timed with each build of
+                             libnexg.so in one process, interleaved A B A B)
 """
 import argparse
 import json
@@ -24,11 +26,16 @@ def main():
     ap.add_argument("--distinct", type=int, default=1 << 20)
     ap.add_argument("--tiles", type=int, default=16)
     ap.add_argument("--kinds", default="")
+    ap.add_argument("--libs", default="")
     args = ap.parse_args()
     import torch
-    from nex_amd import abi, workloads
+    from nex_amd import _lib, abi, workloads
     from nex_amd.engine import Engine
-    eng = Engine(0)
+    engines = []
+    for path in (args.libs.split(",") if args.libs else [_lib.LIB_PATH]):
+        _lib._lib, _lib.LIB_PATH = None, os.path.abspath(path)
+        engines.append(Engine(0))
+    eng = engines[0]
     stream = torch.cuda.current_stream()
     kinds = args.kinds.split(",") if args.kinds else ["clean"] + list(workloads.MUTATIONS) + ["all"]
     for k in kinds:
@@ -37,20 +44,27 @@ def main():
         mix, counts = workloads.malformed_mix(eng, args.distinct, mutate_share=share, kinds=sel)
         b = workloads.tiled(mix, args.tiles)
         out = torch.empty(Engine.out_bytes(abi.OUT_SPARSE, b.count), dtype=torch.uint8, device="cuda")
-        for _ in range(args.warmup):
-            eng.parse(b, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        e0.record(stream)
-        for _ in range(args.steps):
-            eng.parse(b, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        s = e0.elapsed_time(e1) / 1e3 / args.steps
+        def timed(e):
+            for _ in range(args.warmup):
+                e.parse(b, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record(stream)
+            for _ in range(args.steps):
+                e.parse(b, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / 1e3 / args.steps
+        rounds = 2 if len(engines) > 1 else 1
+        times = [[timed(e) for e in engines] for _ in range(rounds)]
+        s = min(t[0] for t in times)
         exc = float((out[: b.count] == 0).float().mean().item())
-        print(json.dumps({"kind": k, "frames": b.count, "bytes": b.total_bytes, "kernel_ms": round(s * 1e3, 4),
-                          "mpkt_s": round(b.count / s / 1e6, 1), "frac": round(b.total_bytes / s / 8e12, 4),
-                          "exception_share": round(exc, 4), "mutated": counts.get(k, None)}), flush=True)
+        line = {"kind": k, "frames": b.count, "bytes": b.total_bytes, "kernel_ms": round(s * 1e3, 4),
+                "mpkt_s": round(b.count / s / 1e6, 1), "frac": round(b.total_bytes / s / 8e12, 4),
+                "exception_share": round(exc, 4), "mutated": counts.get(k, None)}
+        if len(engines) > 1:
+            line["kernel_ms_by_lib"] = [[round(x * 1e3, 4) for x in t] for t in times]
+        print(json.dumps(line), flush=True)
         del b, mix, out
         torch.cuda.empty_cache()
 
