@@ -15,6 +15,11 @@ import numpy as np
 from . import abi
 
 MUTATIONS = ("truncate", "pad", "ip_length", "ver_ihl", "l4_length", "ipv6_hbh", "vlan", "proto200", "random")
+#: not in the App. C mix; selectable through `kinds` (tools/bench_malformed.py):
+#: tcp_ts = the real-traffic TCP shape, NOP NOP Timestamps (12 B) after the
+#: TCP header of a TCP frame, data offset 8 (checksums left stale)
+EXTRA = ("tcp_ts",)
+_ALL = MUTATIONS + EXTRA
 
 
 def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share: float = 0.5,
@@ -30,12 +35,12 @@ def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share
     data = base.data.cpu().numpy()[: offs[-1]]
     lens = np.diff(offs)
     rng = np.random.default_rng(seed)
-    pick = np.array([MUTATIONS.index(k) for k in kinds])
+    pick = np.array([_ALL.index(k) for k in kinds])
     kind = np.where(rng.random(count) < mutate_share, pick[rng.integers(0, len(pick), count)], -1)
     # per-frame byte edits on a copy of the frame bytes (lengths unchanged)
     buf = data.copy()
     eth_v4 = (buf[offs[:-1] + 12] == 0x08) & (buf[offs[:-1] + 13] == 0x00)
-    sel = lambda k: np.nonzero(kind == MUTATIONS.index(k))[0]
+    sel = lambda k: np.nonzero(kind == _ALL.index(k))[0]
     i = sel("ip_length")  # bytes 16..17 (IPv4 total length) / 18..19 (IPv6 payload length)
     pos = offs[i] + np.where(eth_v4[i], 16, 18)
     v = rng.integers(0, 1 << 16, len(i))
@@ -63,6 +68,9 @@ def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share
     hbh = sel("ipv6_hbh")
     hbh = hbh[~eth_v4[hbh]]
     ins[hbh] = 8
+    tts = sel("tcp_ts")
+    tts = tts[buf[offs[tts] + np.where(eth_v4[tts], 23, 20)] == 6]
+    ins[tts] = 12
     new_len = new_len + pad + ins
     new_offs = np.zeros(count + 1, np.int64)
     np.cumsum(new_len, out=new_offs[1:])
@@ -80,6 +88,15 @@ def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share
             f = np.concatenate([f, rng.integers(0, 256, pad[j], dtype=np.uint8)])
         elif ins[j] == 4:  # 802.1Q tag in front of the EtherType (frame[12:14])
             f = np.concatenate([f[:12], np.array([0x81, 0, 0, 0x64], np.uint8), f[12:]])
+        elif ins[j] == 12:  # NOP NOP Timestamps after the TCP header, data offset 8
+            l4 = 34 if eth_v4[j] else 54
+            g = f.copy()
+            g[l4 + 12] = (8 << 4) | (g[l4 + 12] & 0x0F)
+            k = 16 if eth_v4[j] else 18
+            v = ((int(g[k]) << 8) | int(g[k + 1])) + 12
+            g[k], g[k + 1] = v >> 8, v & 0xFF
+            ts = np.concatenate([np.array([1, 1, 8, 10], np.uint8), rng.integers(0, 256, 8, dtype=np.uint8)])
+            f = np.concatenate([g[:l4 + 20], ts, g[l4 + 20:]])
         elif ins[j] == 8:  # hop-by-hop header carrying the original next header
             nh = f[20]
             g = f.copy()
@@ -90,7 +107,7 @@ def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share
         out[new_offs[j]:new_offs[j] + len(f)] = f
     dev = torch.from_numpy(np.concatenate([out, np.zeros(16, np.uint8)])).to(engine.torch_device)
     doffs = torch.from_numpy(new_offs).to(engine.torch_device)
-    counts = {m: int((kind == k).sum()) for k, m in enumerate(MUTATIONS)}
+    counts = {m: int((kind == k).sum()) for k, m in enumerate(_ALL) if m in kinds}
     counts["unmodified"] = int((kind < 0).sum())
     return FrameBatch(data=dev[: int(new_offs[-1])], count=count, offsets=doffs), counts
 

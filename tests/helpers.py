@@ -287,6 +287,41 @@ def vlan(frame: bytes, tags, tpids=None) -> bytes:
     return frame[:12] + ins + frame[12:]
 
 
+def tcp_ts_frames(oracle, base, rng, fix_checksums=True):
+    """Real-traffic TCP shape: NOP, NOP, Timestamps (RFC 7323) inserted after
+    the 20-B TCP header of every TCP frame in `base` (IPv4 and IPv6), data
+    offset 8, IP lengths grown by 12; with fix_checksums the oracle's computed
+    IPv4 / TCP checksums are written back (valid frames), else left stale.
+    Plus edge variants: the option bytes perturbed (other layouts), doff 8
+    without room for the options, and truncated copies."""
+    out = []
+    for f in base:
+        v4 = f[12:14] == b"\x08\x00"
+        l4 = 34 if v4 else 54
+        if len(f) < l4 + 20 or f[23 if v4 else 20] != 6:
+            continue
+        ts = bytes([1, 1, 8, 10]) + bytes(rng.integers(0, 256, 8, dtype=np.uint8))
+        g = bytearray(f[:l4 + 20] + ts + f[l4 + 20:])
+        g[l4 + 12] = (8 << 4) | (g[l4 + 12] & 0x0F)
+        if v4:
+            tl = int.from_bytes(g[16:18], "big") + 12
+            g[16:18] = tl.to_bytes(2, "big")
+        else:
+            pl = int.from_bytes(g[18:20], "big") + 12
+            g[18:20] = pl.to_bytes(2, "big")
+        if fix_checksums:
+            r = oracle.parse_frame(bytes(g))
+            if v4:
+                g[24:26] = int(r["ip_csum_calc"]).to_bytes(2, "big")
+            g[l4 + 16:l4 + 18] = int(r["l4_csum_calc"]).to_bytes(2, "big")
+        out.append(bytes(g))
+        h = bytearray(g)
+        h[l4 + 20 + int(rng.integers(4))] = int(rng.choice([0, 1, 2, 3, 8, 10, 255]))
+        out.append(bytes(h))
+        out.append(bytes(g[: int(rng.integers(l4, len(g)))]))
+    return out
+
+
 def vlan_frames():
     """VLAN-extension cases: single / double / QinQ tags over every inner type,
     truncated tags, three tags (only two unwrapped)."""

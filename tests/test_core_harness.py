@@ -125,6 +125,8 @@ def test_canonical_fast_path_on_imix(oracle):
         l4 = 34 if v4 else 54
         fr[l4 + 4] = int(rng.integers(256))
         frames.append(bytes(fr))
+    frames += helpers.tcp_ts_frames(oracle, base[:1500], rng)  # TCP timestamps (register fast path)
+    frames += helpers.tcp_ts_frames(oracle, base[1500:2000], rng, fix_checksums=False)
     for e in (64, 79, 80, 81, 83, 84, 85, 100):  # IPv4/UDP of IP end e, padded by 1..40
         for pad in (1, 3, 4, 17, 40):
             body = bytes(rng.integers(0, 256, e - 42, dtype=np.uint8))

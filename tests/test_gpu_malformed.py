@@ -59,3 +59,22 @@ def test_tiled_repeats(engine, mix):
     for k in range(3):
         assert (d3[k * batch.count:(k + 1) * batch.count] == d1).all()
     assert int(t.offsets[-1].item()) == 3 * span
+
+
+def test_tcp_timestamps_match_oracle(engine, oracle):
+    """The real-traffic TCP shape (NOP NOP Timestamps, data offset 8; the
+    register fast path takes it behind IPv4 and IPv6, damaged layouts go to
+    the generic core) at every byte alignment the packed IMIX layout
+    produces, in record and sparse form."""
+    batch, counts = workloads.malformed_mix(engine, 40000, seed=78, kinds=("tcp_ts",))
+    assert counts["tcp_ts"] > 15000
+    frames = host_frames(batch)
+    want = oracle.parse_frames(frames)
+    assert ((want["l4_nopt"] == 3) & (want["l4_length"] == 32)).sum() > 3000
+    got = engine.parse_to_numpy(batch, out_kind=abi.OUT_RECORD)
+    helpers.records_equal(got, want, frames, "tcp_ts record")
+    d = np.zeros(len(frames), abi.DESC_DTYPE)
+    for n in abi.DESC_DTYPE.names:
+        d[n] = want[n]
+    got = engine.parse_to_numpy(batch, out_kind=abi.OUT_SPARSE)
+    helpers.records_equal(got, d, frames, "tcp_ts sparse")
