@@ -612,11 +612,26 @@ int nexg_pcap_read_batch(nexg_pcap* p, uint8_t* data, uint64_t data_cap, uint64_
 int nexg_pcap_read_raw(nexg_pcap* p, uint8_t* buf, uint64_t cap, uint64_t* offsets,
                        uint32_t* lengths, uint64_t max_frames, uint64_t* ts_ns,
                        uint64_t* n_frames, uint64_t* bytes_used);
+/* Zero-copy shape: no read at all. nexg_pcap_map maps the file read-only
+ * (the page cache itself; *data, *size = file bytes, *first = offset of the
+ * first record or block). nexg_pcap_walk_mapped describes the records in the
+ * window [from, from + max_bytes) of the mapping: offsets[k] (relative to
+ * `from`) / lengths[k], *next = the offset after the last complete record
+ * (the next call's `from`). The caller registers the mapping for DMA
+ * (hipHostRegister) and copies [from, *next) to the GPU as is: the same
+ * in-place layout as read_raw (record headers between frames, monotone), at
+ * PCIe rate with no host copy. End of file when *next == size. Classic pcap
+ * uses nexg_pcap_set_read_threads for the parallel walk. Use one shape per
+ * reader: the mapped walk does not move the file position. */
+int nexg_pcap_map(nexg_pcap* p, const uint8_t** data, uint64_t* size, uint64_t* first);
+int nexg_pcap_walk_mapped(nexg_pcap* p, uint64_t from, uint64_t max_bytes, uint64_t* offsets,
+                          uint32_t* lengths, uint64_t max_frames, uint64_t* ts_ns, uint64_t* n_frames,
+                          uint64_t* next);
 /* read_raw's file reads split over up to `threads` (1..64) parallel preads
  * of >= 4-MiB pieces (default 1), and for classic pcap the record walk of a
- * read of >= 8 MiB split over as many threads (speculative chunk starts,
- * stitched; a disagreement re-walks that chunk). Results are identical for
- * any count.
+ * read (or mapped window) of >= 8 MiB split over as many threads, eight
+ * interleaved chunks each (speculative chunk starts, stitched; a
+ * disagreement re-walks that chunk). Results are identical for any count.
  * (read_batch stays single-threaded: parallel record copies into pinned
  * staging measured 2.5-4x slower on the GPU boxes, profiles/r01_ingest/threads.) */
 int nexg_pcap_set_read_threads(nexg_pcap* p, uint32_t threads);

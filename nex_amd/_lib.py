@@ -55,6 +55,8 @@ def load():
         "nexg_pcap_last_error": (ctypes.c_char_p, [P]),
         "nexg_pcap_read_batch": (I, [P, P, U64, P, U64, P, ctypes.POINTER(U64)]),
         "nexg_pcap_read_raw": (I, [P, P, U64, P, P, U64, P, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+        "nexg_pcap_map": (I, [P, ctypes.POINTER(P), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+        "nexg_pcap_walk_mapped": (I, [P, U64, U64, P, P, U64, P, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "nexg_pcap_set_read_threads": (I, [P, U32]),
         "nexg_pcap_close": (I, [P]),
         "nexg_rx_config_default": (None, [P]),

@@ -291,5 +291,5 @@ EXPORTED_SYMBOLS = (
     "nexg_tpacket3_walk", "nexg_tx_open", "nexg_tx_send_batch", "nexg_tx_close",
     "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_build_tcp_batch",
     "nexg_build_icmp_echo_batch", "nexg_pcap_open", "nexg_pcap_linktype", "nexg_pcap_last_error",
-    "nexg_pcap_read_batch", "nexg_pcap_read_raw", "nexg_pcap_set_read_threads", "nexg_pcap_close", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
+    "nexg_pcap_read_batch", "nexg_pcap_read_raw", "nexg_pcap_map", "nexg_pcap_walk_mapped", "nexg_pcap_set_read_threads", "nexg_pcap_close", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
 )

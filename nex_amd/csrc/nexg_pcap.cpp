@@ -15,11 +15,17 @@
 //                          (pinned) buffer with one read; frames are described
 //                          in place by offsets + lengths, so the host touches
 //                          each byte once and the GPU skips the record headers.
-// Both walk records in memory (scan_one); the file is read in large chunks.
+//   nexg_pcap_map + nexg_pcap_walk_mapped : no read at all; the file is
+//                          mapped (page cache) and walked in place, the caller
+//                          registers the mapping for DMA and copies record
+//                          regions straight to the GPU.
+// All walk records in memory (scan_one); the file is read in large chunks.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <sys/types.h>
 #include <unistd.h>
 
@@ -78,6 +84,8 @@ struct nexg_pcap {
     std::vector<uint8_t> carry;  // read_raw: bytes of an incomplete record
     bool file_eof = false;
     uint32_t threads = 1;  // read_raw: parallel pread pieces per chunk
+    const uint8_t* map = nullptr;  // nexg_pcap_map: the file mapped read-only
+    size_t map_size = 0;
     int fatal = 0;  // sticky error of a malformed / truncated file
     char err[160] = {0};
 };
@@ -280,16 +288,59 @@ void walk_classic(const nexg_pcap* p, const uint8_t* buf, size_t have, size_t fr
     w.end = pos;
 }
 
+// The walk is a dependent chain of header loads (each record's length gives
+// the next header's address), so one chain per thread is memory-latency
+// bound; each thread walks kChains chunks interleaved, one header of each per
+// step, to keep that many cache misses in flight.
+constexpr size_t kChains = 8;
+
+void walk_interleaved(const nexg_pcap* p, const uint8_t* buf, size_t have, const size_t* from, const size_t* stop,
+                      bool want_ts, WalkPart* w, size_t m) {
+    size_t pos[kChains];
+    bool live[kChains];
+    size_t active = 0;
+    for (size_t j = 0; j < m; j++) {
+        pos[j] = from[j];
+        w[j].begin = from[j];
+        live[j] = pos[j] < stop[j];
+        active += live[j];
+    }
+    while (active) {
+        for (size_t j = 0; j < m; j++) {
+            if (!live[j]) continue;
+            const size_t q = pos[j];
+            bool go = q < stop[j] && have - q >= 16;
+            uint32_t caplen = 0;
+            if (go) {
+                caplen = rd32(p, buf + q + 8);
+                if (caplen > (1u << 26)) { w[j].bad = true; go = false; }
+                else if (have - q < 16 + (size_t)caplen) go = false;
+            }
+            if (!go) {
+                live[j] = false;
+                active--;
+                w[j].end = q;
+                continue;
+            }
+            w[j].offs.push_back(q + 16);
+            w[j].lens.push_back(caplen);
+            if (want_ts)
+                w[j].ts.push_back((uint64_t)rd32(p, buf + q) * 1000000000ull +
+                                  (uint64_t)rd32(p, buf + q + 4) * (p->nsec ? 1u : 1000u));
+            pos[j] = q + 16 + caplen;
+        }
+    }
+}
+
 int64_t parallel_walk(nexg_pcap* p, const uint8_t* buf, size_t have, uint64_t max_frames, uint64_t* offsets,
                       uint32_t* lengths, uint64_t* ts_ns, size_t* end) {
-    const size_t T = p->threads;
+    const size_t T = p->threads * kChains;  // chunks: kChains per thread
     const size_t per = (have + T - 1) / T;
     std::vector<WalkPart> parts(T);
-    auto work = [&](size_t k) {
+    auto start_of = [&](size_t k) {  // chunk k's first plausible header that chains 4 deep (or to the end)
         const size_t a = k * per, b = a + per < have ? a + per : have;
-        if (a >= have) { parts[k].begin = parts[k].end = have; return; }
         size_t s = a;
-        if (k > 0) {  // first plausible header that chains 4 deep (or to the buffer end)
+        if (k > 0) {
             for (; s < b; s++) {
                 size_t q = s;
                 int depth = 0;
@@ -301,10 +352,23 @@ int64_t parallel_walk(nexg_pcap* p, const uint8_t* buf, size_t have, uint64_t ma
                 if (depth == 4 || (depth > 0 && q >= have)) break;
             }
         }
-        walk_classic(p, buf, have, s, b, ts_ns != nullptr, parts[k]);
+        return s;
+    };
+    auto work = [&](size_t t) {
+        size_t from[kChains], stop[kChains];
+        for (size_t j = 0; j < kChains; j++) {
+            const size_t k = t * kChains + j, a = k * per;
+            if (a >= have) {
+                from[j] = stop[j] = have;
+                continue;
+            }
+            stop[j] = a + per < have ? a + per : have;
+            from[j] = start_of(k);
+        }
+        walk_interleaved(p, buf, have, from, stop, ts_ns != nullptr, &parts[t * kChains], kChains);
     };
     std::vector<std::thread> pool;
-    for (size_t k = 1; k < T; k++) pool.emplace_back(work, k);
+    for (size_t t = 1; t < p->threads; t++) pool.emplace_back(work, t);
     work(0);
     for (auto& t : pool) t.join();
     // stitch; re-walk a chunk whose start disagrees with the previous end
@@ -329,13 +393,56 @@ int64_t parallel_walk(nexg_pcap* p, const uint8_t* buf, size_t have, uint64_t ma
         memcpy(lengths + first[k], parts[k].lens.data(), m * 4);
         if (ts_ns) memcpy(ts_ns + first[k], parts[k].ts.data(), m * 8);
     };
+    auto copy_chunks = [&](size_t t) {
+        for (size_t j = 0; j < kChains; j++) copy(t * kChains + j);
+    };
     pool.clear();
-    for (size_t k = 1; k < T; k++) pool.emplace_back(copy, k);
-    copy(0);
+    for (size_t t = 1; t < p->threads; t++) pool.emplace_back(copy_chunks, t);
+    copy_chunks(0);
     for (auto& t : pool) t.join();
     *end = n < first[T] ? (size_t)(offsets[n - 1] + lengths[n - 1]) : parts[T - 1].end;
     if (n == 0) *end = 0;
     return (int64_t)n;
+}
+
+// Records of buf[0, have): the parallel classic walk when it applies, else
+// scan_one in sequence; offsets / lengths into buf, *pos = bytes described.
+// Returns 0, or the error of a malformed record met before any frame.
+int walk_records(nexg_pcap* p, const uint8_t* buf, size_t have, uint64_t max_frames, uint64_t* offsets,
+                 uint32_t* lengths, uint64_t* ts_ns, uint64_t* n_out, size_t* pos_out) {
+    uint64_t n = 0;
+    size_t pos = 0;
+    bool walked = false;
+    if (!p->ng && have >= (8u << 20)) {  // classic pcap: chunked walk (kChains per thread, threads in parallel)
+        size_t end = 0;
+        const int64_t got = parallel_walk(p, buf, have, max_frames, offsets, lengths, ts_ns, &end);
+        if (got >= 0) {
+            n = (uint64_t)got;
+            pos = end;
+            walked = true;
+        }  // else: a malformed record; the sequential walk below reports it
+    }
+    while (!walked && n < max_frames) {
+        size_t used = 0;
+        Rec r;
+        const int rc = scan_one(p, buf + pos, have - pos, &used, &r);
+        if (rc == 0) break;
+        if (rc < 0) {
+            p->fatal = rc;
+            if (n) break;
+            return rc;
+        }
+        if (rc == 1) {  // > 65535 B passes through (NEXG_ERR_BAD_EXTENT in the parse)
+            offsets[n] = pos + r.data;
+            lengths[n] = r.caplen;
+            if (ts_ns) ts_ns[n] = r.ts_ns;
+            n++;
+        }
+        pos += used;
+    }
+    *n_out = n;
+    *pos_out = pos;
+    return 0;
 }
 
 }  // namespace
@@ -476,34 +583,8 @@ int nexg_pcap_read_raw(nexg_pcap* p, uint8_t* buf, uint64_t cap, uint64_t* offse
     }
     uint64_t n = 0;
     size_t pos = 0;
-    bool walked = false;
-    if (!p->ng && p->threads > 1 && have >= (8u << 20)) {  // classic pcap: the record walk in parallel
-        size_t end = 0;
-        const int64_t got = parallel_walk(p, buf, have, max_frames, offsets, lengths, ts_ns, &end);
-        if (got >= 0) {
-            n = (uint64_t)got;
-            pos = end;
-            walked = true;
-        }  // else: a malformed record; the sequential walk below reports it
-    }
-    while (!walked && n < max_frames) {
-        size_t used = 0;
-        Rec r;
-        const int rc = scan_one(p, buf + pos, have - pos, &used, &r);
-        if (rc == 0) break;
-        if (rc < 0) {
-            p->fatal = rc;
-            if (n) break;
-            return rc;
-        }
-        if (rc == 1) {  // > 65535 B passes through (NEXG_ERR_BAD_EXTENT in the parse)
-            offsets[n] = pos + r.data;
-            lengths[n] = r.caplen;
-            if (ts_ns) ts_ns[n] = r.ts_ns;
-            n++;
-        }
-        pos += used;
-    }
+    const int wrc = walk_records(p, buf, have, max_frames, offsets, lengths, ts_ns, &n, &pos);
+    if (wrc) return wrc;
     if (pos < have) {  // an incomplete record, or records past max_frames: next call
         if (n == 0 && pos == 0 && p->file_eof && p->carry.empty() && have < cap)
             return p->fatal = set_err(p, NEXG_EINVAL, "truncated capture file");
@@ -517,6 +598,52 @@ int nexg_pcap_read_raw(nexg_pcap* p, uint8_t* buf, uint64_t cap, uint64_t* offse
     return NEXG_OK;
 }
 
+int nexg_pcap_map(nexg_pcap* p, const uint8_t** data, uint64_t* size, uint64_t* first) {
+    if (!p || !data || !size || !first) return NEXG_EINVAL;
+    if (!p->map) {
+        struct stat st;
+        const int fd = fileno(p->f);
+        if (fstat(fd, &st) != 0) return set_err(p, NEXG_EINVAL, "fstat failed");
+        if (st.st_size > 0) {
+            // MAP_POPULATE: page tables filled at map time (the record walk
+            // and the DMA registration then take no per-page faults)
+            void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, 0);
+            if (m == MAP_FAILED) return set_err(p, NEXG_ENOMEM, "mmap failed");
+            p->map = static_cast<const uint8_t*>(m);
+        }
+        p->map_size = (size_t)st.st_size;
+    }
+    *data = p->map;
+    *size = p->map_size;
+    *first = p->ng ? 0u : 24u;  // pcapng: the blocks from the section header on
+    return NEXG_OK;
+}
+
+int nexg_pcap_walk_mapped(nexg_pcap* p, uint64_t from, uint64_t max_bytes, uint64_t* offsets,
+                          uint32_t* lengths, uint64_t max_frames, uint64_t* ts_ns, uint64_t* n_frames,
+                          uint64_t* next) {
+    if (!p || !n_frames || !next || !max_frames || !offsets || !lengths) return NEXG_EINVAL;
+    *n_frames = 0;
+    *next = from;
+    if (!p->map && p->map_size == 0) return set_err(p, NEXG_EINVAL, "walk_mapped before nexg_pcap_map");
+    if (from > p->map_size) return set_err(p, NEXG_EINVAL, "offset past the end of the file");
+    if (p->fatal) return p->fatal;
+    const size_t left = p->map_size - (size_t)from;
+    const size_t have = max_bytes < left ? (size_t)max_bytes : left;
+    if (have == 0) return NEXG_OK;  // end of file
+    uint64_t n = 0;
+    size_t pos = 0;
+    const int rc = walk_records(p, p->map + from, have, max_frames, offsets, lengths, ts_ns, &n, &pos);
+    if (rc) return rc;
+    if (n == 0 && pos == 0) {  // not even one record in the window
+        if (have == left) return p->fatal = set_err(p, NEXG_EINVAL, "truncated capture file");
+        return set_err(p, NEXG_ERANGE, "max_bytes smaller than one record");
+    }
+    *n_frames = n;
+    *next = from + pos;
+    return NEXG_OK;
+}
+
 int nexg_pcap_set_read_threads(nexg_pcap* p, uint32_t threads) {
     if (!p || threads == 0 || threads > 64) return NEXG_EINVAL;
     p->threads = threads;
@@ -525,6 +652,7 @@ int nexg_pcap_set_read_threads(nexg_pcap* p, uint32_t threads) {
 
 int nexg_pcap_close(nexg_pcap* p) {
     if (!p) return NEXG_EINVAL;
+    if (p->map) munmap(const_cast<uint8_t*>(p->map), p->map_size);
     if (p->f) fclose(p->f);
     delete p;
     return NEXG_OK;

@@ -82,8 +82,36 @@ class PcapReader:
             for a, b in zip(offs[:-1], offs[1:]):
                 yield bytes(data[int(a):int(b)])
 
+    def map(self) -> Tuple[np.ndarray, int]:
+        """Zero-copy shape (nexg_pcap_map): (read-only uint8 array over the
+        file's page-cache mapping, offset of the first record). The array is
+        valid until close()."""
+        data, size, first = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self.lib.nexg_pcap_map(self.h, ctypes.byref(data), ctypes.byref(size), ctypes.byref(first))
+        if rc != abi.OK:
+            raise PcapError(self.lib.nexg_pcap_last_error(self.h).decode() or f"status {rc}")
+        if size.value == 0:
+            return np.zeros(0, np.uint8), first.value
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * size.value).from_address(data.value))
+        arr.flags.writeable = False  # PROT_READ
+        return arr, first.value
+
+    def walk_mapped(self, start: int, max_bytes: int, offsets: np.ndarray, lengths: np.ndarray,
+                    ts_ns: Optional[np.ndarray] = None) -> Tuple[int, int]:
+        """Records in the mapping window [start, start + max_bytes)
+        (nexg_pcap_walk_mapped): (frames, next start); offsets relative to
+        start."""
+        n, nxt = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self.lib.nexg_pcap_walk_mapped(
+            self.h, start, max_bytes, offsets.ctypes.data, lengths.ctypes.data, len(offsets),
+            None if ts_ns is None else ts_ns.ctypes.data, ctypes.byref(n), ctypes.byref(nxt))
+        if rc != abi.OK:
+            raise PcapError(self.lib.nexg_pcap_last_error(self.h).decode() or f"status {rc}")
+        return n.value, nxt.value
+
     def set_read_threads(self, threads: int):
-        """Split read_raw's file reads over `threads` parallel preads."""
+        """Split read_raw's file reads over `threads` parallel preads (and the
+        classic-pcap record walk of read_raw / walk_mapped over as many threads)."""
         rc = self.lib.nexg_pcap_set_read_threads(self.h, threads)
         if rc != abi.OK:
             raise PcapError(f"invalid thread count {threads}")
@@ -167,3 +195,75 @@ def device_raw_batches(reader: PcapReader, max_frames: int = 1 << 20, cap: int =
             ln = lens[:max(n, 1)].to(device, non_blocking=True)
         s.synchronize()  # the pinned staging buffers are reused by the next read
         yield FrameBatch(data=d[:used], count=n, offsets=o[:n], lengths=ln[:n], hints=abi.FRAMES_MONOTONE)
+
+
+def mapped_frames(reader: PcapReader, window: int = 1 << 22, max_frames: int = 1 << 14) -> Iterator[bytes]:
+    """All frames via the zero-copy shape (test / inspection helper)."""
+    arr, pos = reader.map()
+    offs = np.empty(max_frames, np.uint64)
+    lens = np.empty(max_frames, np.uint32)
+    while pos < len(arr):
+        n, nxt = reader.walk_mapped(pos, window, offs, lens)
+        for k in range(n):
+            a = pos + int(offs[k])
+            yield bytes(arr[a:a + int(lens[k])])
+        pos = nxt
+
+
+def device_mapped_batches(reader: PcapReader, max_frames: int = 1 << 20, window: int = 1 << 28,
+                          device="cuda", stream=None):
+    """Yield FrameBatch objects in the zero-copy shape (nexg_pcap_map /
+    nexg_pcap_walk_mapped): the file's page-cache mapping is registered for
+    DMA (hipHostRegister, one window-sized chunk at a time as the walk
+    reaches it) and each window of complete records goes H2D as is,
+    record headers in place, described by offsets + lengths with
+    NEXG_FRAMES_MONOTONE — no host copy of the frame bytes, so the rate is
+    the PCIe rate. Parse each batch on `stream` before asking for the next
+    (the device window and the offset staging are reused)."""
+    import torch
+    from .engine import FrameBatch
+    arr, pos = reader.map()
+    size = len(arr)
+    if pos >= size:
+        return
+    hip = ctypes.CDLL("libamdhip64.so")  # torch's HIP runtime (already loaded)
+    base = arr.ctypes.data
+    chunk = window  # registered for DMA chunk by chunk as the walk reaches it
+    registered = []
+
+    def register_upto(end):
+        for c in range(len(registered), (min(end, size) + chunk - 1) // chunk):
+            a, b = c * chunk, min(size, (c + 1) * chunk)
+            if hip.hipHostRegister(ctypes.c_void_p(base + a), ctypes.c_size_t(b - a), ctypes.c_uint(0)) != 0:
+                raise PcapError("hipHostRegister of the capture mapping failed")
+            registered.append(c)
+    s = stream or torch.cuda.current_stream()
+    try:
+        buf = torch.empty(window, dtype=torch.uint8, device=device)
+        offs = torch.empty(max_frames, dtype=torch.int64, pin_memory=True)
+        lens = torch.empty(max_frames, dtype=torch.int32, pin_memory=True)
+        onp, lnp = offs.numpy().view(np.uint64), lens.numpy().view(np.uint32)
+        while pos < size:
+            s.synchronize()  # the previous batch's copies and parse are done with the staging
+            register_upto(pos + window)
+            n, nxt = reader.walk_mapped(pos, window, onp, lnp)
+            if n == 0:  # pcapng blocks without packets
+                pos = nxt
+                continue
+            nbytes = nxt - pos
+            a = pos
+            while a < nxt:  # one copy per registered chunk the window touches
+                b = min(nxt, (a // chunk + 1) * chunk)
+                if hip.hipMemcpyAsync(ctypes.c_void_p(buf.data_ptr() + a - pos), ctypes.c_void_p(base + a),
+                                      ctypes.c_size_t(b - a), ctypes.c_int(1), ctypes.c_void_p(s.cuda_stream)) != 0:
+                    raise PcapError("H2D copy from the capture mapping failed")
+                a = b
+            with torch.cuda.stream(s):
+                o = offs[:n].to(device, non_blocking=True)
+                ln = lens[:n].to(device, non_blocking=True)
+            yield FrameBatch(data=buf[:nbytes], count=n, offsets=o, lengths=ln, hints=abi.FRAMES_MONOTONE)
+            pos = nxt
+    finally:
+        s.synchronize()
+        for c in registered:
+            hip.hipHostUnregister(ctypes.c_void_p(base + c * chunk))

@@ -265,6 +265,31 @@ def test_pcap_ingest_to_gpu_parse(engine, oracle, tmp_path):
     helpers.records_equal(got, oracle.parse_frames(frames), frames, "pcap ingest")
 
 
+@pytest.mark.parametrize("fmt", ["classic", "pcapng"])
+def test_pcap_mapped_ingest_to_gpu_parse(engine, oracle, tmp_path, fmt):
+    """Zero-copy capture ingest (nexg_pcap_map: the page-cache mapping
+    registered for DMA, windows of records copied H2D in place, offsets +
+    lengths + monotone hint) -> span parse == the oracle, with windows that
+    cut records (several batches)."""
+    from nex_amd.ingest import PcapReader, device_mapped_batches
+    from tests import pcapfile
+    frames = [oracle.gen_frame(abi.WL_IMIX, i) for i in range(3000)] + helpers.crafted_frames()[1:]
+    path = tmp_path / ("x.pcap" if fmt == "classic" else "x.pcapng")
+    if fmt == "classic":
+        path.write_bytes(pcapfile.classic(frames))
+    else:
+        blob = pcapfile.ng_shb() + pcapfile.ng_idb(1)
+        path.write_bytes(blob + b"".join(pcapfile.ng_epb(f, i) for i, f in enumerate(frames)))
+    got, batches = [], 0
+    with PcapReader(str(path)) as r:
+        for b in device_mapped_batches(r, max_frames=700, window=1 << 18):
+            got.append(engine.parse_to_numpy(b, out_kind=abi.OUT_RECORD))
+            batches += 1
+    got = np.concatenate(got)
+    assert batches > 3
+    helpers.records_equal(got, oracle.parse_frames(frames), frames, f"mapped ingest {fmt}")
+
+
 @pytest.mark.parametrize("flags", [abi.PARSE_VLAN, abi.PARSE_VLAN | abi.PARSE_STRICT])
 def test_vlan_extension_on_gpu(engine, oracle, corpus, flags):
     """NEXG_PARSE_VLAN in every kernel variant == the oracle's extension."""

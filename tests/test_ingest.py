@@ -290,3 +290,61 @@ def test_raw_parallel_walk_against_lookalike_headers(tmp_path, threads):
                 r.set_read_threads(threads)
                 got = list(raw_frames(r, cap=cap, max_frames=maxf))
             assert got == want, (big_endian, cap, maxf)
+
+
+@pytest.mark.parametrize("window", [1 << 22, 20000, 9100])
+def test_mapped_shape_matches_packed(tmp_path, frames, window):
+    """nexg_pcap_map + nexg_pcap_walk_mapped (zero-copy shape) describe the
+    same frames as the packed reader, for classic pcap in both byte orders /
+    resolutions and pcapng, at window sizes that cut records."""
+    from nex_amd.ingest import mapped_frames
+    files, fr = _all_variants(tmp_path, frames)
+    for name, blob in files.items():
+        path = _write(tmp_path, name, blob)
+        with PcapReader(path) as r:
+            packed = list(r.frames())
+        with PcapReader(path) as r:
+            got = list(mapped_frames(r, window=window, max_frames=13))
+        assert got == packed, name
+
+
+def test_mapped_shape_errors_and_layout(tmp_path, frames):
+    """Records are described in place (offsets relative to the window start,
+    16-B classic record headers between them, monotone); a truncated file
+    raises after its complete records; a window smaller than a record raises
+    ERANGE; an empty capture maps to nothing."""
+    from nex_amd.ingest import mapped_frames
+    path = _write(tmp_path, "m.pcap", pcapfile.classic(frames[:20]))
+    with PcapReader(path) as r:
+        arr, first = r.map()
+        assert first == 24 and len(arr) == os.path.getsize(path)
+        offs, lens = np.empty(64, np.uint64), np.empty(64, np.uint32)
+        n, nxt = r.walk_mapped(first, 1 << 20, offs, lens)
+        assert n == 20 and nxt == len(arr)
+        assert int(offs[0]) == 16 and (np.diff(offs[:n].astype(np.int64)) == lens[:n - 1].astype(np.int64) + 16).all()
+    path = _write(tmp_path, "mt.pcap", pcapfile.classic(frames[:10])[:-3])
+    with PcapReader(path) as r:
+        got = []
+        with pytest.raises(PcapError):
+            for f in mapped_frames(r, window=1 << 20):
+                got.append(f)
+        assert got == frames[:9]
+    path = _write(tmp_path, "mb.pcap", pcapfile.classic(frames[-1:]))  # a 9000-B record
+    with PcapReader(path) as r, pytest.raises(PcapError):
+        list(mapped_frames(r, window=4096))
+    path = _write(tmp_path, "me.pcap", pcapfile.classic([]))
+    with PcapReader(path) as r:
+        assert list(mapped_frames(r)) == []
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_mapped_parallel_walk(tmp_path, threads):
+    """The mapped walk uses the parallel classic walk for windows >= 8 MiB and
+    gives the sequential result for any thread count."""
+    from nex_amd.ingest import mapped_frames
+    rng = np.random.default_rng(9)
+    fr = [bytes(rng.integers(0, 256, int(rng.integers(14, 1600)), dtype=np.uint8)) for _ in range(12000)]
+    path = _write(tmp_path, "p.pcap", pcapfile.classic(fr))
+    with PcapReader(path) as r:
+        r.set_read_threads(threads)
+        assert list(mapped_frames(r, window=9 << 20, max_frames=1 << 15)) == fr

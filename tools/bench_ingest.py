@@ -53,9 +53,11 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 18, help="frames per staged batch")
     ap.add_argument("--workload", choices=["imix", "udp64"], default="imix")
     ap.add_argument("--reps", type=int, default=2)
-    ap.add_argument("--shape", choices=["raw", "packed"], default="packed",
+    ap.add_argument("--shape", choices=["raw", "packed", "mapped"], default="packed",
                     help="raw: file bytes read straight into pinned staging, frames in place "
-                         "(offsets + lengths); packed: records copied back to back (offsets only)")
+                         "(offsets + lengths); packed: records copied back to back (offsets only); "
+                         "mapped: no read, the page-cache mapping registered for DMA and copied "
+                         "H2D in place (nexg_pcap_map / nexg_pcap_walk_mapped)")
     ap.add_argument("--threads", type=int, default=1,
                     help="raw shape: parallel preads per file chunk (nexg_pcap_set_read_threads)")
     args = ap.parse_args()
@@ -86,8 +88,8 @@ def main():
     B = args.batch
     # packed: room for B full-size frames; raw: a file chunk per batch, with
     # enough offset slots that the frame limit never cuts a chunk short
-    cap = B * 1518 + 4096 if args.shape == "packed" else 64 << 20
-    if args.shape == "raw":
+    cap = B * 1518 + 4096 if args.shape == "packed" else (256 << 20 if args.shape == "mapped" else 64 << 20)
+    if args.shape in ("raw", "mapped"):
         B = cap // 32
     nbuf = 2
     host = [torch.empty(cap, dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)]
@@ -102,11 +104,31 @@ def main():
 
     stats = {"read_s": 0.0}
 
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")  # torch's HIP runtime
+
     def run_once():
         stats["read_s"] = 0.0
         r = PcapReader(path)
         if args.threads > 1:
             r.set_read_threads(args.threads)
+        win = [(0, 0)] * nbuf  # mapped shape: the file window of each slot
+        mpos = [0]
+        R = 256 << 20  # the mapping is registered for DMA in chunks of R, as the walk reaches them
+        registered = set()
+        stats["register_s"] = 0.0
+        if args.shape == "mapped":
+            arr, mpos[0] = r.map()
+            base, size = arr.ctypes.data, len(arr)
+
+        def register_upto(end):  # reader thread: chunks covering [.., end) registered (counted)
+            t_r = time.perf_counter()
+            for c in range(0, (min(end, size) + R - 1) // R):
+                if c not in registered:
+                    a, b = c * R, min(size, (c + 1) * R)
+                    assert hip.hipHostRegister(ctypes.c_void_p(base + a), ctypes.c_size_t(b - a), ctypes.c_uint(0)) == 0
+                    registered.add(c)
+            stats["register_s"] += time.perf_counter() - t_r
         free = [threading.Semaphore(1) for _ in range(nbuf)]  # staging slot reusable
         ready = [threading.Semaphore(0) for _ in range(nbuf)]
         counts = [0] * nbuf
@@ -117,7 +139,17 @@ def main():
             while True:
                 free[k].acquire()
                 t_r = time.perf_counter()
-                if args.shape == "raw":
+                if args.shape == "mapped":  # record walk of the next window (headers only)
+                    n = 0
+                    while mpos[0] < size:
+                        register_upto(mpos[0] + cap)
+                        n, nxt = r.walk_mapped(mpos[0], cap, hoff[k].numpy()[:B].view(np.uint64),
+                                               hlen[k].numpy().view(np.uint32))
+                        win[k] = (mpos[0], nxt)
+                        mpos[0] = nxt
+                        if n:
+                            break
+                elif args.shape == "raw":
                     while True:  # (0, >0): only non-packet blocks consumed, read on
                         n, used = r.read_raw_into(host[k].numpy(), hoff[k].numpy()[:B].view(np.uint64),
                                                   hlen[k].numpy().view(np.uint32))
@@ -141,20 +173,30 @@ def main():
             n = counts[k]
             if n == 0:
                 break
-            nb = int(hoff[k][B]) if args.shape == "raw" else int(hoff[k][n])
+            nb = (int(hoff[k][B]) if args.shape == "raw" else
+                  win[k][1] - win[k][0] if args.shape == "mapped" else int(hoff[k][n]))
             if parsed[k] is not None:
                 copy_s.wait_event(parsed[k])  # device slot k still read by an earlier parse
             with torch.cuda.stream(copy_s):
-                dev[k][:nb].copy_(host[k][:nb], non_blocking=True)
+                if args.shape == "mapped":  # straight from the registered page cache,
+                    a = win[k][0]           # one copy per registered chunk the window touches
+                    while a < win[k][1]:
+                        b = min(win[k][1], (a // R + 1) * R)
+                        assert hip.hipMemcpyAsync(ctypes.c_void_p(dev[k].data_ptr() + a - win[k][0]),
+                                                  ctypes.c_void_p(base + a), ctypes.c_size_t(b - a), ctypes.c_int(1),
+                                                  ctypes.c_void_p(copy_s.cuda_stream)) == 0
+                        a = b
+                else:
+                    dev[k][:nb].copy_(host[k][:nb], non_blocking=True)
                 doff[k][: n + 1].copy_(hoff[k][: n + 1], non_blocking=True)
-                if args.shape == "raw":
+                if args.shape in ("raw", "mapped"):
                     dlen[k][:n].copy_(hlen[k][:n], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(copy_s)
             ev.synchronize()  # staging slot k may be refilled once its bytes left
             free[k].release()
             comp_s.wait_event(ev)
-            if args.shape == "raw":
+            if args.shape in ("raw", "mapped"):
                 # records in file order with their headers in place: one ordered span per
                 # group (NEXG_FRAMES_MONOTONE routes to the span kernel, gaps read through)
                 fb = FrameBatch(data=dev[k][:nb], count=n, offsets=doff[k][:n], lengths=dlen[k][:n],
@@ -171,6 +213,10 @@ def main():
             k = (k + 1) % nbuf
         th.join()
         comp_s.synchronize()
+        if args.shape == "mapped":
+            for c in registered:
+                hip.hipHostUnregister(ctypes.c_void_p(base + c * R))
+            del arr
         r.close()
         return frames
 
@@ -192,8 +238,9 @@ def main():
         "gib_s": round(total_bytes / best / 2**30, 3), "frames": args.frames, "bytes": total_bytes,
         "workload": args.workload, "batch_frames": B, "shape": args.shape, "seconds": round(best, 4),
         "frames_ok": ok, "pcap_write_s": round(wr, 2), "reader_busy_s": round(stats["read_s"], 4),
-        "read_threads": args.threads,
-        "note": "one reader thread (file read from the page cache + copy into pinned staging; "
+        "read_threads": args.threads, "register_s": round(stats.get("register_s", 0.0), 4),
+        "note": "mapped shape: hipHostRegister of the page-cache mapping (counted), host record "
+                "walk per 64-MiB window, H2D straight from the mapping; other shapes: one reader thread (file read from the page cache + copy into pinned staging; "
                 "raw shape: split over read_threads parallel preads), "
                 "H2D / parse / D2H on two streams, reader one batch ahead"}))
 
