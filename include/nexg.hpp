@@ -948,6 +948,37 @@ class PcapReader {  // classic pcap / pcapng, a batch of records per call
         return frames;
     }
 
+    // Zero-copy shape (nexg_pcap_map / nexg_pcap_walk_mapped): the file's
+    // page-cache mapping (valid while the reader lives) and the records of
+    // one window of it, described in place; register the mapping for DMA
+    // (hipHostRegister) and copy [from, next) to the device as is.
+    struct MappedWindow {
+        uint64_t from = 0, next = 0;     // file range of the complete records
+        std::vector<uint64_t> offsets;  // relative to from
+        std::vector<uint32_t> lengths;
+    };
+    const uint8_t* map(uint64_t* size, uint64_t* first) {
+        const uint8_t* d = nullptr;
+        if (nexg_pcap_map(p_, &d, size, first) != NEXG_OK)
+            throw Error(std::string("capture map failed: ") + nexg_pcap_last_error(p_));
+        return d;
+    }
+    // records of [pos, pos + max_bytes); pos advances past them (end of file: pos == size)
+    MappedWindow walk_mapped(uint64_t& pos, uint64_t max_bytes, uint64_t max_frames) {
+        MappedWindow w;
+        w.from = pos;
+        w.offsets.resize(max_frames);
+        w.lengths.resize(max_frames);
+        uint64_t n = 0;
+        if (nexg_pcap_walk_mapped(p_, pos, max_bytes, w.offsets.data(), w.lengths.data(), max_frames, nullptr, &n,
+                                  &w.next) != NEXG_OK)
+            throw Error(std::string("capture walk failed: ") + nexg_pcap_last_error(p_));
+        w.offsets.resize(n);
+        w.lengths.resize(n);
+        pos = w.next;
+        return w;
+    }
+
    private:
     nexg_pcap* p_ = nullptr;
     std::vector<uint8_t> buf_;

@@ -12,6 +12,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <unistd.h>
+
 #include <fstream>
 #include <map>
 #include <memory>
@@ -376,6 +378,39 @@ int main(int argc, char** argv) {
         } catch (const Error& e) {
             printf("datalink checks skipped: %s\n", e.what());
         }
+    }
+    // PcapReader: the fixtures as a classic pcap file, read back packed and
+    // walked in place through the mapping (the zero-copy shape): same frames
+    {
+        char path[] = "/tmp/nexg_cpp_pcap_XXXXXX";
+        const int fd = mkstemp(path);
+        FILE* f = fdopen(fd, "wb");
+        const uint32_t gh[6] = {0xA1B2C3D4u, 0x00040002u, 0, 0, 65535, 1};
+        fwrite(gh, 4, 6, f);
+        for (size_t i = 0; i < frames.size(); i++) {
+            const uint32_t rh[4] = {(uint32_t)i, 0, (uint32_t)frames[i].size(), (uint32_t)frames[i].size()};
+            fwrite(rh, 4, 4, f);
+            fwrite(frames[i].data(), 1, frames[i].size(), f);
+        }
+        fclose(f);
+        std::vector<std::vector<uint8_t>> packed, mapped;
+        {
+            PcapReader r(path);
+            for (auto b = r.next_batch(7); !b.empty(); b = r.next_batch(7)) packed.insert(packed.end(), b.begin(), b.end());
+        }
+        {
+            PcapReader r(path);
+            uint64_t size = 0, pos = 0;
+            const uint8_t* m = r.map(&size, &pos);
+            while (pos < size) {
+                const auto w = r.walk_mapped(pos, 4096, 5);
+                for (size_t k = 0; k < w.offsets.size(); k++)
+                    mapped.emplace_back(m + w.from + w.offsets[k], m + w.from + w.offsets[k] + w.lengths[k]);
+            }
+        }
+        unlink(path);
+        CHECK(packed == frames);
+        CHECK(mapped == frames);
     }
     // every fixture: Frame fields == the record the oracle writes (device == oracle in --gpu)
     for (const auto& n : names) {
