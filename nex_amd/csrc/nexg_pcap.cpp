@@ -605,10 +605,12 @@ int nexg_pcap_map(nexg_pcap* p, const uint8_t** data, uint64_t* size, uint64_t* 
         const int fd = fileno(p->f);
         if (fstat(fd, &st) != 0) return set_err(p, NEXG_EINVAL, "fstat failed");
         if (st.st_size > 0) {
-            // MAP_POPULATE: page tables filled at map time (the record walk
-            // and the DMA registration then take no per-page faults)
-            void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, 0);
+            // no MAP_POPULATE: a capture may be far larger than host memory;
+            // pages come in as the walk (or the caller's DMA registration of
+            // a window) reaches them, read ahead sequentially
+            void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, fd, 0);
             if (m == MAP_FAILED) return set_err(p, NEXG_ENOMEM, "mmap failed");
+            madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
             p->map = static_cast<const uint8_t*>(m);
         }
         p->map_size = (size_t)st.st_size;
