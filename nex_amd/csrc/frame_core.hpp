@@ -635,8 +635,8 @@ NEXG_HD bool fast_udp4_64(const uint32_t (&w)[16], uint32_t opt_flags, nexg_reco
 // (frame.rs:570-658) is decided by those bytes plus one L4 tail sum, i.e. the
 // canonical IMIX shapes {IPv4 IHL 5, IPv6 without extension headers} x {TCP
 // data offset 5, UDP, ICMP/ICMPv6} and the common ways real traffic leaves
-// them: TCP timestamps (NOP, NOP, TS), other EtherTypes
-// (Ethernet only, Q3), an IP header that does not parse (non-strict:
+// them: TCP option lists of one TLV (NOP, NOP, timestamps / SACK; MSS),
+// other EtherTypes (Ethernet only, Q3), an IP header that does not parse (non-strict:
 // ip = Some(all None), Q4/Q12), other IP protocols and short
 // ICMP (no transport layer, Q9/Q15), a UDP length word that does not fit or a
 // TCP header that does not parse (transport layer only, Q14), and IP lengths
@@ -712,14 +712,19 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     const uint32_t doff = L(12) >> 12, ulen = L(4);
     const bool tfail = tcp && (n < 20u || doff < 5u || 4u * doff > n);  // no TcpPacket
     const bool q14 = udp && (n < 8u || ulen < 8u || ulen > n);          // no UdpPacket
-    // NOP, NOP, Timestamps (RFC 7323's layout: the option list of most TCP
-    // data segments): the option walk (tcp.rs:767-818) gives 3 options that
-    // re-serialise to the same 12 bytes and data offset (tcp.rs:521-575), so
-    // the checksum sums the raw bytes from l4 + 20 on like a payload; only
-    // the four layout bytes (l4 + 20..23, inside the window for both
-    // families) are read
+    // TCP option lists of one TLV, alone (MSS of a SYN-ACK: 02 04 ..) or
+    // behind NOP, NOP (timestamps, RFC 7323's layout for most data segments;
+    // SACK blocks), exactly filling the data offset: the option walk
+    // (tcp.rs:767-818) gives 1 / 3 options that re-serialise to the same
+    // bytes and data offset (tcp.rs:521-575), so the checksum sums the raw
+    // bytes from l4 + 20 on like a payload; only the four layout bytes
+    // (l4 + 20..23, inside the window for both families) are read
     const uint32_t o0 = v6 ? w[18] : w[13], o1 = v6 ? w[19] : w[14];
-    const bool tsopt = tcp && !tfail && doff == 8u && (o0 >> 16) == 0x0101u && (o1 & 0xFFFFu) == 0x0A08u;
+    const uint32_t b20 = (o0 >> 16) & 0xFFu, b21 = o0 >> 24, b22 = o1 & 0xFFu, b23 = (o1 >> 8) & 0xFFu;
+    const uint32_t olen = 4u * doff - 20u;  // used when doff > 5
+    const bool one = b20 >= 2u && b21 >= 2u && b21 == olen;
+    const bool nnx = b20 == 1u && b21 == 1u && b22 >= 2u && b23 >= 2u && 2u + b23 == olen;
+    const bool tsopt = tcp && !tfail && doff > 5u && (one || nnx);
     if ((tcp && !tfail && doff != 5u && !tsopt) || (udp && !q14 && ulen != n)) return false;
     const bool tonly = tfail || q14;                                  // transport layer, no packet
     const bool none = !(tcp || udp || icmp) || (icmp && n < 8u);      // no transport layer
@@ -812,14 +817,14 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     if (tcp) {
         r.tcp_seq = (L(4) << 16) | L(6);
         r.tcp_ack = (L(8) << 16) | L(10);
-        r.l4_length = tsopt ? 32u : 20u;
-        r.l4_nopt = tsopt ? 3u : 0u;
+        r.l4_length = (uint16_t)(4u * doff);
+        r.l4_nopt = tsopt ? (nnx ? 3u : 1u) : 0u;
         r.l4_type = (uint8_t)L(12);
         r.l4_code = (uint8_t)(L(12) >> 8);
         r.tcp_window = (uint16_t)L(14);
         r.tcp_urg = (uint16_t)L(18);
     }
-    const uint32_t hp = tsopt ? 32u : h;  // header bytes before the payload
+    const uint32_t hp = tsopt ? 4u * doff : h;  // header bytes before the payload
     r.payload_off = (uint16_t)(n > hp ? l4 + hp : 0u);
     r.payload_len = (uint16_t)(n - hp);
     return true;

@@ -322,6 +322,37 @@ def tcp_ts_frames(oracle, base, rng, fix_checksums=True):
     return out
 
 
+def tcp_option_frames(oracle, base, rng):
+    """TCP frames of `base` with one-TLV option lists the register path takes
+    (MSS alone; NOP NOP SACK with 1-4 blocks; NOP NOP any-kind TLV) and near
+    misses (a length one off, EOL / NOP inside, two TLVs), valid checksums."""
+    out = []
+    lists = [bytes([2, 4, 5, 180]),                                     # MSS (SYN-ACK)
+             *[bytes([1, 1, 5, 2 + 8 * k]) + bytes(rng.integers(0, 256, 8 * k, dtype=np.uint8)) for k in (1, 2, 3, 4)],
+             bytes([1, 1, 30, 6, 9, 9, 9, 9]),                          # unknown kind, NOP NOP form
+             bytes([3, 3, 7, 0]),                                       # WS + EOL pad (not one TLV)
+             bytes([1, 1, 5, 11]) + bytes(9),                           # SACK length one off
+             bytes([2, 4, 5, 180, 1, 3, 3, 7]),                         # two TLVs
+             bytes([1, 1, 1, 1])]                                       # NOPs only
+    for i, f in enumerate(base):
+        v4 = f[12:14] == b"\x08\x00"
+        l4 = 34 if v4 else 54
+        if len(f) < l4 + 20 or f[23 if v4 else 20] != 6:
+            continue
+        opts = lists[i % len(lists)]
+        opts = opts + bytes((-len(opts)) % 4)
+        g = bytearray(f[:l4 + 20] + opts + f[l4 + 20:])
+        g[l4 + 12] = ((5 + len(opts) // 4) << 4) | (g[l4 + 12] & 0x0F)
+        k = 16 if v4 else 18
+        g[k:k + 2] = (int.from_bytes(g[k:k + 2], "big") + len(opts)).to_bytes(2, "big")
+        r = oracle.parse_frame(bytes(g))
+        if v4:
+            g[24:26] = int(r["ip_csum_calc"]).to_bytes(2, "big")
+        g[l4 + 16:l4 + 18] = int(r["l4_csum_calc"]).to_bytes(2, "big")
+        out.append(bytes(g))
+    return out
+
+
 def vlan_frames():
     """VLAN-extension cases: single / double / QinQ tags over every inner type,
     truncated tags, three tags (only two unwrapped)."""
