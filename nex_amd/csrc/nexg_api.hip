@@ -18,10 +18,6 @@ struct nexg_ctx {
     char last_error[256];
     void* scratch;          // device memory for per-call hand-offs (TwoPass tail sums)
     uint64_t scratch_bytes;
-    void* items;            // deferred generic pass: work items (16 B per frame of the largest batch)
-    uint64_t items_bytes;
-    uint32_t* item_counters;  // two alternating item counters (zeroed at allocation)
-    uint32_t item_which;      // the counter the next launch appends to
 };
 
 namespace {
@@ -55,41 +51,6 @@ void* scratch(nexg_ctx* ctx, uint64_t bytes) {
     }
     ctx->scratch_bytes = want;
     return ctx->scratch;
-}
-
-// NEXG_SPAN_DEFER=1: packed batches with the sparse output hand their
-// declined frames to a second launch (k_span_items) instead of parsing them
-// inside the streaming kernel
-bool span_defer() {
-    static const bool on = [] {
-        const char* e = getenv("NEXG_SPAN_DEFER");
-        return e && strcmp(e, "1") == 0;
-    }();
-    return on;
-}
-
-// the deferred pass's item buffer (grown like scratch) and counters
-bool defer_buffers(nexg_ctx* ctx, uint64_t count) {
-    if (!ctx->item_counters) {
-        void* c = nullptr;
-        if (hipMalloc(&c, 8) != hipSuccess) return false;
-        if (hipMemset(c, 0, 8) != hipSuccess) {
-            (void)hipFree(c);
-            return false;
-        }
-        ctx->item_counters = static_cast<uint32_t*>(c);
-    }
-    const uint64_t bytes = count * 16u;
-    if (ctx->items_bytes >= bytes) return true;
-    if (ctx->items) (void)hipFree(ctx->items);
-    ctx->items = nullptr;
-    ctx->items_bytes = 0;
-    if (hipMalloc(&ctx->items, bytes) != hipSuccess) {
-        ctx->items = nullptr;
-        return false;
-    }
-    ctx->items_bytes = bytes;
-    return true;
 }
 
 int fail(nexg_ctx* ctx, int code, const char* fmt, const char* detail) {
@@ -159,11 +120,9 @@ int nexg_ctx_create(int device, nexg_ctx** out) {
 }
 
 int nexg_ctx_destroy(nexg_ctx* ctx) {
-    if (ctx && (ctx->scratch || ctx->items || ctx->item_counters)) {
+    if (ctx && ctx->scratch) {
         DeviceGuard g(ctx);
-        if (ctx->scratch) (void)hipFree(ctx->scratch);
-        if (ctx->items) (void)hipFree(ctx->items);
-        if (ctx->item_counters) (void)hipFree(ctx->item_counters);
+        (void)hipFree(ctx->scratch);
     }
     free(ctx);
     return NEXG_OK;
@@ -196,19 +155,8 @@ int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_
         a.tail = static_cast<uint32_t*>(scratch(ctx, a.count * 4u));
         if (!a.tail) return fail(ctx, NEXG_ENOMEM, "device scratch allocation failed%s", nullptr);
     }
-    const bool defer = span_defer() && v == nexg::ParseVariant::SpanTile && out_kind == NEXG_OUT_SPARSE &&
-                       a.count && a.count <= 0xFFFFFFFFull;
-    if (defer) {
-        if (!defer_buffers(ctx, a.count))
-            return fail(ctx, NEXG_ENOMEM, "device item buffer allocation failed%s", nullptr);
-        a.items = static_cast<uint4*>(ctx->items);
-        a.item_counters = ctx->item_counters;
-        a.item_which = ctx->item_which;
-    }
-    const int rc = hip_status(ctx, nexg::launch_parse(v, a, out_kind, static_cast<hipStream_t>(stream)),
-                              NEXG_ELAUNCH);
-    if (defer) ctx->item_which ^= 1u;  // the item kernel zeroed the other counter
-    return rc;
+    return hip_status(ctx, nexg::launch_parse(v, a, out_kind, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
 }
 
 int nexg_sparse_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,

@@ -23,12 +23,6 @@ struct ParseArgs {
     uint32_t hints = 0;       // NEXG_FRAMES_* (include/nexg.h)
     uint32_t* tail = nullptr; // TwoPass tail-sum hand-off (count entries) for outputs
                               // narrower than 4 B per frame; null -> the output itself
-    // SpanTile + NEXG_OUT_SPARSE with the generic pass deferred (ctx-owned):
-    // work items of the declined frames, the two alternating item counters and
-    // the one this launch appends to (the item kernel zeroes the other)
-    uint4* items = nullptr;
-    uint32_t* item_counters = nullptr;
-    uint32_t item_which = 0;
 };
 
 // Kernel variants of the parse path.

@@ -83,14 +83,6 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             // same process, 24 KiB at 5 waves equal, 28-32 KiB slower
             // (profiles/r02_kbench/kbench_subtile.log). Records (about 100
             // VGPRs) run uncapped on 16 KiB: capping them spills 44+ B.
-            if constexpr (OUT == NEXG_OUT_SPARSE) {
-                if (span_variant() == 1 && a.items) {  // generic pass deferred to k_span_items
-                    hipLaunchKernelGGL((k_parse_span<OUT, 1, 20480, 6, true>), grid, block, 0, s, a);
-                    const uint32_t ib = blocks < 1024u ? (uint32_t)blocks : 1024u;
-                    hipLaunchKernelGGL(k_span_items<NEXG_OUT_SPARSE>, dim3(ib), block, 0, s, a);
-                    break;
-                }
-            }
             if (span_variant() == 1) {
                 if (OUT == NEXG_OUT_RECORD) hipLaunchKernelGGL((k_parse_span<OUT, 1, 16384, 1>), grid, block, 0, s, a);
                 else hipLaunchKernelGGL((k_parse_span<OUT, 1, 20480, 6>), grid, block, 0, s, a);

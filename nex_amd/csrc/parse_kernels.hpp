@@ -557,117 +557,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 // sub-tile k also retires every lookup into sub-tile k-2's buffer (3 barriers
 // per sub-tile, ~42 KB LDS); NB = 1 (the library's): one buffer and a 4th
 // barrier (~25 KB LDS, 6 workgroups per CU).
-// wave-cooperative sums of the deferred checksum ranges (SpanDeferred) of a
-// wave's lanes: four at a time, one per 16-lane row, each lane summing up to
-// four 16-B loads in flight per step, rows reduced by xor shuffles. fa = the
-// absolute address of the lane's frame byte 0. Every lane of the wave calls it.
-__device__ __forceinline__ uint32_t span_deferred_sums(const SpanDeferred& dfr, uint64_t fa) {
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t mine = 0;
-    const uint32_t grp = lane >> 4, gl = lane & 15u;
-    for (uint64_t m = __ballot(dfr.which() != 0u); m;) {
-        const uint64_t cur = m;
-        uint64_t rest = cur;
-        uint32_t pick = 64u;  // this group's deferred lane (64: none)
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            const uint32_t b = rest ? (uint32_t)__builtin_ctzll(rest) : 64u;
-            pick = k == grp ? b : pick;
-            rest &= rest - 1;
-        }
-        m = rest;
-        const int src = (int)(pick & 63u);
-        const uint32_t rg = (uint32_t)__shfl((int)dfr.rng, src, 64);
-        const uint64_t fsrc = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(fa >> 32), src, 64) << 32) |
-                              (uint32_t)__shfl((int)(uint32_t)fa, src, 64);
-        const uint64_t A = fsrc + (rg & 0xFFFFu);
-        const uint64_t B = pick < 64u ? A + (rg >> 16) : A;
-        uint32_t s = 0;
-        for (uint64_t c = (A & ~15ull) + 16u * gl; c < B; c += 1024u) {
-            uint4 v[4];
-#pragma unroll
-            for (uint32_t k = 0; k < 4; k++)
-                v[k] = c + 256u * k < B ? load16(reinterpret_cast<const void*>(c + 256u * k)) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (uint32_t k = 0; k < 4; k++) s += chunk_range_sum(v[k], c + 256u * k, A, B);
-        }
-        s += __shfl_xor(s, 8, 16);
-        s += __shfl_xor(s, 4, 16);
-        s += __shfl_xor(s, 2, 16);
-        s += __shfl_xor(s, 1, 16);
-        const uint32_t rk = (uint32_t)__builtin_popcountll(cur & ((1ull << lane) - 1ull));
-        const uint32_t tot = (uint32_t)__shfl((int)s, (int)((rk & 3u) << 4), 64);
-        if (((cur >> lane) & 1ull) && rk < 4u) mine = tot;
-    }
-    return mine;
-}
-
-// The deferred generic pass of k_parse_span<NEXG_OUT_SPARSE, .., DEFER>: one
-// lane per declined frame (work items {index, tail sum, tail end | len << 16}),
-// its 80-B head gathered from HBM at any alignment into an LDS slot, the
-// generic core as in the span kernel, the descriptor stored into the frame's
-// exception slot (its rank among the group's exception codes, which the span
-// kernel wrote). Grid-stride over the launch's item count; zeroes the other
-// counter for the next launch.
-template <int OUT = NEXG_OUT_SPARSE>  // (a template: this header is included by several translation units)
-__global__ __launch_bounds__(256) void k_span_items(ParseArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kTile * 96];
-    __shared__ __attribute__((aligned(16))) uint8_t s_slot[kTile * SpanFrame::kSlot];
-    const uint32_t t = threadIdx.x;
-    const uint32_t n = a.item_counters[a.item_which];
-    if (blockIdx.x == 0 && t == 0) a.item_counters[a.item_which ^ 1u] = 0;
-    uint8_t* codes = reinterpret_cast<uint8_t*>(a.out);
-    uint2* exc = reinterpret_cast<uint2*>(codes + NEXG_SPARSE_EXC_OFFSET(a.count));
-    for (uint32_t b0 = blockIdx.x * kTile; b0 < n; b0 += gridDim.x * kTile) {  // uniform per workgroup
-        const uint32_t i = b0 + t;
-        const bool work = i < n;
-        const uint4 it = work ? a.items[i] : make_uint4(0, 0, 0, 0);
-        const uint64_t idx = (uint64_t)it.x | ((uint64_t)it.y << 32);
-        const uint32_t tq = it.z, qend = it.w & 0xFFFFu, len = it.w >> 16;
-        uint64_t off = 0;
-        uint32_t l2 = 0;
-        const bool ok = work && frame_extent(a, idx, off, l2) && l2 == len;
-        const uint64_t g = reinterpret_cast<uint64_t>(a.data) + off;
-        // head: the 16-B blocks from g & ~15 covering [g, g + min(len, 84))
-        uint8_t* st = s_stage + 96u * t;
-        const uint64_t gb = g & ~15ull, ge = g + (len < 84u ? len : 84u);
-#pragma unroll
-        for (uint32_t k = 0; k < 6; k++)
-            reinterpret_cast<uint4*>(st)[k] = ok && gb + 16u * k < ge ? load16(reinterpret_cast<const void*>(gb + 16u * k))
-                                                                      : make_uint4(0, 0, 0, 0);
-        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(st + ((uint32_t)(g & 15u) & ~3u));
-        const uint32_t sh = (uint32_t)(g & 3u);
-        uint32_t* slot = reinterpret_cast<uint32_t*>(s_slot + SpanFrame::kSlot * t);
-#pragma unroll
-        for (uint32_t k = 0; k < 20; k++) {
-            const uint32_t v = __builtin_amdgcn_alignbyte(s32[k + 1], s32[k], sh);
-            slot[k] = 4u * k < len ? (v & range_mask(4u * k, 0, len)) : 0u;
-        }
-        nexg_record rr{};
-        SpanDeferred dfr{};
-        if (ok) {
-            SpanFrame f{s_slot + SpanFrame::kSlot * t, reinterpret_cast<const uint8_t*>(g), qend, (uint32_t)(g & 1u), tq};
-            parse_frame(f, (uint32_t)(g & 1u), len, a.opt_flags, a.ip_offset, rr);
-            dfr = f.d;
-        } else if (work) {
-            rr.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
-        }
-        const uint32_t mine = span_deferred_sums(dfr, g);
-        if (dfr.which()) span_patch(dfr, mine, rr);
-        if (work) {  // exception slot: the exception codes of the group before this frame
-            const uint64_t g0 = idx & ~63ull;
-            uint32_t rank = 0;
-            for (uint64_t j = g0; j < idx; j += 4) {  // dword loads stay below the code area's end
-                const uint32_t v = *reinterpret_cast<const uint32_t*>(codes + j);
-#pragma unroll
-                for (uint32_t q = 0; q < 4; q++) rank += (j + q < idx && ((v >> (8u * q)) & 0xFFu) == 0u) ? 1u : 0u;
-            }
-            exc[g0 + rank] = make_uint2(rr.flags, (uint32_t)rr.payload_off | ((uint32_t)rr.payload_len << 16));
-        }
-    }
-}
-
-template <int OUT, int NB = 1, uint32_t SUB = 16384, int WPE = 1, bool DEFER = false>
+template <int OUT, int NB = 1, uint32_t SUB = 16384, int WPE = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_parse_span(ParseArgs a) {
     // each stage buffer: [96-B apron | SUB bytes | 96-B pad]; the apron holds
     // the previous sub-tile's last 96 bytes, so a head window that starts
@@ -840,16 +730,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // path for the few declined lanes of each wave. Items: {span position,
     // len | tail end << 16, tail sum, owner lane} in the idle prefix buffer;
     // results go back through the owner's slot.
-    if (DEFER) {  // declined frames become work items of k_span_items (sparse output only)
-        static_assert(!DEFER || OUT == NEXG_OUT_SPARSE, "deferred generic pass: sparse output");
-        const uint64_t m = __ballot(gen);
-        if (m) {
-            uint32_t wb = 0;
-            if (lane == 0) wb = atomicAdd(a.item_counters + a.item_which, (uint32_t)__builtin_popcountll(m));
-            wb = (uint32_t)__shfl((int)wb, 0, 64);
-            if (gen) a.items[wb + lanes_below(m)] = make_uint4((uint32_t)idx, (uint32_t)(idx >> 32), tq, qend | len << 16);
-        }
-    } else if (__syncthreads_or(gen)) {
+    if (__syncthreads_or(gen)) {
         if (t < kBuckets) s_hist[t] = 0;
         __syncthreads();
         const uint32_t rank = gen ? atomicAdd(&s_hist[key], 1u) : 0u;
