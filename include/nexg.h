@@ -29,7 +29,9 @@
  *     (NEXG_OK = 0, negative on error) and never aborts.
  *   - All frame / output buffers are DEVICE pointers owned by the caller;
  *     work is enqueued on `stream` (a hipStream_t, NULL = default stream) and
- *     is stream-ordered: the call returns before the kernels finish.
+ *     is stream-ordered: the call returns before the kernels finish. Calls
+ *     on one context may use different streams: the context's one device
+ *     scratch (TwoPass tail sums) is handed between streams with an event.
  *   - One context per device; a context is not thread-safe (the reference's
  *     RawReceiver is likewise single-consumer, nex-datalink/src/lib.rs:363).
  *   - Frame-level parse failures are data, not call errors: they are reported
@@ -687,7 +689,10 @@ int nexg_rx_open(const char* ifname, const nexg_rx_config* cfg, nexg_rx** out);
 /* Up to max_frames frames (bytes packed: frame k at data + offsets[k],
  * offsets[n] = end; offsets holds max_frames + 1 entries); waits up to the
  * read timeout for the first frame (*n_frames = 0 on timeout), then takes
- * whatever the ring / socket already holds. ts_ns optional. */
+ * whatever the ring / socket already holds. ts_ns optional. NEXG_ERANGE
+ * (nothing taken) when data_cap cannot hold the next frame (ring mode) or one
+ * read_buffer_size slot (recvmmsg mode): a retry with a larger buffer
+ * resumes at that frame. */
 int nexg_rx_next_batch(nexg_rx* rx, uint8_t* data, uint64_t data_cap, uint64_t* offsets,
                        uint64_t max_frames, uint64_t* ts_ns, uint64_t* n_frames);
 /* PACKET_STATISTICS since the last call: frames seen, frames dropped. */

@@ -18,6 +18,9 @@ struct nexg_ctx {
     char last_error[256];
     void* scratch;          // device memory for per-call hand-offs (TwoPass tail sums)
     uint64_t scratch_bytes;
+    hipEvent_t scratch_done;    // recorded after the last launch that used the scratch ...
+    hipStream_t scratch_stream; // ... on this stream
+    bool scratch_used;
 };
 
 namespace {
@@ -51,6 +54,26 @@ void* scratch(nexg_ctx* ctx, uint64_t bytes) {
     }
     ctx->scratch_bytes = want;
     return ctx->scratch;
+}
+
+// The scratch is shared by every call on the context, whatever its stream:
+// a call on another stream than the last user's waits for that user's launch
+// (stream order alone covers calls on one stream).
+hipError_t scratch_acquire(nexg_ctx* ctx, hipStream_t stream) {
+    if (!ctx->scratch_used || ctx->scratch_stream == stream) return hipSuccess;
+    return hipStreamWaitEvent(stream, ctx->scratch_done, 0);
+}
+
+hipError_t scratch_release(nexg_ctx* ctx, hipStream_t stream) {
+    if (!ctx->scratch_done) {
+        const hipError_t e = hipEventCreateWithFlags(&ctx->scratch_done, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    const hipError_t e = hipEventRecord(ctx->scratch_done, stream);
+    if (e != hipSuccess) return e;
+    ctx->scratch_stream = stream;
+    ctx->scratch_used = true;
+    return hipSuccess;
 }
 
 int fail(nexg_ctx* ctx, int code, const char* fmt, const char* detail) {
@@ -120,9 +143,10 @@ int nexg_ctx_create(int device, nexg_ctx** out) {
 }
 
 int nexg_ctx_destroy(nexg_ctx* ctx) {
-    if (ctx && ctx->scratch) {
+    if (ctx && (ctx->scratch || ctx->scratch_done)) {
         DeviceGuard g(ctx);
-        (void)hipFree(ctx->scratch);
+        if (ctx->scratch) (void)hipFree(ctx->scratch);
+        if (ctx->scratch_done) (void)hipEventDestroy(ctx->scratch_done);
     }
     free(ctx);
     return NEXG_OK;
@@ -151,12 +175,15 @@ int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_
     a.out = out;
     a.tile_order = nexg::tile_order_for(a);
     const nexg::ParseVariant v = nexg::choose_parse_variant(a);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
     if (nexg::parse_needs_tail(v, out_kind) && a.count) {
         a.tail = static_cast<uint32_t*>(scratch(ctx, a.count * 4u));
         if (!a.tail) return fail(ctx, NEXG_ENOMEM, "device scratch allocation failed%s", nullptr);
+        if (int rc = hip_status(ctx, scratch_acquire(ctx, st), NEXG_ELAUNCH)) return rc;
+        if (int rc = hip_status(ctx, nexg::launch_parse(v, a, out_kind, st), NEXG_ELAUNCH)) return rc;
+        return hip_status(ctx, scratch_release(ctx, st), NEXG_ELAUNCH);
     }
-    return hip_status(ctx, nexg::launch_parse(v, a, out_kind, static_cast<hipStream_t>(stream)),
-                      NEXG_ELAUNCH);
+    return hip_status(ctx, nexg::launch_parse(v, a, out_kind, st), NEXG_ELAUNCH);
 }
 
 int nexg_sparse_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,

@@ -212,6 +212,7 @@ int nexg_rx_next_batch(nexg_rx* rx, uint8_t* data, uint64_t data_cap, uint64_t* 
                 if (rc) return rc;
                 if (next < bd->hdr.bh1.num_pkts) {  // the batch is full: resume here next call
                     rx->pkt = next;
+                    if (n == 0) return NEXG_ERANGE;  // not even the next frame fits data_cap: never spin on it
                     break;
                 }
                 __atomic_store_n(&bd->hdr.bh1.block_status, (uint32_t)TP_STATUS_KERNEL, __ATOMIC_RELEASE);
@@ -232,6 +233,7 @@ int nexg_rx_next_batch(nexg_rx* rx, uint8_t* data, uint64_t data_cap, uint64_t* 
         }
     } else {
         const uint32_t S = rx->cfg.read_buffer_size;
+        if (data_cap < S) return NEXG_ERANGE;  // no slot ever fits: fail instead of polling a readable socket forever
         std::vector<mmsghdr> msgs(1024);
         std::vector<iovec> iov(1024);
         std::vector<sockaddr_ll> from(1024);

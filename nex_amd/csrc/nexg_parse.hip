@@ -48,21 +48,6 @@ ParseVariant choose_parse_variant(const ParseArgs& a) {
     return ParseVariant::TwoPass;
 }
 
-// Span kernel generation: NEXG_SPAN=1 (4 barriers per 16-KiB sub-tile, the
-// default: measured best), 1w1 (the same without the 6-waves/SIMD register
-// cap), 2 (2 barriers), 2d (8-KiB double-buffered
-// sub-tiles, 1 barrier). Fewer barriers measured slower (0.66 vs 0.73 of
-// peak, profiles/r02_kbench/): the per-group stream, not the barriers,
-// bounds the loop.
-static int span_variant() {
-    static const int v = [] {
-        const char* e = getenv("NEXG_SPAN");
-        if (!e) return 1;
-        return strcmp(e, "1") == 0 ? 1 : strcmp(e, "2d") == 0 ? 3 : strcmp(e, "1w1") == 0 ? 4 : 2;
-    }();
-    return v;
-}
-
 template <int OUT>
 static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream_t s) {
     const uint64_t blocks = (a.count + kTile - 1) / kTile;
@@ -83,13 +68,10 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             // same process, 24 KiB at 5 waves equal, 28-32 KiB slower
             // (profiles/r02_kbench/kbench_subtile.log). Records (about 100
             // VGPRs) run uncapped on 16 KiB: capping them spills 44+ B.
-            if (span_variant() == 1) {
-                if (OUT == NEXG_OUT_RECORD) hipLaunchKernelGGL((k_parse_span<OUT, 1, 16384, 1>), grid, block, 0, s, a);
-                else hipLaunchKernelGGL((k_parse_span<OUT, 1, 20480, 6>), grid, block, 0, s, a);
-            }
-            else if (span_variant() == 4) hipLaunchKernelGGL((k_parse_span<OUT, 1>), grid, block, 0, s, a);
-            else if (span_variant() == 3) hipLaunchKernelGGL((k_parse_span2<OUT, 8192, 2>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((k_parse_span2<OUT, 16384, 1>), grid, block, 0, s, a);
+            // (Two-barrier / double-buffered generations measured slower,
+            // 0.66-0.69 vs 0.75: tools/kbench.hip keeps them for A/B.)
+            if (OUT == NEXG_OUT_RECORD) hipLaunchKernelGGL((k_parse_span<OUT, 1, 16384, 1>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_parse_span<OUT, 1, 20480, 6>), grid, block, 0, s, a);
             break;
         case ParseVariant::TwoPass:
             hipLaunchKernelGGL((k_tail_sums<OUT, 4>), grid, block, 0, s, a);

@@ -302,6 +302,7 @@ void walk_interleaved(const nexg_pcap* p, const uint8_t* buf, size_t have, const
     for (size_t j = 0; j < m; j++) {
         pos[j] = from[j];
         w[j].begin = from[j];
+        w[j].end = from[j];  // a chain that never starts describes nothing: it ends where it began
         live[j] = pos[j] < stop[j];
         active += live[j];
     }

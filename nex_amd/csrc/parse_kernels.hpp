@@ -828,148 +828,4 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
-// k_parse_span with two barriers per sub-tile instead of four (NB = 1), or
-// one (NB = 2, double-buffered stage). The scan needs no exchange of chunk
-// sums: chunk c = t + 256 i (the coalesced load order) sits in scan block
-// b = c / 64 = 4 i + wave, whose 64 chunks are exactly one wave's i-th
-// loads, so each wave scans its blocks in registers (DPP), stores the
-// in-block exclusive prefixes and the block totals, and after the one
-// publishing barrier a lookup adds the totals of the blocks before its
-// chunk (NBLK predicated adds). NB = 2 stages sub-tile k into buffer k & 1:
-// the barrier that publishes sub-tile k+1 also retires every lookup into
-// sub-tile k, so buffer k & 1 is free again when sub-tile k+2 arrives.
-template <int OUT, uint32_t SUB = 16384, int NB = 1, int WPE = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_parse_span2(ParseArgs a) {
-    constexpr uint32_t CPT = SUB / 4096u;  // 16-B chunks per thread per sub-tile
-    constexpr uint32_t NBLK = 4u * CPT;    // 64-chunk scan blocks per sub-tile
-    static_assert(CPT >= 1 && SUB % 4096u == 0, "sub-tile is a multiple of 4 KiB");
-    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[NB][SUB];
-    __shared__ __attribute__((aligned(16))) uint32_t s_pfx[NB][SUB / 16u];
-    __shared__ __attribute__((aligned(16))) uint32_t s_tot[NB][NBLK];
-    __shared__ uint64_t s_span[2];
-    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    const uint64_t f0 = (uint64_t)blockIdx.x * kTile;
-    const uint64_t idx = f0 + t;
-    const uint32_t nf = a.count - f0 < kTile ? (uint32_t)(a.count - f0) : kTile;
-    const uint64_t base = reinterpret_cast<uint64_t>(a.data);
-    uint64_t off = 0;
-    uint32_t len = 0;
-    const bool have = t < nf;
-    const bool ok = have && frame_extent(a, idx, off, len);
-    if (t == 0) s_span[0] = off;
-    if (t == nf - 1) s_span[1] = off + len;
-    __syncthreads();
-    const uint64_t lo = s_span[0], hi = s_span[1];
-    const bool inside = !have || (ok && off >= lo && off + len <= hi);
-    const bool span_ok = __syncthreads_and(inside) && hi >= lo && hi - lo <= (1ull << 30);
-    nexg_record r{};
-    if (!span_ok) {  // not one ordered span here: every lane parses its own frame from HBM
-        if (have) {
-            if (!ok) {
-                r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
-            } else {
-                GlobalFrame f{a.data + off};
-                parse_frame(f, (uint32_t)((base + off) & 1u), len, a.opt_flags, a.ip_offset, r);
-            }
-        }
-        store_out<OUT>(a, idx, have, r);
-        return;
-    }
-    const uint64_t A0 = (base + lo) & ~15ull;
-    const uint32_t span = (uint32_t)(((base + hi + 15u) & ~15ull) - A0);
-    const uint32_t hr = (uint32_t)(base + off - A0);
-    const bool want_tail = have && len > kLaneWin;
-    const bool fast = have && ((base + off) & 3u) == 0 && !(a.opt_flags & NEXG_PARSE_FROM_IP);
-    uint32_t qa = 0, qb = 0, run = 0;
-    uint32_t w[20];
-#pragma unroll
-    for (int j = 0; j < 20; j++) w[j] = 0;
-
-    uint4 cur[CPT];
-    auto fetch = [&](uint32_t S) {
-#pragma unroll
-        for (uint32_t i = 0; i < CPT; i++) {
-            const uint32_t c = S + 16u * (t + 256u * i);
-            cur[i] = c < span ? load16<true>(reinterpret_cast<const void*>(A0 + c)) : make_uint4(0, 0, 0, 0);
-        }
-    };
-    fetch(0);
-    uint32_t buf = 0;
-    for (uint32_t S = 0; S < span; S += SUB, buf = NB == 2 ? buf ^ 1u : 0u) {
-        uint8_t* sb = s_bytes[buf];
-        uint32_t* sp = s_pfx[buf];
-        uint32_t* st = s_tot[buf];
-        // (1) stage bytes; in-block exclusive prefixes and block totals in registers
-#pragma unroll
-        for (uint32_t i = 0; i < CPT; i++) {
-            const uint32_t c = t + 256u * i;
-            *reinterpret_cast<uint4*>(sb + 16u * c) = cur[i];
-            const uint32_t cs = chunk_le_sum(cur[i]);
-            const uint32_t inc = wave_incl_scan_dpp(cs);
-            sp[c] = inc - cs;
-            if (lane == 63u) st[4u * i + wv] = inc;
-        }
-        const uint32_t E = S + SUB;
-        if (E < span) fetch(E);
-        __syncthreads();
-        // (2) prefix values at this sub-tile's positions, head window copy
-        // (block totals re-read from LDS as broadcasts: no registers held)
-        const bool last = E >= span;
-        auto q_at = [&](uint32_t d) {  // d = position - S, 0 <= d <= SUB
-            const uint32_t c = d >> 4, m = d & 15u, b = c >> 6;
-            uint32_t q = run;
-#pragma unroll
-            for (uint32_t k = 0; k < NBLK; k += 4) {
-                const uint4 v = *reinterpret_cast<const uint4*>(st + k);
-                q += (k < b ? v.x : 0u) + (k + 1 < b ? v.y : 0u) + (k + 2 < b ? v.z : 0u) + (k + 3 < b ? v.w : 0u);
-            }
-            if (c < SUB / 16u) q += sp[c] + (m ? chunk_prefix_sum(sb + 16u * c, m) : 0u);
-            return q;
-        };
-        const uint32_t da = hr + kLaneWin - S, db = hr + len - S;  // wrap: < 0 -> huge
-        if (want_tail && (da < SUB || (last && da == SUB))) qa = q_at(da);
-        if (have && (db < SUB || (last && db == SUB))) qb = q_at(db);
-        const uint32_t dh = hr - S;
-        if (fast) {
-            if (dh <= SUB - kLaneWin) {  // whole window in this sub-tile (the usual case)
-#pragma unroll
-                for (int j = 0; j < 20; j++) w[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4u * j);
-            } else if (dh < SUB || dh + kLaneWin - 1u < kLaneWin - 1u) {  // straddles a sub-tile edge
-#pragma unroll
-                for (int j = 0; j < 20; j++) {
-                    const uint32_t d = dh + 4u * j;
-                    if (d < SUB) w[j] = *reinterpret_cast<const uint32_t*>(sb + d);
-                }
-            }
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < NBLK; k += 4) {
-            const uint4 v = *reinterpret_cast<const uint4*>(st + k);
-            run += v.x + v.y + v.z + v.w;
-        }
-        if (NB == 1) __syncthreads();
-    }
-    if (have) {
-        bool done = false;
-        if (fast) {
-#pragma unroll
-            for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
-            done = fast_canonical80(w, len, a.opt_flags, want_tail ? (uint32_t)(qb - qa) : 0u, len, r);
-        }
-        if (!done) {
-            GlobalFrame f{a.data + off};
-            parse_frame(f, (uint32_t)((base + off) & 1u), len, a.opt_flags, a.ip_offset, r);
-        }
-    }
-    if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
-    if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the (now idle) byte buffer
-        static_assert(OUT != NEXG_OUT_RECORD || NB * SUB >= kTile * 64u, "record staging needs 16 KiB");
-        uint8_t* stage = &s_bytes[0][0];
-        __syncthreads();  // NB = 2: the other buffer may still be read; NB = 1: already idle
-        if (have) stage_record(stage + 64u * t, r);
-        __syncthreads();
-        copy_out_records<64>(stage, a.out, f0, nf);
-    }
-}
-
 }  // namespace nexg

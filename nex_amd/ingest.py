@@ -229,14 +229,20 @@ def device_mapped_batches(reader: PcapReader, max_frames: int = 1 << 20, window:
     hip = ctypes.CDLL("libamdhip64.so")  # torch's HIP runtime (already loaded)
     base = arr.ctypes.data
     chunk = window  # registered for DMA chunk by chunk as the walk reaches it
-    registered = []
+    registered = []  # chunk indices currently page-locked (at most the two the window touches)
+    nxt_chunk = [0]
 
     def register_upto(end):
-        for c in range(len(registered), (min(end, size) + chunk - 1) // chunk):
+        for c in range(nxt_chunk[0], (min(end, size) + chunk - 1) // chunk):
             a, b = c * chunk, min(size, (c + 1) * chunk)
             if hip.hipHostRegister(ctypes.c_void_p(base + a), ctypes.c_size_t(b - a), ctypes.c_uint(0)) != 0:
                 raise PcapError("hipHostRegister of the capture mapping failed")
             registered.append(c)
+            nxt_chunk[0] = c + 1
+
+    def unregister_below(p):  # chunks wholly behind the walk: their copies have completed
+        while registered and (registered[0] + 1) * chunk <= p:
+            hip.hipHostUnregister(ctypes.c_void_p(base + registered.pop(0) * chunk))
     s = stream or torch.cuda.current_stream()
     try:
         buf = torch.empty(window, dtype=torch.uint8, device=device)
@@ -245,6 +251,7 @@ def device_mapped_batches(reader: PcapReader, max_frames: int = 1 << 20, window:
         onp, lnp = offs.numpy().view(np.uint64), lens.numpy().view(np.uint32)
         while pos < size:
             s.synchronize()  # the previous batch's copies and parse are done with the staging
+            unregister_below(pos)  # a capture may be far larger than host memory: pin only the window
             register_upto(pos + window)
             n, nxt = reader.walk_mapped(pos, window, onp, lnp)
             if n == 0:  # pcapng blocks without packets

@@ -16,9 +16,11 @@ from . import abi
 
 MUTATIONS = ("truncate", "pad", "ip_length", "ver_ihl", "l4_length", "ipv6_hbh", "vlan", "proto200", "random")
 #: not in the App. C mix; selectable through `kinds` (tools/bench_malformed.py):
-#: tcp_ts = the real-traffic TCP shape, NOP NOP Timestamps (12 B) after the
-#: TCP header of a TCP frame, data offset 8 (checksums left stale)
-EXTRA = ("tcp_ts",)
+#: real-traffic TCP option lists inserted after the TCP header of a TCP frame
+#: (data offset and IP length grown to fit, checksums left stale):
+#: tcp_ts = NOP NOP Timestamps (12 B, data offset 8: most data segments),
+#: tcp_sack = NOP NOP SACK with 1-4 blocks (12-36 B), tcp_mss = MSS alone (4 B, SYN-ACK)
+EXTRA = ("tcp_ts", "tcp_sack", "tcp_mss")
 _ALL = MUTATIONS + EXTRA
 
 
@@ -68,9 +70,20 @@ def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share
     hbh = sel("ipv6_hbh")
     hbh = hbh[~eth_v4[hbh]]
     ins[hbh] = 8
-    tts = sel("tcp_ts")
-    tts = tts[buf[offs[tts] + np.where(eth_v4[tts], 23, 20)] == 6]
-    ins[tts] = 12
+    topt = {}  # frame -> TCP option bytes inserted after its 20-B TCP header
+    for k in ("tcp_ts", "tcp_sack", "tcp_mss"):
+        t = sel(k)
+        t = t[buf[offs[t] + np.where(eth_v4[t], 23, 20)] == 6]
+        blocks = rng.integers(1, 5, len(t))
+        body = rng.integers(0, 256, (len(t), 32), dtype=np.uint8)
+        for j, nb, b in zip(t.tolist(), blocks.tolist(), body):
+            if k == "tcp_ts":
+                topt[j] = np.concatenate([np.array([1, 1, 8, 10], np.uint8), b[:8]])
+            elif k == "tcp_sack":
+                topt[j] = np.concatenate([np.array([1, 1, 5, 2 + 8 * nb], np.uint8), b[:8 * nb]])
+            else:
+                topt[j] = np.array([2, 4, 5, 180], np.uint8)
+            ins[j] = len(topt[j])
     new_len = new_len + pad + ins
     new_offs = np.zeros(count + 1, np.int64)
     np.cumsum(new_len, out=new_offs[1:])
@@ -86,17 +99,17 @@ def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share
         f = buf[offs[j]:offs[j + 1]]
         if pad[j]:
             f = np.concatenate([f, rng.integers(0, 256, pad[j], dtype=np.uint8)])
-        elif ins[j] == 4:  # 802.1Q tag in front of the EtherType (frame[12:14])
-            f = np.concatenate([f[:12], np.array([0x81, 0, 0, 0x64], np.uint8), f[12:]])
-        elif ins[j] == 12:  # NOP NOP Timestamps after the TCP header, data offset 8
+        elif j in topt:  # TCP options after the TCP header, data offset grown to fit
+            o = topt[j]
             l4 = 34 if eth_v4[j] else 54
             g = f.copy()
-            g[l4 + 12] = (8 << 4) | (g[l4 + 12] & 0x0F)
+            g[l4 + 12] = ((5 + len(o) // 4) << 4) | (g[l4 + 12] & 0x0F)
             k = 16 if eth_v4[j] else 18
-            v = ((int(g[k]) << 8) | int(g[k + 1])) + 12
+            v = ((int(g[k]) << 8) | int(g[k + 1])) + len(o)
             g[k], g[k + 1] = v >> 8, v & 0xFF
-            ts = np.concatenate([np.array([1, 1, 8, 10], np.uint8), rng.integers(0, 256, 8, dtype=np.uint8)])
-            f = np.concatenate([g[:l4 + 20], ts, g[l4 + 20:]])
+            f = np.concatenate([g[:l4 + 20], o, g[l4 + 20:]])
+        elif ins[j] == 4:  # 802.1Q tag in front of the EtherType (frame[12:14])
+            f = np.concatenate([f[:12], np.array([0x81, 0, 0, 0x64], np.uint8), f[12:]])
         elif ins[j] == 8:  # hop-by-hop header carrying the original next header
             nh = f[20]
             g = f.copy()

@@ -370,3 +370,82 @@ def vlan_frames():
     f.append(bytes(12) + b"\x81\x00\x00\x01\x08")    # inner EtherType cut short
     f.append(bytes(12) + b"\x81\x00\x00\x01\x08\x00")  # tag complete, nothing after
     return f
+
+
+def tcp_option_lists(rng):
+    """Systematic TCP option lists around the register path's one-TLV branch
+    (frame_core.hpp fast_canonical80: `one` = kind >= 2 with length == the
+    option bytes; `nnx` = NOP NOP + kind >= 2 with 2 + length == the option
+    bytes), for every data offset 6..15: the branch's own shapes (MSS alone,
+    SACK 1-4 blocks, timestamps, any kind) and the near misses either side
+    (lengths one off, EOL / NOP where the TLV should be, lengths 0 / 1, two
+    TLVs, NOPs only). The reference's walk and re-serialisation are
+    tcp.rs:731-836 and :521-575."""
+    rnd = lambda n: bytes(rng.integers(0, 256, max(0, n), dtype=np.uint8))
+    out = []
+    for olen in range(4, 41, 4):
+        for kind in (2, 3, 4, 5, 8, 30, 254):
+            for d in (0, 0, 0, -1, 1, -olen + 2):  # the branch's own shape three times
+                ln = olen + d
+                if 0 <= ln < 256:
+                    out.append(bytes([kind, ln]) + rnd(olen - 2))
+        for kind in (5, 8, 19, 2, 255):
+            for d in (0, 0, 0, -1, 1):
+                ln = olen - 2 + d
+                if 0 <= ln < 256:
+                    out.append(bytes([1, 1, kind, ln]) + rnd(olen - 4))
+        out.append(bytes([1, 1, 0, olen - 2]) + rnd(olen - 4))      # EOL where the kind goes
+        out.append(bytes([1, 1, 1, olen - 2]) + rnd(olen - 4))      # a third NOP
+        out.append(bytes([1, 1, 5, 1]) + rnd(olen - 4))             # length 1
+        out.append(bytes([1, 1, 5, 0]) + rnd(olen - 4))             # length 0
+        out.append(bytes([0, olen]) + rnd(olen - 2))                # EOL first (rest is padding)
+        out.append(bytes([1, olen - 1]) + rnd(olen - 2))            # one NOP, then junk
+        out.append(bytes([1, 2, olen - 2]) + rnd(olen - 3))         # NOP + TLV (not two NOPs)
+        out.append(bytes([1]) * olen)                               # NOPs only
+        if olen >= 8:
+            out.append(bytes([2, 4, 5, 180, 5, olen - 4]) + rnd(olen - 6))        # two TLVs
+            out.append(bytes([1, 1, 8, 10]) + rnd(8) + bytes(olen - 12) if olen >= 12 else
+                       bytes([1, 1, 8, olen - 2]) + rnd(olen - 4))                  # TS + EOL padding
+            out.append(bytes([1, 1, 5, olen - 6]) + rnd(olen - 8) + bytes([1, 1, 1, 0]))  # TLV short, NOPs
+    return out
+
+
+def tcp_option_sweep(oracle, rng, bases):
+    """Every list of tcp_option_lists() put behind TCP frames of `bases`
+    (IPv4 and IPv6, several payload lengths incl. 0 and odd), data offset and
+    IP length set to fit; per frame the checksum-valid form (oracle's computed
+    IPv4 / TCP checksums written back), a copy with one payload or option
+    byte flipped (L4 verdict false), an IPv4 copy with a stale header
+    checksum, and a copy truncated inside the option area (no TcpPacket)."""
+    tcp = []
+    for f in bases:
+        v4 = f[12:14] == b"\x08\x00"
+        l4 = 34 if v4 else 54
+        if len(f) >= l4 + 20 and f[23 if v4 else 20] == 6:
+            tcp.append((f, v4, l4))
+    assert len(tcp) >= 4
+    out = []
+    lists = tcp_option_lists(rng)
+    for i, opts in enumerate(lists):
+        for j in range(3):
+            f, v4, l4 = tcp[(3 * i + j) % len(tcp)]
+            g = bytearray(f[:l4 + 20] + opts + f[l4 + 20:])
+            g[l4 + 12] = ((5 + len(opts) // 4) << 4) | (g[l4 + 12] & 0x0F)
+            k = 16 if v4 else 18
+            g[k:k + 2] = (int.from_bytes(g[k:k + 2], "big") + len(opts)).to_bytes(2, "big")
+            r = oracle.parse_frame(bytes(g))
+            if v4:
+                g[24:26] = int(r["ip_csum_calc"]).to_bytes(2, "big")
+            if r["l4_csum_calc"] or r["flags"] & abi.C_L4_CHECKED:
+                g[l4 + 16:l4 + 18] = int(r["l4_csum_calc"]).to_bytes(2, "big")
+            out.append(bytes(g))
+            h = bytearray(g)
+            h[int(rng.integers(l4 + 20, len(h)))] ^= 0x24
+            out.append(bytes(h))
+            if v4 and j == 0:
+                h = bytearray(g)
+                h[25] ^= 0x01
+                out.append(bytes(h))
+            if j == 1:
+                out.append(bytes(g[: l4 + 20 + int(rng.integers(0, len(opts)))]))
+    return out

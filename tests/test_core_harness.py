@@ -128,6 +128,7 @@ def test_canonical_fast_path_on_imix(oracle):
     frames += helpers.tcp_ts_frames(oracle, base[:1500], rng)  # TCP timestamps (register fast path)
     frames += helpers.tcp_ts_frames(oracle, base[1500:2000], rng, fix_checksums=False)
     frames += helpers.tcp_option_frames(oracle, base[:2500], rng)  # one-TLV option lists and near misses
+    frames += helpers.tcp_option_sweep(oracle, rng, base[:600])  # ... for every data offset 6..15
     for e in (64, 79, 80, 81, 83, 84, 85, 100):  # IPv4/UDP of IP end e, padded by 1..40
         for pad in (1, 3, 4, 17, 40):
             body = bytes(rng.integers(0, 256, e - 42, dtype=np.uint8))

@@ -8,6 +8,7 @@ truncated to read_buffer_size as the reference's recvfrom truncates them."""
 import os
 import struct
 import subprocess
+import time
 
 import numpy as np
 import pytest
@@ -179,3 +180,28 @@ def test_open_errors():
         RawReceiver("no-such-if0", Config())
     with pytest.raises((DatalinkError, PermissionError)):
         RawReceiver("lo", Config(read_buffer_size=0))
+
+
+@live
+@pytest.mark.parametrize("mode", [0, 1], ids=["tpacket_v3", "recvmmsg"])
+@pytest.mark.timeout(60)
+def test_rx_buffer_too_small_fails_instead_of_spinning(frames, mode):
+    """a data_cap that cannot hold the next frame (ring) or
+    one read_buffer_size slot (recvmmsg) returns NEXG_ERANGE instead of
+    polling a readable socket forever (read_timeout -1 = wait); a retry with
+    a large buffer then resumes at that frame, losing nothing."""
+    from nex_amd.datalink import Config, DatalinkError, RawReceiver
+    fr = _tagged([f for f in frames if len(f) >= 100] * 4, 30 + mode)
+    with RawReceiver("lo", Config(read_timeout_ms=-1, mode=mode, skip_outgoing=True)) as rx:
+        _send(fr)
+        time.sleep(0.05)
+        with pytest.raises(DatalinkError):
+            for _ in range(100):  # other loopback traffic may fit first; ours never does
+                d, o = rx.next_batch(data_cap=40)
+                assert len(o) > 1
+        got = []
+        while len(got) < len(fr):
+            d, o = rx.next_batch()
+            got += [bytes(d[int(a):int(b)]) for a, b in zip(o[:-1], o[1:])]
+            got = [g for g in got if g[6:12] == MAC_SRC[:5] + bytes([30 + mode])]
+        assert got == fr

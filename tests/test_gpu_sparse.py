@@ -181,3 +181,33 @@ def test_record_gap_batches_match_oracle(engine, oracle):
     want = oracle.parse_frames(frames)
     helpers.records_equal(engine.parse_to_numpy(b, out_kind=abi.OUT_RECORD), want, frames, "record gap")
     helpers.records_equal(engine.parse_to_numpy(b, out_kind=abi.OUT_SPARSE), desc_of(want), frames, "gap sparse")
+
+
+def test_twopass_scratch_across_streams(engine, oracle, corpus):
+    """narrow-output TwoPass parses hand their tail sums over
+    through the one ctx scratch. Calls on one context from two streams are
+    ordered by the context (an event per hand-over), so interleaved verdict /
+    sparse parses of two different batches on two streams, with no sync in
+    between, each equal the oracle."""
+    import torch
+    fa, fb = corpus[:20000], corpus[-20000:]
+    ba, bb = FrameBatch.from_frames(fa, pad_to=4), FrameBatch.from_frames(fb, pad_to=4)
+    wa, wb = oracle.parse_frames(fa), oracle.parse_frames(fb)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    outs = []
+    for k in range(6):
+        outs.append(("a", engine.parse(ba, out_kind=abi.OUT_VERDICT, stream=sa)))
+        outs.append(("b", engine.parse(bb, out_kind=abi.OUT_VERDICT, stream=sb)))
+        outs.append(("a", engine.parse(ba, out_kind=abi.OUT_SPARSE, stream=sa)))
+        outs.append(("b", engine.parse(bb, out_kind=abi.OUT_SPARSE, stream=sb)))
+    torch.cuda.synchronize()
+    for k, (which, out) in enumerate(outs):
+        frames, want, batch = (fa, wa, ba) if which == "a" else (fb, wb, bb)
+        h = out.cpu().numpy()
+        if k % 4 < 2:
+            got = abi.verdict_to_flags(h[: 2 * len(frames)].view(abi.VERDICT_DTYPE)["verdict"])
+            assert (got == want["flags"].astype(np.uint32)).all(), (k, which)
+        else:
+            d = abi.sparse_to_desc(h, batch.count, batch.frame_lengths())
+            helpers.records_equal(d, desc_of(want), frames, f"stream {which} call {k}")

@@ -348,3 +348,35 @@ def test_mapped_parallel_walk(tmp_path, threads):
     with PcapReader(path) as r:
         r.set_read_threads(threads)
         assert list(mapped_frames(r, window=9 << 20, max_frames=1 << 15)) == fr
+
+
+@pytest.mark.parametrize("shape", ["raw", "mapped"])
+def test_parallel_walk_large_final_record(tmp_path, shape):
+    """a chunk with no plausible header start (all its bytes
+    inside one record larger than a chunk) is never live in the interleaved
+    walk; when the buffer ends on a record boundary right after it, the walk
+    must still report the whole buffer as consumed, not offset 0 (which made
+    read_raw hand the same frames back forever and walk_mapped never
+    advance). 16 threads = 128 chunks of ~66 KB over a buffer just over
+    8 MiB whose last record is 300 KB of 0xFF (no look-alike header)."""
+    import itertools
+
+    from nex_amd.ingest import mapped_frames, raw_frames
+    rng = np.random.default_rng(11)
+    fr, total = [], 24
+    while total < (8 << 20) + 4096 - 300_000:
+        f = rng.integers(0, 256, int(rng.integers(60, 1500)), dtype=np.uint8).tobytes()
+        fr.append(f)
+        total += 16 + len(f)
+    fr.append(b"\xff" * 300_000)
+    fr_mid = fr[:-1] + [b"\xff" * 140_000] + fr[-1:]  # and a chunk-spanning record in the middle
+    for name, frs in (("end", fr), ("mid", fr_mid)):
+        path = _write(tmp_path, f"big_{name}.pcap", pcapfile.classic(frs))
+        with PcapReader(path) as r:
+            r.set_read_threads(16)
+            if shape == "raw":
+                it = raw_frames(r, cap=os.path.getsize(path) + 64, max_frames=1 << 15)
+            else:
+                it = mapped_frames(r, window=os.path.getsize(path) + 64, max_frames=1 << 15)
+            got = list(itertools.islice(it, len(frs) + 8))
+        assert len(got) == len(frs) and got == frs, (name, len(got), len(frs))

@@ -21,7 +21,6 @@ for s in ${STEPS:-tests}; do
     tests) step pytest_gpu 900 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench_udp64 500 python bench.py --steps 50 --cpu-seconds 5 ;;
-    benchw1) step bench_w1 400 env NEXG_SPAN=1w1 python bench.py --steps 50 --no-cpu-baseline ;;
     malformed) step bench_malformed 500 python tools/bench_malformed.py ;;
     benchpcap) step bench_pcap 400 python bench.py --workload imix_pcap --steps 20 --cpu-seconds 5 ;;
     ser) step bench_ser 300 python bench.py --workload ser --steps 50 --no-cpu-baseline ;;
@@ -30,7 +29,6 @@ for s in ${STEPS:-tests}; do
     rehearse2) step rehearse2 600 env NEXG_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 2 ;;
     rehearse8) step rehearse8 900 env NEXG_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 8 --steps 10 --warmup 3 --cpu-seconds 2 ;;
     benchimix) step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5 ;;
-    spanvar) for v in 1 2 2d; do step bench_imix_span$v 300 env NEXG_SPAN=$v python bench.py --workload imix --steps 20 --warmup 20 --no-cpu-baseline; done ;;
     pmc) step pmc 900 bash tools/pmc.sh ;;
     prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed --no-ser
           step prof_pcap 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pcap -o run -- python3 bench.py --workload imix_pcap --steps 60 --warmup 25 --no-cpu-baseline
