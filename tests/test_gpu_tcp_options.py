@@ -65,7 +65,7 @@ def gapped(frames, rng, max_gap):
 def layouts(frames):
     rng = np.random.default_rng(836)
     out = [("packed", FrameBatch.from_packed(frames)),
-           ("packed shift 3", FrameBatch.from_packed(frames, pad_to=1, shift=3))]
+           ("packed shift 4", FrameBatch.from_packed(frames, pad_to=1, shift=4))]
     data, ot, lt = gapped(frames, rng, 3)
     out.append(("gaps 0-3 + monotone", FrameBatch(data=data, count=len(frames), offsets=ot, lengths=lt,
                                                   hints=abi.FRAMES_MONOTONE)))
