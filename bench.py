@@ -167,7 +167,7 @@ def load_traffic(workload, out_kind):
         return None
 
 
-def timed(step, steps, warmup, stream, device, host_clock=False):
+def timed(step, steps, warmup, stream, device, host_clock=False, with_local=False):
     """W untimed steps, then exactly K steps bracketed by barrier + sync on
     both sides (nex_amd.dist.timed_steps). Returns (max-over-ranks elapsed
     seconds, per-launch kernel seconds from HIP events on the launch stream)."""
@@ -181,7 +181,7 @@ def timed(step, steps, warmup, stream, device, host_clock=False):
     kernel_s = ev0.elapsed_time(ev1) / 1e3 / steps
     if host_clock:  # copies + kernels on side streams: the host clock is the measure
         kernel_s = local / steps
-    return elapsed, kernel_s
+    return (elapsed, kernel_s, local) if with_local else (elapsed, kernel_s)
 
 
 def stream_ceilings(eng, batch, args, stream, device):
@@ -228,6 +228,7 @@ def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
     elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
                               steps, max(20, args.warmup), stream, device)
     tp = dist.throughput(F, alg, steps, elapsed, device)
+    per_rank = dist.all_ranks(round(kernel_s * 1e3, 4), device)
     if rank != 0:
         return None
     ach = alg / kernel_s / 1e9
@@ -238,6 +239,8 @@ def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
          "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("imix", args.out),
                       "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg}}
+    if world > 1:
+        r["per_rank_kernel_ms"] = per_rank
     if world == 1 and not args.no_cpu_baseline:
         try:
             r["cpu_baseline"] = cpu_baseline(batch, "imix", 1 << 20, args.cpu_seconds / 2, host_threads())
@@ -411,8 +414,11 @@ def main():
         cfg["e2e_chunk_frames"] = C
 
     warm = max(args.warmup, 20) if args.workload in ("imix", "imix_pcap", "malformed") and not args.e2e else args.warmup  # see imix_line
-    elapsed, kernel_s = timed(step, args.steps, warm, stream, device, host_clock=args.e2e)
+    elapsed, kernel_s, local_s = timed(step, args.steps, warm, stream, device, host_clock=args.e2e, with_local=True)
     tp = dist.throughput(F, alg_bytes, args.steps, elapsed, device)
+    # each rank's kernel time and its own timed-region wall time (balance across GPUs)
+    per_rank = {"kernel_ms": dist.all_ranks(round(kernel_s * 1e3, 4), device),
+                "elapsed_ms_per_step": dist.all_ranks(round(local_s / args.steps * 1e3, 4), device)}
     ceilings = None
     if args.workload == "udp64" and not args.e2e and not args.no_imix:
         ceilings = stream_ceilings(eng, batch, args, stream, device)
@@ -477,6 +483,8 @@ def main():
         res["roofline"]["stream_ceilings"] = dict(
             ceilings, frac_of_read_only=round(achieved / ceilings["read_only_gbs"], 4),
             frac_of_read64_write8=round(achieved / ceilings["read64_write8_gbs"], 4))
+    if world > 1:
+        res["per_rank"] = per_rank
     if imix is not None:
         res["imix"] = imix
     if malformed is not None:

@@ -41,10 +41,12 @@ def device_index(local: int) -> int:
     return local % n if n else local
 
 
-def init(backend: str = None):
+def init(backend: str = None, force: bool = False):
+    """Create the process group for world > 1 (or at world 1 with `force`,
+    so the RCCL branches below can be exercised on a one-GPU box)."""
     import torch.distributed as dist
     rank, world, _ = env_rank_world()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
         dist.init_process_group(backend=backend or pick_backend(), rank=rank, world_size=world)
@@ -118,3 +120,17 @@ def sum_over_ranks(value: int, device=None) -> int:
                      device=device if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
+
+
+def all_ranks(value: float, device=None) -> list:
+    """Every rank's `value`, in rank order (per-rank kernel times in the
+    multi-rank bench line: the balance across GPUs)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return [value]
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]

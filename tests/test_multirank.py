@@ -79,7 +79,8 @@ def _bench_worker(rank, world, port, q):
     elapsed_max, local = dist.timed_steps(step, steps=5, warmup=2)
     frames, nbytes = 1000 + rank, 64 * (1000 + rank)
     tp = dist.throughput(frames, nbytes, 5, elapsed_max)
-    q.put((rank, len(calls), elapsed_max, local, tp))
+    per_rank = dist.all_ranks(float(10 * rank + 1))  # bench.py's per-rank kernel_ms list
+    q.put((rank, len(calls), elapsed_max, local, tp, per_rank))
     tdist.destroy_process_group()
 
 
@@ -105,3 +106,4 @@ def test_two_rank_bench_reduction():
         assert tp["total_frames"] == total and tp["total_bytes"] == 64 * total
         assert tp["value"] == round(total / emax / 1e6, 2)
         assert tp["ms_per_step"] == round(emax / 5 * 1e3, 4)
+        assert r[5] == [1.0, 11.0]  # every rank's value, in rank order
