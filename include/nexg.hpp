@@ -549,6 +549,246 @@ struct EchoPacket {  // echo_request (icmpv6.rs:2268-2294) / echo_reply (2427-24
 };
 using EchoRequestPacket = EchoPacket<128>;
 using EchoReplyPacket = EchoPacket<129>;
+
+/* Neighbor Discovery messages (icmpv6.rs ndp, 640-1901), both ways the
+ * reference builds them: try_from(Icmpv6Packet) is the TryFrom conversion
+ * dump.rs uses (fixed part read from the packet payload, options in 8-B
+ * chunks), from_bytes(message) is Packet::try_from_buf over the whole ICMPv6
+ * message (type byte first; options walked by their length field, the rest
+ * kept as payload) as the reference's ndp_tests call it. Quirks kept: RS / RA
+ * from_bytes need 24 B and panic in the reference on a length-0 option (an
+ * error here), NS / NA / Redirect stop there; TryFrom for NS asks a 24-B and
+ * for Redirect a 40-B payload although their fixed parts are 20 / 36 B. */
+namespace ndp {
+struct NdpOptionPacket {  // icmpv6.rs:776-857
+    uint8_t option_type = 0;
+    uint8_t length = 0;  // unit: 8 bytes
+    std::vector<uint8_t> payload;
+    static Result<NdpOptionPacket, const char*> from_bytes(const uint8_t* b, size_t n) {  // icmpv6.rs:784-810
+        if (n < 2) return "Malformed";
+        const size_t total = (size_t)b[1] * 8;
+        if (n < total) return "Malformed";
+        if (total < 2) return "NDP option of length 0 (the reference underflows)";
+        return NdpOptionPacket{b[0], b[1], std::vector<uint8_t>(b + 2, b + total)};
+    }
+    void append_to(std::vector<uint8_t>& out) const {  // icmpv6.rs:817-823
+        out.push_back(option_type);
+        out.push_back(length);
+        out.insert(out.end(), payload.begin(), payload.end());
+    }
+};
+namespace detail_ndp {
+inline Result<std::vector<NdpOptionPacket>, const char*> chunks(const std::vector<uint8_t>& p, size_t from) {
+    std::vector<NdpOptionPacket> out;  // TryFrom: 8-B chunks, type = chunk[0], length = chunk[1]
+    for (size_t k = from; k < p.size(); k += 8) {
+        const size_t e = k + 8 < p.size() ? k + 8 : p.size();
+        if (e - k < 2) return "NDP option chunk of 1 byte (the reference panics)";
+        out.push_back(NdpOptionPacket{p[k], p[k + 1], std::vector<uint8_t>(p.begin() + k + 2, p.begin() + e)});
+    }
+    return out;
+}
+// try_from_buf option walk from byte i; the rest becomes `rest`
+inline const char* walk(const uint8_t* b, size_t n, size_t i, bool stop_short, std::vector<NdpOptionPacket>& out,
+                        std::vector<uint8_t>& rest) {
+    while (i + 2 <= n) {
+        const size_t ol = (size_t)b[i + 1] * 8;
+        if (stop_short && ol < 2) break;
+        if (i + ol > n) break;
+        if (ol < 2) return "NDP option of length 0 (the reference panics)";
+        out.push_back(NdpOptionPacket{b[i], b[i + 1], std::vector<uint8_t>(b + i + 2, b + i + ol)});
+        i += ol;
+    }
+    rest.assign(b + i, b + n);
+    return nullptr;
+}
+inline uint32_t be32(const uint8_t* p) { return ((uint32_t)detail::be16(p) << 16) | detail::be16(p + 2); }
+inline Ipv6Addr v6(const uint8_t* p) {
+    Ipv6Addr a;
+    memcpy(a.octets.data(), p, 16);
+    return a;
+}
+inline void head(std::vector<uint8_t>& o, const Icmpv6Header& h) {
+    o.push_back(h.icmpv6_type);
+    o.push_back(h.icmpv6_code);
+    o.push_back((uint8_t)(h.checksum >> 8));
+    o.push_back((uint8_t)h.checksum);
+}
+inline void put32(std::vector<uint8_t>& o, uint32_t v) {
+    for (int k = 3; k >= 0; k--) o.push_back((uint8_t)(v >> (8 * k)));
+}
+inline Icmpv6Header hdr(const uint8_t* b) { return Icmpv6Header{b[0], b[1], detail::be16(b + 2)}; }
+}  // namespace detail_ndp
+
+struct RouterSolicitPacket {  // icmpv6.rs:872-1023
+    Icmpv6Header header;
+    uint32_t reserved = 0;
+    std::vector<NdpOptionPacket> options;
+    std::vector<uint8_t> payload;
+    static Result<RouterSolicitPacket, const char*> try_from(const Icmpv6Packet& p) {
+        if (p.header.icmpv6_type != 133) return "Not a Router Solicitation packet";
+        if (p.payload.size() < 8) return "Payload too short for Router Solicitation";
+        auto o = detail_ndp::chunks(p.payload, 4);
+        if (o.is_err()) return o.error();
+        return RouterSolicitPacket{p.header, detail_ndp::be32(p.payload.data()), o.value(), {}};
+    }
+    static Result<RouterSolicitPacket, const char*> from_bytes(const uint8_t* b, size_t n) {
+        if (n < 24) return "Malformed";  // NDP_SOL_PACKET_LEN
+        RouterSolicitPacket m{detail_ndp::hdr(b), detail_ndp::be32(b + 4), {}, {}};
+        if (const char* e = detail_ndp::walk(b, n, 8, false, m.options, m.payload)) return e;
+        return m;
+    }
+    std::vector<uint8_t> to_bytes() const {
+        std::vector<uint8_t> o;
+        detail_ndp::head(o, header);
+        detail_ndp::put32(o, reserved);
+        for (const auto& x : options) x.append_to(o);
+        return o;
+    }
+    size_t total_len() const { return 8 + 4 + payload.size(); }
+};
+
+struct RouterAdvertPacket {  // icmpv6.rs:1055-1234
+    Icmpv6Header header;
+    uint8_t hop_limit = 0, flags = 0;
+    uint16_t lifetime = 0;
+    uint32_t reachable_time = 0, retrans_time = 0;
+    std::vector<NdpOptionPacket> options;
+    std::vector<uint8_t> payload;
+    static Result<RouterAdvertPacket, const char*> try_from(const Icmpv6Packet& p) {
+        if (p.header.icmpv6_type != 134) return "Not a Router Advertisement packet";
+        if (p.payload.size() < 16) return "Payload too short for Router Advertisement";
+        auto o = detail_ndp::chunks(p.payload, 12);
+        if (o.is_err()) return o.error();
+        const uint8_t* q = p.payload.data();
+        return RouterAdvertPacket{p.header, q[0], q[1], detail::be16(q + 2), detail_ndp::be32(q + 4),
+                                  detail_ndp::be32(q + 8), o.value(), {}};
+    }
+    static Result<RouterAdvertPacket, const char*> from_bytes(const uint8_t* b, size_t n) {
+        if (n < 24) return "Malformed";  // NDP_ADV_PACKET_LEN
+        RouterAdvertPacket m{detail_ndp::hdr(b), b[4], b[5], detail::be16(b + 6), detail_ndp::be32(b + 8),
+                             detail_ndp::be32(b + 12), {}, {}};
+        if (const char* e = detail_ndp::walk(b, n, 16, false, m.options, m.payload)) return e;
+        return m;
+    }
+    std::vector<uint8_t> to_bytes() const {
+        std::vector<uint8_t> o;
+        detail_ndp::head(o, header);
+        o.push_back(hop_limit);
+        o.push_back(flags);
+        o.push_back((uint8_t)(lifetime >> 8));
+        o.push_back((uint8_t)lifetime);
+        detail_ndp::put32(o, reachable_time);
+        detail_ndp::put32(o, retrans_time);
+        for (const auto& x : options) x.append_to(o);
+        return o;
+    }
+    size_t total_len() const { return 8 + 16 + payload.size(); }
+};
+
+struct NeighborSolicitPacket {  // icmpv6.rs:1258-1434
+    Icmpv6Header header;
+    uint32_t reserved = 0;
+    Ipv6Addr target_addr;
+    std::vector<NdpOptionPacket> options;
+    std::vector<uint8_t> payload;
+    static Result<NeighborSolicitPacket, const char*> try_from(const Icmpv6Packet& p) {
+        if (p.header.icmpv6_type != 135) return "Not a Neighbor Solicitation packet";
+        if (p.payload.size() < 24) return "Payload too short for Neighbor Solicitation";
+        auto o = detail_ndp::chunks(p.payload, 20);
+        if (o.is_err()) return o.error();
+        return NeighborSolicitPacket{p.header, detail_ndp::be32(p.payload.data()), detail_ndp::v6(p.payload.data() + 4),
+                                     o.value(), {}};
+    }
+    static Result<NeighborSolicitPacket, const char*> from_bytes(const uint8_t* b, size_t n) {
+        if (n < 24) return "Malformed";
+        NeighborSolicitPacket m{detail_ndp::hdr(b), detail_ndp::be32(b + 4), detail_ndp::v6(b + 8), {}, {}};
+        if (const char* e = detail_ndp::walk(b, n, 24, true, m.options, m.payload)) return e;
+        return m;
+    }
+    std::vector<uint8_t> to_bytes() const {
+        std::vector<uint8_t> o;
+        detail_ndp::head(o, header);
+        detail_ndp::put32(o, reserved);
+        o.insert(o.end(), target_addr.octets.begin(), target_addr.octets.end());
+        for (const auto& x : options) x.append_to(o);
+        return o;
+    }
+    size_t total_len() const { return 8 + 24 + payload.size(); }
+};
+
+struct NeighborAdvertPacket {  // icmpv6.rs:1472-1664
+    Icmpv6Header header;
+    uint8_t flags = 0;
+    uint32_t reserved = 0;  // u24be
+    Ipv6Addr target_addr;
+    std::vector<NdpOptionPacket> options;
+    std::vector<uint8_t> payload;
+    static Result<NeighborAdvertPacket, const char*> try_from(const Icmpv6Packet& p) {
+        if (p.header.icmpv6_type != 136) return "Not a Neighbor Advert packet";
+        if (p.payload.size() < 20) return "Payload too short for Neighbor Advert";
+        auto o = detail_ndp::chunks(p.payload, 20);
+        if (o.is_err()) return o.error();
+        const uint8_t* q = p.payload.data();
+        return NeighborAdvertPacket{p.header, q[0], detail_ndp::be32(q) & 0xFFFFFFu, detail_ndp::v6(q + 4), o.value(), {}};
+    }
+    static Result<NeighborAdvertPacket, const char*> from_bytes(const uint8_t* b, size_t n) {
+        if (n < 24) return "Malformed";
+        NeighborAdvertPacket m{detail_ndp::hdr(b), b[4], detail_ndp::be32(b + 4) & 0xFFFFFFu, detail_ndp::v6(b + 8), {}, {}};
+        if (const char* e = detail_ndp::walk(b, n, 24, true, m.options, m.payload)) return e;
+        return m;
+    }
+    std::vector<uint8_t> to_bytes() const {
+        std::vector<uint8_t> o;
+        detail_ndp::head(o, header);
+        detail_ndp::put32(o, (uint32_t)flags << 24 | (reserved & 0xFFFFFFu));
+        o.insert(o.end(), target_addr.octets.begin(), target_addr.octets.end());
+        for (const auto& x : options) x.append_to(o);
+        return o;
+    }
+    size_t total_len() const { return 8 + 24 + payload.size(); }
+};
+
+struct RedirectPacket {  // icmpv6.rs:1696-1901
+    Icmpv6Header header;
+    uint32_t reserved = 0;
+    Ipv6Addr target_addr, dest_addr;
+    std::vector<NdpOptionPacket> options;
+    std::vector<uint8_t> payload;
+    static Result<RedirectPacket, const char*> try_from(const Icmpv6Packet& p) {
+        if (p.header.icmpv6_type != 137) return "Not a Redirect packet";
+        if (p.payload.size() < 40) return "Payload too short for Redirect";
+        auto o = detail_ndp::chunks(p.payload, 36);
+        if (o.is_err()) return o.error();
+        const uint8_t* q = p.payload.data();
+        return RedirectPacket{p.header, detail_ndp::be32(q), detail_ndp::v6(q + 4), detail_ndp::v6(q + 20), o.value(), {}};
+    }
+    static Result<RedirectPacket, const char*> from_bytes(const uint8_t* b, size_t n) {
+        if (n < 40) return "Malformed";
+        RedirectPacket m{detail_ndp::hdr(b), detail_ndp::be32(b + 4), detail_ndp::v6(b + 8), detail_ndp::v6(b + 24), {}, {}};
+        if (const char* e = detail_ndp::walk(b, n, 40, true, m.options, m.payload)) return e;
+        return m;
+    }
+    std::vector<uint8_t> to_bytes() const {
+        std::vector<uint8_t> o;
+        detail_ndp::head(o, header);
+        detail_ndp::put32(o, reserved);
+        o.insert(o.end(), target_addr.octets.begin(), target_addr.octets.end());
+        o.insert(o.end(), dest_addr.octets.begin(), dest_addr.octets.end());
+        for (const auto& x : options) x.append_to(o);
+        return o;
+    }
+    size_t total_len() const { return 8 + 40 + payload.size(); }
+};
+
+// The whole ICMPv6 message of a Frame's Icmpv6Packet (header + payload),
+// what from_bytes takes
+inline std::vector<uint8_t> message_bytes(const Icmpv6Packet& p) {
+    std::vector<uint8_t> o;
+    detail_ndp::head(o, p.header);
+    o.insert(o.end(), p.payload.begin(), p.payload.end());
+    return o;
+}
+}  // namespace ndp
 }  // namespace icmpv6
 
 /* ---- the engine --------------------------------------------------------- */

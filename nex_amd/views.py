@@ -174,16 +174,37 @@ class Icmpv6EchoPacket:  # icmpv6.rs:2268-2294 (echo_request) / 2427-2453 (echo_
 
 
 @dataclass
-class NdpOptionPacket:  # icmpv6.rs:640-760
+class NdpOptionPacket:  # icmpv6.rs:776-857
     option_type: int
-    length: int
+    length: int  # unit: 8 bytes
     payload: bytes
+
+    @classmethod
+    def from_bytes(cls, b: bytes) -> "NdpOptionPacket":
+        """Packet::try_from_buf (icmpv6.rs:784-810): >= 2 B, length * 8 B
+        present, payload = bytes[2 .. length * 8] (trailing bytes ignored)."""
+        if len(b) < 2:
+            raise ViewError("Malformed")
+        total = b[1] * 8
+        if len(b) < total:
+            raise ViewError("Malformed")
+        if total < 2:  # total_len - 2 underflows in the reference (usize)
+            raise ViewError("NDP option of length 0: the reference panics (usize underflow)")
+        return cls(b[0], b[1], bytes(b[2:total]))
+
+    def to_bytes(self) -> bytes:  # icmpv6.rs:817-823
+        return bytes([self.option_type, self.length]) + self.payload
+
+    def option_payload_length(self) -> int:  # icmpv6.rs:852-856, as written (payload.len() * 8 - 2)
+        n = len(self.payload)
+        return n * 8 - 2 if n > 0 else 0
 
 
 def _ndp_options(b: bytes) -> List[NdpOptionPacket]:
-    """icmpv6.rs:1295-1307 / 1510-1522: the bytes after the fixed part in 8-B
-    chunks (the last one possibly shorter), type = chunk[0], length = chunk[1]
-    (a 1-byte trailing chunk makes the reference index out of range)."""
+    """The TryFrom<Icmpv6Packet> option split (e.g. icmpv6.rs:1295-1307 /
+    1510-1522): the bytes after the fixed part in 8-B chunks (the last one
+    possibly shorter), type = chunk[0], length = chunk[1] (a 1-byte trailing
+    chunk makes the reference index out of range)."""
     out = []
     for k in range(0, len(b), 8):
         c = b[k:k + 8]
@@ -193,8 +214,116 @@ def _ndp_options(b: bytes) -> List[NdpOptionPacket]:
     return out
 
 
+def _ndp_options_buf(b: bytes, i: int, skip_short: bool):
+    """The Packet::try_from_buf option walk from byte i (e.g. icmpv6.rs:
+    937-957): while two bytes remain, an option of length * 8 bytes that fits
+    is taken, else the walk stops; the rest is the payload. NS / NA /
+    Redirect also stop at a length-0 option (skip_short, icmpv6.rs:1347);
+    RS / RA slice bytes[i+2 .. i] there, which panics."""
+    opts = []
+    while i + 2 <= len(b):
+        ol = b[i + 1] * 8
+        if skip_short and ol < 2:
+            break
+        if i + ol > len(b):
+            break
+        if ol < 2:
+            raise ViewError("NDP option of length 0: the reference panics (slice i+2..i)")
+        opts.append(NdpOptionPacket(b[i], b[i + 1], bytes(b[i + 2:i + ol])))
+        i += ol
+    return opts, bytes(b[i:])
+
+
+def _opts_bytes(opts: List[NdpOptionPacket]) -> bytes:
+    return b"".join(o.to_bytes() for o in opts)
+
+
+def _hdr_bytes(h: IcmpHeader) -> bytes:
+    return bytes([h.icmp_type, h.icmp_code]) + h.checksum.to_bytes(2, "big")
+
+
+def _hdr(b: bytes) -> IcmpHeader:
+    return IcmpHeader(b[0], b[1], _be16(b, 2))
+
+
 @dataclass
-class NeighborSolicitPacket:  # icmpv6.rs:1258-1315
+class RouterSolicitPacket:  # icmpv6.rs:872-1023
+    header: IcmpHeader
+    reserved: int
+    options: List[NdpOptionPacket] = field(default_factory=list)
+    payload: bytes = b""
+
+    @classmethod
+    def try_from(cls, pkt: Icmpv6Packet) -> "RouterSolicitPacket":  # icmpv6.rs:879-917
+        if pkt.header.icmp_type != 133:
+            raise ViewError("Not a Router Solicitation packet")
+        if len(pkt.payload) < 8:
+            raise ViewError("Payload too short for Router Solicitation")
+        p = pkt.payload
+        return cls(pkt.header, int.from_bytes(p[:4], "big"), _ndp_options(p[4:]))
+
+    @classmethod
+    def from_bytes(cls, b: bytes) -> "RouterSolicitPacket":  # icmpv6.rs:921-969: >= 24 B (NDP_SOL_PACKET_LEN)
+        if len(b) < 24:
+            raise ViewError("Malformed")
+        opts, rest = _ndp_options_buf(b, 8, False)
+        return cls(_hdr(b), int.from_bytes(b[4:8], "big"), opts, rest)
+
+    def to_bytes(self) -> bytes:  # icmpv6.rs:976-988
+        return _hdr_bytes(self.header) + self.reserved.to_bytes(4, "big") + _opts_bytes(self.options)
+
+    def total_len(self) -> int:  # ICMPV6_HEADER_LEN + 4 + payload, icmpv6.rs:998-1008
+        return 8 + 4 + len(self.payload)
+
+    def options_length(self) -> int:  # icmpv6.rs:1016-1022
+        n = len(self.to_bytes())
+        return n - 8 if n > 8 else 0
+
+
+@dataclass
+class RouterAdvertPacket:  # icmpv6.rs:1055-1234
+    header: IcmpHeader
+    hop_limit: int
+    flags: int
+    lifetime: int
+    reachable_time: int
+    retrans_time: int
+    options: List[NdpOptionPacket] = field(default_factory=list)
+    payload: bytes = b""
+
+    @classmethod
+    def try_from(cls, pkt: Icmpv6Packet) -> "RouterAdvertPacket":  # icmpv6.rs:1066-1117
+        if pkt.header.icmp_type != 134:
+            raise ViewError("Not a Router Advertisement packet")
+        if len(pkt.payload) < 16:
+            raise ViewError("Payload too short for Router Advertisement")
+        p = pkt.payload
+        return cls(pkt.header, p[0], p[1], _be16(p, 2), int.from_bytes(p[4:8], "big"),
+                   int.from_bytes(p[8:12], "big"), _ndp_options(p[12:]))
+
+    @classmethod
+    def from_bytes(cls, b: bytes) -> "RouterAdvertPacket":  # icmpv6.rs:1120-1177: >= 24 B (NDP_ADV_PACKET_LEN)
+        if len(b) < 24:
+            raise ViewError("Malformed")
+        opts, rest = _ndp_options_buf(b, 16, False)
+        return cls(_hdr(b), b[4], b[5], _be16(b, 6), int.from_bytes(b[8:12], "big"),
+                   int.from_bytes(b[12:16], "big"), opts, rest)
+
+    def to_bytes(self) -> bytes:  # icmpv6.rs:1185-1201
+        return (_hdr_bytes(self.header) + bytes([self.hop_limit, self.flags]) + self.lifetime.to_bytes(2, "big") +
+                self.reachable_time.to_bytes(4, "big") + self.retrans_time.to_bytes(4, "big") +
+                _opts_bytes(self.options))
+
+    def total_len(self) -> int:  # ICMPV6_HEADER_LEN + 16 + payload, icmpv6.rs:1209-1219
+        return 8 + 16 + len(self.payload)
+
+    def options_length(self) -> int:  # icmpv6.rs:1227-1233
+        n = len(self.to_bytes())
+        return n - 16 if n > 16 else 0
+
+
+@dataclass
+class NeighborSolicitPacket:  # icmpv6.rs:1258-1434
     header: IcmpHeader
     reserved: int
     target_addr: ipaddress.IPv6Address
@@ -202,21 +331,36 @@ class NeighborSolicitPacket:  # icmpv6.rs:1258-1315
     payload: bytes = b""
 
     @classmethod
-    def try_from(cls, pkt: Icmpv6Packet) -> "NeighborSolicitPacket":
+    def try_from(cls, pkt: Icmpv6Packet) -> "NeighborSolicitPacket":  # icmpv6.rs:1266-1315
         if pkt.header.icmp_type != 135:
             raise ViewError("Not a Neighbor Solicitation packet")
-        if len(pkt.payload) < 24:
+        if len(pkt.payload) < 24:  # asks 24 B though the fixed part is 20 (a 24-B message fails)
             raise ViewError("Payload too short for Neighbor Solicitation")
         p = pkt.payload
         return cls(pkt.header, int.from_bytes(p[:4], "big"), ipaddress.IPv6Address(bytes(p[4:20])),
                    _ndp_options(p[20:]))
 
+    @classmethod
+    def from_bytes(cls, b: bytes) -> "NeighborSolicitPacket":  # icmpv6.rs:1319-1377: >= 24 B
+        if len(b) < 24:
+            raise ViewError("Malformed")
+        opts, rest = _ndp_options_buf(b, 24, True)
+        return cls(_hdr(b), int.from_bytes(b[4:8], "big"), ipaddress.IPv6Address(bytes(b[8:24])), opts, rest)
+
+    def to_bytes(self) -> bytes:  # icmpv6.rs:1385-1400
+        return (_hdr_bytes(self.header) + self.reserved.to_bytes(4, "big") + self.target_addr.packed +
+                _opts_bytes(self.options))
+
     def total_len(self) -> int:  # ICMPV6_HEADER_LEN + 24 + payload (empty after try_from), icmpv6.rs:1407-1417
         return 8 + 24 + len(self.payload)
 
+    def options_length(self) -> int:  # icmpv6.rs:1426-1433
+        n = len(self.to_bytes())
+        return n - 24 if n > 24 else 0
+
 
 @dataclass
-class NeighborAdvertPacket:  # icmpv6.rs:1472-1531
+class NeighborAdvertPacket:  # icmpv6.rs:1472-1664
     header: IcmpHeader
     flags: int
     reserved: int
@@ -225,7 +369,7 @@ class NeighborAdvertPacket:  # icmpv6.rs:1472-1531
     payload: bytes = b""
 
     @classmethod
-    def try_from(cls, pkt: Icmpv6Packet) -> "NeighborAdvertPacket":
+    def try_from(cls, pkt: Icmpv6Packet) -> "NeighborAdvertPacket":  # icmpv6.rs:1481-1535
         if pkt.header.icmp_type != 136:
             raise ViewError("Not a Neighbor Advert packet")
         if len(pkt.payload) < 20:
@@ -234,8 +378,77 @@ class NeighborAdvertPacket:  # icmpv6.rs:1472-1531
         return cls(pkt.header, p[0], int.from_bytes(p[1:4], "big"), ipaddress.IPv6Address(bytes(p[4:20])),
                    _ndp_options(p[20:]))
 
+    @classmethod
+    def from_bytes(cls, b: bytes) -> "NeighborAdvertPacket":  # icmpv6.rs:1539-1603: >= 24 B
+        if len(b) < 24:
+            raise ViewError("Malformed")
+        opts, rest = _ndp_options_buf(b, 24, True)
+        return cls(_hdr(b), b[4], int.from_bytes(b[5:8], "big"), ipaddress.IPv6Address(bytes(b[8:24])), opts, rest)
+
+    def to_bytes(self) -> bytes:  # icmpv6.rs:1610-1631: flags << 24 | reserved & 0xFFFFFF
+        fr = (self.flags << 24) | (self.reserved & 0xFFFFFF)
+        return _hdr_bytes(self.header) + fr.to_bytes(4, "big") + self.target_addr.packed + _opts_bytes(self.options)
+
     def total_len(self) -> int:  # icmpv6.rs:1638-1648
         return 8 + 24 + len(self.payload)
+
+    def options_length(self) -> int:  # icmpv6.rs:1656-1663
+        n = len(self.to_bytes())
+        return n - 24 if n > 24 else 0
+
+
+@dataclass
+class RedirectPacket:  # icmpv6.rs:1696-1901
+    header: IcmpHeader
+    reserved: int
+    target_addr: ipaddress.IPv6Address
+    dest_addr: ipaddress.IPv6Address
+    options: List[NdpOptionPacket] = field(default_factory=list)
+    payload: bytes = b""
+
+    @classmethod
+    def try_from(cls, pkt: Icmpv6Packet) -> "RedirectPacket":  # icmpv6.rs:1705-1765
+        if pkt.header.icmp_type != 137:
+            raise ViewError("Not a Redirect packet")
+        if len(pkt.payload) < 40:  # asks 40 B though the fixed part is 36 (a 40-B message fails)
+            raise ViewError("Payload too short for Redirect")
+        p = pkt.payload
+        return cls(pkt.header, int.from_bytes(p[:4], "big"), ipaddress.IPv6Address(bytes(p[4:20])),
+                   ipaddress.IPv6Address(bytes(p[20:36])), _ndp_options(p[36:]))
+
+    @classmethod
+    def from_bytes(cls, b: bytes) -> "RedirectPacket":  # icmpv6.rs:1769-1843: >= 40 B
+        if len(b) < 40:
+            raise ViewError("Malformed")
+        opts, rest = _ndp_options_buf(b, 40, True)
+        return cls(_hdr(b), int.from_bytes(b[4:8], "big"), ipaddress.IPv6Address(bytes(b[8:24])),
+                   ipaddress.IPv6Address(bytes(b[24:40])), opts, rest)
+
+    def to_bytes(self) -> bytes:  # icmpv6.rs:1849-1867
+        return (_hdr_bytes(self.header) + self.reserved.to_bytes(4, "big") + self.target_addr.packed +
+                self.dest_addr.packed + _opts_bytes(self.options))
+
+    def total_len(self) -> int:  # ICMPV6_HEADER_LEN + 40 + payload, icmpv6.rs:1874-1884
+        return 8 + 40 + len(self.payload)
+
+    def options_length(self) -> int:  # icmpv6.rs:1893-1900
+        n = len(self.to_bytes())
+        return n - 40 if n > 40 else 0
+
+
+NDP_VIEWS = {133: RouterSolicitPacket, 134: RouterAdvertPacket, 135: NeighborSolicitPacket,
+             136: NeighborAdvertPacket, 137: RedirectPacket}
+
+
+def icmpv6_message_bytes(rec, frame: bytes) -> Optional[bytes]:
+    """The ICMPv6 message a GPU record located: from its L4 offset to the end
+    of the Frame's IP payload (what Packet::try_from_buf of an NDP message
+    takes, icmpv6.rs ndp); None without an ICMPv6 layer."""
+    if not int(rec["flags"]) & abi.L_ICMPV6:
+        return None
+    l4, po, pl = int(rec["l4_off"]), int(rec["payload_off"]), int(rec["payload_len"])
+    end = po + pl if pl else l4 + 4
+    return bytes(frame[l4:end])
 
 
 IcmpView = Union[EchoRequestPacket, EchoReplyPacket, DestinationUnreachablePacket, TimeExceededPacket]

@@ -238,6 +238,63 @@ for name, cite, msg, typ, code, pl, view in (
         note="Frame.payload of ICMP = bytes after the 4-B header (Q15)")
 
 
+# icmpv6.rs ndp_tests (1908-2202). The parse tests decode a bare ICMPv6
+# message with Packet::from_bytes (try_from_buf); here each message rides in
+# Eth/IPv6 (next header 58) and "view" holds the message type, the fields the
+# test asserts ("options": [type, length, payload hex] in order) and what the
+# TryFrom<Icmpv6Packet> conversion dump.rs uses gives for the same message
+# ("try_from": "same" or the reference's error string).
+NDP_RS = bytes([0x85, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00,
+                0x02, 0x01, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x01, 0x01, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00])
+NDP_RA = bytes([0x86, 0x00, 0x00, 0x00, 0xff, 0x80, 0x09, 0x00, 0x12, 0x34, 0x56, 0x78, 0x87, 0x65, 0x43, 0x21,
+                0x01, 0x01, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x05, 0x01, 0x00, 0x00, 0x57, 0x68, 0x61, 0x74])
+NDP_NS = bytes([0x87, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0xff, 0x02] + [0] * 13 + [0x01])
+NDP_NA = bytes([0x88, 0x00, 0x00, 0x00, 0x80, 0x00, 0x00, 0x00, 0xff, 0x02] + [0] * 13 + [0x01])
+NDP_REDIRECT = bytes([0x89, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0xff, 0x02] + [0] * 13 + [0x01] + [0] * 16)
+for name, cite, msg, view in (
+        ("icmpv6_ndp_router_solicit", "icmpv6.rs:1922-1956 (basic_rs_parse)", NDP_RS,
+         {"kind": "RouterSolicit", "l4_csum": 0, "reserved": 0,
+          "options": [[2, 1, "000000000000"], [1, 1, "000000000000"]], "try_from": "same"}),
+        ("icmpv6_ndp_router_advert", "icmpv6.rs:1991-2031 (basic_ra_parse)", NDP_RA,
+         {"kind": "RouterAdvert", "l4_csum": 0, "hop_limit": 0xff, "flags": 0x80, "lifetime": 0x900,
+          "reachable_time": 0x12345678, "retrans_time": 0x87654321,
+          "options": [[1, 1, "000000000000"], [5, 1, "000057686174"]], "try_from": "same"}),
+        ("icmpv6_ndp_neighbor_solicit", "icmpv6.rs:2071-2083 (basic_ns_parse)", NDP_NS,
+         {"kind": "NeighborSolicit", "l4_csum": 0, "reserved": 0, "target_addr": "ff02::1", "options": [],
+          "try_from": "Payload too short for Neighbor Solicitation"}),
+        ("icmpv6_ndp_neighbor_advert", "icmpv6.rs:2113-2126 (basic_na_parse)", NDP_NA,
+         {"kind": "NeighborAdvert", "l4_csum": 0, "reserved": 0, "flags": 0x80, "target_addr": "ff02::1",
+          "options": [], "try_from": "same"}),
+        ("icmpv6_ndp_redirect", "icmpv6.rs:2157-2171 (basic_redirect_parse)", NDP_REDIRECT,
+         {"kind": "Redirect", "l4_csum": 0, "reserved": 0, "target_addr": "ff02::1", "dest_addr": "::",
+          "options": [], "try_from": "Payload too short for Redirect"})):
+    add(name, cite, eth(ipv6_hdr(msg, 58), 0x86DD),
+        {"layers": ["eth", "ip", "ipv6", "icmpv6"], "l4_type": msg[0], "l4_code": 0, "view": view},
+        note="NDP message decoded from the GPU record's ICMPv6 bytes (from_bytes) and Icmpv6Packet (TryFrom)")
+
+# NdpOptionPacket::from_bytes (basic_option_parsing, icmpv6.rs:1908-1920) and
+# the *_create tests' to_bytes images (icmpv6.rs:1958-1989, 2033-2069,
+# 2085-2111, 2128-2155, 2173-2202)
+NDP = {
+    "option": {"cite": "icmpv6.rs:1908-1920", "bytes": "0201060504030201000000",
+               "option_type": 2, "length": 1, "payload": "060504030201"},
+    "create": [
+        {"kind": "RouterSolicit", "cite": "icmpv6.rs:1958-1989", "reserved": 0,
+         "options": [[1, 1, "000000000000"]], "bytes": "8500000000000000" "0101000000000000"},
+        {"kind": "RouterAdvert", "cite": "icmpv6.rs:2033-2069", "hop_limit": 0xff, "flags": 0x80,
+         "lifetime": 0, "reachable_time": 0, "retrans_time": 0, "options": [[5, 1, "000000000000"]],
+         "bytes": "86000000ff800000" "0000000000000000" "0501000000000000"},
+        {"kind": "NeighborSolicit", "cite": "icmpv6.rs:2085-2111", "reserved": 0, "target_addr": "ff02::1",
+         "options": [], "bytes": "8700000000000000" "ff020000000000000000000000000001"},
+        {"kind": "NeighborAdvert", "cite": "icmpv6.rs:2128-2155", "flags": 0x80, "reserved": 0,
+         "target_addr": "ff02::1", "options": [], "bytes": "8800000080000000" "ff020000000000000000000000000001"},
+        {"kind": "Redirect", "cite": "icmpv6.rs:2173-2202", "reserved": 0, "target_addr": "ff02::1",
+         "dest_addr": "::", "options": [],
+         "bytes": "8900000000000000" "ff020000000000000000000000000001" "00000000000000000000000000000000"},
+    ],
+}
+
+
 TCP_P = bytes([0xc1, 0x67, 0x23, 0x28, 0x90, 0x37, 0xd2, 0xb8, 0x94, 0x4b, 0xb2, 0x76, 0x80, 0x18,
                0x0f, 0xaf, 0xc0, 0x31, 0x00, 0x00, 0x01, 0x01, 0x08, 0x0a, 0x2c, 0x57, 0xcd, 0xa5,
                0x02, 0xa0, 0x41, 0x92]) + b"test"
@@ -327,7 +384,7 @@ BUILD_L4 = {
 
 
 def main():
-    out = {"util": UTIL, "icmpv6": ICMPV6, "frames": V, "build": BUILD, "build_l4": BUILD_L4,
+    out = {"util": UTIL, "icmpv6": ICMPV6, "frames": V, "build": BUILD, "build_l4": BUILD_L4, "ndp": NDP,
            "source": "shellrow/nex reference tests (see each 'cite')"}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_vectors.json")
     with open(path, "w") as f:

@@ -65,6 +65,8 @@ def check_expect(rec, frame: bytes, exp: dict, name="", reparse=None, parse_flag
         elif k in ("eth_dst", "eth_src"):
             e = fr.datalink.ethernet
             assert (e.destination if k == "eth_dst" else e.source).hex() == v, name
+        elif k == "view" and v["kind"] in NDP_KINDS:
+            check_ndp_view(rec, frame, v, name)
         elif k == "view":  # the ICMP / ICMPv6 sub-message the reference test downcasts to
             from nex_amd import views
             kind = v["kind"]
@@ -98,6 +100,51 @@ def check_expect(rec, frame: bytes, exp: dict, name="", reparse=None, parse_flag
             assert int(r2["ip_csum"]) == calc == int(r2["ip_csum_calc"]), name
         else:
             assert int(rec[k]) == v, (name, k, int(rec[k]), v)
+
+
+NDP_KINDS = {"RouterSolicit": 133, "RouterAdvert": 134, "NeighborSolicit": 135, "NeighborAdvert": 136,
+             "Redirect": 137}
+
+
+def ndp_fields_equal(m, v: dict, name=""):
+    """An NDP view against an expectation dict (golden "view" / "create":
+    integers, addresses as text, options as [type, length, payload hex])."""
+    for f, want in v.items():
+        if f in ("kind", "cite", "bytes", "try_from", "l4_csum"):
+            continue
+        got = getattr(m, f)
+        if f == "options":
+            got = [[o.option_type, o.length, o.payload.hex()] for o in got]
+        elif f in ("target_addr", "dest_addr"):
+            got = str(got)
+        assert got == want, (name, f, got, want)
+
+
+def check_ndp_view(rec, frame: bytes, v: dict, name=""):
+    """icmpv6.rs ndp_tests on a parsed record: the ICMPv6 message located by
+    the record decoded with Packet::from_bytes (what the tests call) and the
+    Icmpv6Packet of the Frame through TryFrom (what dump.rs calls), each
+    asserted as the reference test asserts."""
+    from nex_amd import views
+    cls = views.NDP_VIEWS[NDP_KINDS[v["kind"]]]
+    msg = views.icmpv6_message_bytes(rec, frame)
+    assert msg is not None, name
+    m = cls.from_bytes(msg)
+    assert m.header.icmp_type == NDP_KINDS[v["kind"]] and m.header.icmp_code == 0, name
+    assert m.header.checksum == v.get("l4_csum", m.header.checksum), name
+    ndp_fields_equal(m, v, name)
+    assert m.to_bytes() == msg, name  # the message re-serialises to itself
+    tf = v.get("try_from")
+    pkt = views.icmpv6_from_record(rec, frame)
+    if tf == "same":
+        ndp_fields_equal(cls.try_from(pkt), v, name)
+    elif tf is not None:
+        try:
+            cls.try_from(pkt)
+        except views.ViewError as e:
+            assert str(e) == tf, (name, str(e), tf)
+        else:
+            raise AssertionError(f"{name}: TryFrom should fail with {tf!r}")
 
 
 def records_equal(a: np.ndarray, b: np.ndarray, frames=None, what=""):

@@ -136,6 +136,71 @@ int main(int argc, char** argv) {
         CHECK(std::string(icmp::EchoReplyPacket::try_from(*icmp_packet(frame("icmp_echo_request"))).error()) ==
               "Not an Echo Reply");
     }
+    {  // icmpv6.rs ndp_tests (1922-2171): the messages decoded from the Frame's ICMPv6 packet
+        using namespace icmpv6::ndp;
+        const Ipv6Addr ff02_1{{0xff, 0x02, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1}};
+        auto msg = [&](const char* n) { return message_bytes(*icmpv6_packet(frame(n))); };
+        {  // basic_rs_parse
+            const auto m = msg("icmpv6_ndp_router_solicit");
+            const auto rs = RouterSolicitPacket::from_bytes(m.data(), m.size());
+            CHECK(rs.is_ok() && rs.value().header.icmpv6_type == 133 && rs.value().header.icmpv6_code == 0);
+            CHECK(rs.is_ok() && rs.value().header.checksum == 0 && rs.value().reserved == 0);
+            CHECK(rs.is_ok() && rs.value().options.size() == 2);
+            CHECK(rs.is_ok() && rs.value().options[0].option_type == 2 && rs.value().options[0].length == 1);
+            CHECK(rs.is_ok() && rs.value().options[0].payload == std::vector<uint8_t>(6, 0));
+            CHECK(rs.is_ok() && rs.value().options[1].option_type == 1 && rs.value().options[1].length == 1);
+            CHECK(rs.is_ok() && rs.value().to_bytes() == m);
+            const auto tf = RouterSolicitPacket::try_from(*icmpv6_packet(frame("icmpv6_ndp_router_solicit")));
+            CHECK(tf.is_ok() && tf.value().options.size() == 2 && tf.value().total_len() == 12);
+        }
+        {  // basic_ra_parse
+            const auto m = msg("icmpv6_ndp_router_advert");
+            const auto ra = RouterAdvertPacket::from_bytes(m.data(), m.size());
+            CHECK(ra.is_ok() && ra.value().header.icmpv6_type == 134 && ra.value().hop_limit == 0xff);
+            CHECK(ra.is_ok() && ra.value().flags == 0x80 && ra.value().lifetime == 0x900);
+            CHECK(ra.is_ok() && ra.value().reachable_time == 0x12345678 && ra.value().retrans_time == 0x87654321u);
+            CHECK(ra.is_ok() && ra.value().options.size() == 2 && ra.value().options[0].option_type == 1);
+            CHECK(ra.is_ok() && ra.value().options[1].option_type == 5 && ra.value().options[1].length == 1);
+            CHECK(ra.is_ok() && ra.value().options[1].payload == (std::vector<uint8_t>{0, 0, 0x57, 0x68, 0x61, 0x74}));
+            CHECK(ra.is_ok() && ra.value().to_bytes() == m);
+        }
+        {  // basic_ns_parse (TryFrom asks 24 B of payload: this 24-B message fails it)
+            const auto m = msg("icmpv6_ndp_neighbor_solicit");
+            const auto ns = NeighborSolicitPacket::from_bytes(m.data(), m.size());
+            CHECK(ns.is_ok() && ns.value().header.icmpv6_type == 135 && ns.value().reserved == 0);
+            CHECK(ns.is_ok() && ns.value().target_addr == ff02_1 && ns.value().options.empty());
+            const auto tf = NeighborSolicitPacket::try_from(*icmpv6_packet(frame("icmpv6_ndp_neighbor_solicit")));
+            CHECK(tf.is_err() && std::string(tf.error()) == "Payload too short for Neighbor Solicitation");
+        }
+        {  // basic_na_parse
+            const auto m = msg("icmpv6_ndp_neighbor_advert");
+            const auto na = NeighborAdvertPacket::from_bytes(m.data(), m.size());
+            CHECK(na.is_ok() && na.value().header.icmpv6_type == 136 && na.value().flags == 0x80);
+            CHECK(na.is_ok() && na.value().reserved == 0 && na.value().target_addr == ff02_1);
+            const auto tf = NeighborAdvertPacket::try_from(*icmpv6_packet(frame("icmpv6_ndp_neighbor_advert")));
+            CHECK(tf.is_ok() && tf.value().flags == 0x80 && tf.value().target_addr == ff02_1);
+            CHECK(tf.is_ok() && tf.value().total_len() == 32);
+        }
+        {  // basic_redirect_parse (TryFrom asks 40 B of payload: this 40-B message fails it)
+            const auto m = msg("icmpv6_ndp_redirect");
+            const auto rd = RedirectPacket::from_bytes(m.data(), m.size());
+            CHECK(rd.is_ok() && rd.value().header.icmpv6_type == 137 && rd.value().reserved == 0);
+            CHECK(rd.is_ok() && rd.value().target_addr == ff02_1 && rd.value().dest_addr == Ipv6Addr{});
+            CHECK(rd.is_ok() && rd.value().to_bytes() == m);
+            const auto tf = RedirectPacket::try_from(*icmpv6_packet(frame("icmpv6_ndp_redirect")));
+            CHECK(tf.is_err() && std::string(tf.error()) == "Payload too short for Redirect");
+        }
+        {  // basic_option_parsing (icmpv6.rs:1908-1920) and basic_na_create (2128-2155)
+            const uint8_t ob[] = {0x02, 0x01, 0x06, 0x05, 0x04, 0x03, 0x02, 0x01, 0x00, 0x00, 0x00};
+            const auto o = NdpOptionPacket::from_bytes(ob, sizeof(ob));
+            CHECK(o.is_ok() && o.value().option_type == 2 && o.value().length == 1);
+            CHECK(o.is_ok() && o.value().payload == (std::vector<uint8_t>{6, 5, 4, 3, 2, 1}));
+            NeighborAdvertPacket na{Icmpv6Header{136, 0, 0}, 0x80, 0, ff02_1, {}, {}};
+            const std::vector<uint8_t> want{0x88, 0, 0, 0, 0x80, 0, 0, 0, 0xff, 0x02, 0, 0, 0, 0, 0, 0,
+                                            0, 0, 0, 0, 0, 0, 0, 0x01};
+            CHECK(na.to_bytes() == want);
+        }
+    }
     {  // frame.rs:665-680 unknown EtherType keeps the payload
         const Frame& f = frame("unknown_ethertype_keeps_payload");
         CHECK(f.datalink && f.datalink->ethernet && f.datalink->ethernet->ethertype == 0x88b5);

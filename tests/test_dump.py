@@ -92,3 +92,46 @@ def test_dump_walks_every_frame(oracle):
     recs = oracle.parse_frames(frames)
     lines = list(views.dump_records(recs, frames, "test"))
     assert sum(1 for ln in lines if ln.startswith("---- Interface: test")) == len(frames)
+
+
+def test_ndp_option_and_create_vectors():
+    """icmpv6.rs ndp_tests on the host: NdpOptionPacket::from_bytes
+    (basic_option_parsing: trailing bytes ignored) and every *_create test's
+    to_bytes image; the images decode back to the same fields; the
+    reference's failure modes (short buffers, length-0 options)."""
+    import ipaddress
+
+    from nex_amd import views
+    from nex_amd.frame import IcmpHeader
+    g = helpers.golden()["ndp"]
+    o = g["option"]
+    opt = views.NdpOptionPacket.from_bytes(bytes.fromhex(o["bytes"]))
+    assert (opt.option_type, opt.length, opt.payload.hex()) == (o["option_type"], o["length"], o["payload"])
+    for c in g["create"]:
+        t = helpers.NDP_KINDS[c["kind"]]
+        cls = views.NDP_VIEWS[t]
+        kw = {k: v for k, v in c.items() if k not in ("kind", "cite", "bytes")}
+        kw["options"] = [views.NdpOptionPacket(a, b, bytes.fromhex(p)) for a, b, p in kw["options"]]
+        for f in ("target_addr", "dest_addr"):
+            if f in kw:
+                kw[f] = ipaddress.IPv6Address(kw[f])
+        m = cls(header=IcmpHeader(t, 0, 0), **kw)
+        assert m.to_bytes().hex() == c["bytes"], c["cite"]
+        back = cls.from_bytes(bytes.fromhex(c["bytes"])) if len(c["bytes"]) >= 48 else None
+        if back is not None:
+            helpers.ndp_fields_equal(back, c, c["cite"])
+    with pytest.raises(views.ViewError):
+        views.NdpOptionPacket.from_bytes(bytes([1]))
+    with pytest.raises(views.ViewError):  # length 1 = 8 B, only 4 present
+        views.NdpOptionPacket.from_bytes(bytes([1, 1, 0, 0]))
+    with pytest.raises(views.ViewError):  # length 0: usize underflow in the reference
+        views.NdpOptionPacket.from_bytes(bytes([1, 0]))
+    with pytest.raises(views.ViewError):
+        views.RouterSolicitPacket.from_bytes(bytes(23))
+    with pytest.raises(views.ViewError):  # RS / RA slice [i+2..i] on a length-0 option: panic
+        views.RouterSolicitPacket.from_bytes(bytes([133, 0, 0, 0, 0, 0, 0, 0]) + bytes([1, 0]) + bytes(14))
+    ns = views.NeighborSolicitPacket.from_bytes(bytes([135]) + bytes(23) + bytes([1, 0, 9, 9]))
+    assert ns.options == [] and ns.payload == bytes([1, 0, 9, 9])  # NS stops at a length-0 option
+    ra = views.RouterAdvertPacket.from_bytes(bytes([134]) + bytes(15) + bytes([5, 1]) + bytes(6) + bytes([1, 2, 3]))
+    assert [(x.option_type, x.length) for x in ra.options] == [(5, 1)] and ra.payload == bytes([1, 2, 3])
+    assert ra.options_length() == 8 and ra.total_len() == 8 + 16 + 3
