@@ -584,6 +584,48 @@ int nexg_build_tcp_batch(nexg_ctx* ctx, const nexg_tcp_build* params, uint8_t* o
 int nexg_build_icmp_echo_batch(nexg_ctx* ctx, const nexg_icmp_echo_build* params,
                                uint8_t* out, uint32_t out_stride, void* stream);
 
+/* ---- arp / ndp probes (the callers examples/arp.rs, examples/ndp.rs) -------
+ * ArpPacketBuilder::new(sender_mac, sender_ip, target_ip) (builder/arp.rs:
+ * 18-37; build() rejects hw_addr_len != 6 / proto_addr_len != 4 with
+ * InvalidFieldLength, :101-118 -> NEXG_EINVAL) serialised by ArpPacket::
+ * to_bytes (arp.rs:385-399) behind EthernetPacketBuilder (EtherType 0x0806),
+ * as examples/arp.rs:59-67 composes it. Frame = 14 + 28 = 42 bytes. */
+typedef struct nexg_arp_build {
+    const uint8_t* sender_ip;  /* 4 B per frame (network order), or NULL -> def_sender_ip */
+    const uint8_t* target_ip;  /* 4 B per frame */
+    const uint8_t* sender_mac; /* 6 B per frame, or NULL -> def_sender_mac (also the Ethernet source) */
+    const uint8_t* target_mac; /* 6 B per frame, or NULL -> def_target_mac (builder: zero) */
+    const uint8_t* eth_dst;    /* 6 B per frame, or NULL -> def_eth_dst (arp.rs: broadcast) */
+    uint8_t def_sender_ip[4];
+    uint8_t def_sender_mac[6], def_target_mac[6], def_eth_dst[6];
+    uint16_t hardware_type;    /* ArpHardwareType::Ethernet = 1 */
+    uint16_t protocol_type;    /* EtherType::Ipv4 = 0x0800 */
+    uint16_t operation;        /* ArpOperation::Request = 1 */
+    uint8_t hw_addr_len;       /* must be 6 */
+    uint8_t proto_addr_len;    /* must be 4 */
+    uint64_t count;
+} nexg_arp_build;
+int nexg_build_arp_batch(nexg_ctx* ctx, const nexg_arp_build* params, uint8_t* out,
+                         uint32_t out_stride, void* stream);
+
+/* NdpPacketBuilder::new(src_mac, src_ip, dst_ip).build() (builder/ndp.rs:
+ * 30-84): a NeighborSolicit (type 135, code 0, reserved 0, target = dst_ip,
+ * one SourceLLAddr option of length 1 carrying src_mac; icmpv6.rs:1385-1400)
+ * with icmpv6::checksum over src_ip -> dst_ip (icmpv6.rs:589-599), inside
+ * Ipv6PacketBuilder (next header 58) and EthernetPacketBuilder (0x86DD), as
+ * examples/ndp.rs:82-108 composes it (hop limit 255; Ethernet destination
+ * 33:33 + the target's last four bytes, ipv6_multicast_mac, ndp.rs:25-35).
+ * ip.family must be 6; ip.dst_ip is the target; the option's MAC is the
+ * Ethernet source. Frame = 14 + 40 + 32 = 86 bytes. */
+typedef struct nexg_ndp_ns_build {
+    nexg_ip_build ip;
+    uint32_t eth_dst_multicast; /* 1: Ethernet destination from the target (ndp.rs); 0: ip.dst_mac / def */
+    uint32_t reserved;
+    uint64_t count;
+} nexg_ndp_ns_build;
+int nexg_build_ndp_ns_batch(nexg_ctx* ctx, const nexg_ndp_ns_build* params, uint8_t* out,
+                            uint32_t out_stride, void* stream);
+
 /* ---- capture-file batch ingest ---------------------------
  * Replaces nex-datalink's pcap::from_file channel (nex-datalink/src/pcap.rs:
  * 95-109) read one frame per RawReceiver::next (pcap.rs:178-190): each call

@@ -106,7 +106,7 @@ struct ParseError {
     }
 };
 
-enum class BuildError { LengthOverflow, AddressFamilyMismatch };  // builder/error.rs:6-53
+enum class BuildError { LengthOverflow, AddressFamilyMismatch, InvalidFieldLength };  // builder/error.rs:6-53
 
 // Result<T, E>, as the reference's parse (ParseError) and build (BuildError)
 // functions return
@@ -336,6 +336,24 @@ struct IcmpPingShape {
     uint8_t ttl = 64, ip_flags = 2, tos = 0;
     uint32_t flow_label = 0;
     std::vector<uint8_t> payload;
+};
+
+// arp.rs's request (examples/arp.rs:59-67): ArpPacketBuilder::new(sender_mac,
+// sender_ip, target) behind a broadcast EthernetPacketBuilder
+struct ArpProbeShape {
+    MacAddr sender_mac{};
+    Ipv4Addr sender_ip{};
+    MacAddr eth_dst{{0xff, 0xff, 0xff, 0xff, 0xff, 0xff}};
+    uint16_t operation = 1;  // ArpOperation::Request
+    uint8_t hw_addr_len = 6, proto_addr_len = 4;  // build() accepts only 6 / 4
+};
+// ndp.rs's solicitation (examples/ndp.rs:82-108): NdpPacketBuilder::new(src_mac,
+// src_ip, target) inside Ipv6PacketBuilder (hop limit 255) and Ethernet to
+// 33:33 + the target's last four bytes
+struct NdpProbeShape {
+    MacAddr src_mac{};
+    Ipv6Addr src_ip{};
+    uint8_t hop_limit = 255;
 };
 
 /* ---- materialisation from a device record ------------------------------ */
@@ -1020,6 +1038,56 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         if (rc == NEXG_ERANGE) return BuildError::LengthOverflow;
         check(rc, "nexg_build_icmp_echo_batch");
         return download_frames(d_out, n, L);
+    }
+
+    // an ARP request for every target (nexg_build_arp_batch)
+    Result<std::vector<std::vector<uint8_t>>, BuildError> build_arp_requests(const std::vector<Ipv4Addr>& targets,
+                                                                             const ArpProbeShape& shape) {
+        DeviceScope ds(device_);
+        std::vector<std::vector<uint8_t>> frames;
+        if (shape.hw_addr_len != 6 || shape.proto_addr_len != 4) return BuildError::InvalidFieldLength;
+        if (targets.empty()) return frames;
+        const uint64_t n = targets.size();
+        std::vector<uint8_t> tip(n * 4);
+        for (uint64_t i = 0; i < n; i++) memcpy(tip.data() + 4 * i, targets[i].octets.data(), 4);
+        nexg_arp_build p{};
+        p.target_ip = static_cast<const uint8_t*>(upload(16, tip.data(), tip.size()));
+        memcpy(p.def_sender_ip, shape.sender_ip.octets.data(), 4);
+        memcpy(p.def_sender_mac, shape.sender_mac.data(), 6);
+        memcpy(p.def_eth_dst, shape.eth_dst.data(), 6);
+        p.hardware_type = 1;
+        p.protocol_type = 0x0800;
+        p.operation = shape.operation;
+        p.hw_addr_len = shape.hw_addr_len;
+        p.proto_addr_len = shape.proto_addr_len;
+        p.count = n;
+        void* d_out = scratch(15, n * 42);
+        check(nexg_build_arp_batch(ctx_, &p, static_cast<uint8_t*>(d_out), 42, stream_), "nexg_build_arp_batch");
+        return download_frames(d_out, n, 42);
+    }
+
+    // an NDP neighbor solicitation for every target (nexg_build_ndp_ns_batch)
+    std::vector<std::vector<uint8_t>> build_ndp_solicits(const std::vector<Ipv6Addr>& targets,
+                                                         const NdpProbeShape& shape) {
+        DeviceScope ds(device_);
+        if (targets.empty()) return {};
+        const uint64_t n = targets.size();
+        std::vector<uint8_t> src(n * 16), dst(n * 16);
+        for (uint64_t i = 0; i < n; i++) {
+            memcpy(src.data() + 16 * i, shape.src_ip.octets.data(), 16);
+            memcpy(dst.data() + 16 * i, targets[i].octets.data(), 16);
+        }
+        nexg_ndp_ns_build p{};
+        p.ip.src_ip = static_cast<const uint8_t*>(upload(16, src.data(), src.size()));
+        p.ip.dst_ip = static_cast<const uint8_t*>(upload(17, dst.data(), dst.size()));
+        p.ip.family = 6;
+        memcpy(p.ip.def_src_mac, shape.src_mac.data(), 6);
+        p.ip.ttl = shape.hop_limit;
+        p.eth_dst_multicast = 1;
+        p.count = n;
+        void* d_out = scratch(15, n * 86);
+        check(nexg_build_ndp_ns_batch(ctx_, &p, static_cast<uint8_t*>(d_out), 86, stream_), "nexg_build_ndp_ns_batch");
+        return download_frames(d_out, n, 86);
     }
 
     // Mutable{Ipv4,Udp,Tcp,Icmp,Icmpv6}Packet::recompute_checksum over every

@@ -50,6 +50,8 @@ def load():
         "nexg_build_udp6_batch": (I, [P, ctypes.POINTER(abi.Udp6Build), P, U32, P]),
         "nexg_build_tcp_batch": (I, [P, ctypes.POINTER(abi.TcpBuild), P, U32, P]),
         "nexg_build_icmp_echo_batch": (I, [P, ctypes.POINTER(abi.IcmpEchoBuild), P, U32, P]),
+        "nexg_build_arp_batch": (I, [P, ctypes.POINTER(abi.ArpBuild), P, U32, P]),
+        "nexg_build_ndp_ns_batch": (I, [P, ctypes.POINTER(abi.NdpNsBuild), P, U32, P]),
         "nexg_pcap_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "nexg_pcap_linktype": (I, [P]),
         "nexg_pcap_last_error": (ctypes.c_char_p, [P]),

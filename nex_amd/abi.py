@@ -272,6 +272,24 @@ class IcmpEchoBuild(ctypes.Structure):
     ]
 
 
+class ArpBuild(ctypes.Structure):
+    """struct nexg_arp_build"""
+    _fields_ = [
+        ("sender_ip", ctypes.c_void_p), ("target_ip", ctypes.c_void_p), ("sender_mac", ctypes.c_void_p),
+        ("target_mac", ctypes.c_void_p), ("eth_dst", ctypes.c_void_p),
+        ("def_sender_ip", ctypes.c_uint8 * 4), ("def_sender_mac", ctypes.c_uint8 * 6),
+        ("def_target_mac", ctypes.c_uint8 * 6), ("def_eth_dst", ctypes.c_uint8 * 6),
+        ("hardware_type", ctypes.c_uint16), ("protocol_type", ctypes.c_uint16), ("operation", ctypes.c_uint16),
+        ("hw_addr_len", ctypes.c_uint8), ("proto_addr_len", ctypes.c_uint8), ("count", ctypes.c_uint64),
+    ]
+
+
+class NdpNsBuild(ctypes.Structure):
+    """struct nexg_ndp_ns_build"""
+    _fields_ = [("ip", IpBuild), ("eth_dst_multicast", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("count", ctypes.c_uint64)]
+
+
 # in-place checksum fix-up (nexg_recompute_checksums_batch)
 FIX_IP = 0x1
 FIX_L4 = 0x2
@@ -290,6 +308,6 @@ EXPORTED_SYMBOLS = (
     "nexg_rx_config_default", "nexg_rx_open", "nexg_rx_next_batch", "nexg_rx_stats", "nexg_rx_close",
     "nexg_tpacket3_walk", "nexg_tx_open", "nexg_tx_send_batch", "nexg_tx_close",
     "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_build_tcp_batch",
-    "nexg_build_icmp_echo_batch", "nexg_pcap_open", "nexg_pcap_linktype", "nexg_pcap_last_error",
+    "nexg_build_icmp_echo_batch", "nexg_build_arp_batch", "nexg_build_ndp_ns_batch", "nexg_pcap_open", "nexg_pcap_linktype", "nexg_pcap_last_error",
     "nexg_pcap_read_batch", "nexg_pcap_read_raw", "nexg_pcap_map", "nexg_pcap_walk_mapped", "nexg_pcap_set_read_threads", "nexg_pcap_close", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
 )

@@ -328,6 +328,30 @@ int nexg_build_icmp_echo_batch(nexg_ctx* ctx, const nexg_icmp_echo_build* p, uin
                       NEXG_ELAUNCH);
 }
 
+int nexg_build_arp_batch(nexg_ctx* ctx, const nexg_arp_build* p, uint8_t* out, uint32_t out_stride,
+                         void* stream) {
+    if (!ctx || !p) return NEXG_EINVAL;
+    if (p->hw_addr_len != 6)  // builder/arp.rs:101-108 BuildError::InvalidFieldLength
+        return fail(ctx, NEXG_EINVAL, "InvalidFieldLength: ARP hardware address (expected 6)%s", nullptr);
+    if (p->proto_addr_len != 4)  // builder/arp.rs:109-115
+        return fail(ctx, NEXG_EINVAL, "InvalidFieldLength: ARP protocol address (expected 4)%s", nullptr);
+    if (p->count && (!p->target_ip || !out)) return fail(ctx, NEXG_EINVAL, "NULL target array or output%s", nullptr);
+    if (out_stride < 42u) return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    DeviceGuard g(ctx);
+    return hip_status(ctx, nexg::launch_build_arp(*p, out, out_stride, static_cast<hipStream_t>(stream)), NEXG_ELAUNCH);
+}
+
+int nexg_build_ndp_ns_batch(nexg_ctx* ctx, const nexg_ndp_ns_build* p, uint8_t* out, uint32_t out_stride,
+                            void* stream) {
+    if (!ctx || !p) return NEXG_EINVAL;
+    if (p->ip.family != 6) return fail(ctx, NEXG_EINVAL, "NDP needs IP family 6%s", nullptr);
+    if (int rc = check_ip_build(ctx, p->ip, p->count, out)) return rc;
+    if (out_stride < 86u) return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    DeviceGuard g(ctx);
+    return hip_status(ctx, nexg::launch_build_ndp_ns(*p, out, out_stride, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
 int nexg_gen_lengths(nexg_ctx* ctx, int workload, uint64_t seed, uint64_t first_index,
                      uint64_t count, uint32_t* lengths, void* stream) {
     if (!ctx) return NEXG_EINVAL;

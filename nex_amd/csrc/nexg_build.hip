@@ -461,6 +461,173 @@ hipError_t launch_build_icmp_echo(const nexg_icmp_echo_build& p, uint8_t* out, u
     return launch_l4(a, kL4Icmp, 0, s);
 }
 
+// ---- arp / ndp probes ------------------------------------------------------
+// One lane per frame: the frame's halfwords (memory order, low byte first)
+// assembled in registers, written to the LDS tile and copied out coalesced
+// like the other builders. 6-B address fields are read bytewise (any
+// alignment); IPv6 addresses as dwords (4-B aligned, nexg_ip_build).
+
+__device__ __forceinline__ uint32_t mac_hw(const uint8_t* per, const uint8_t* def, uint64_t i, int k) {
+    const uint8_t* m = per ? per + 6u * i : def;
+    return (uint32_t)m[2 * k] | ((uint32_t)m[2 * k + 1] << 8);
+}
+
+struct ArpArgs {
+    nexg_arp_build p;
+    uint8_t* out;
+    uint32_t out_stride;
+};
+
+// builder/arp.rs:18-37 + arp.rs:385-399 behind Ethernet (examples/arp.rs:59-67)
+template <uint32_t MAXS>
+__global__ __launch_bounds__(256) void k_build_arp(ArpArgs a) {
+    constexpr bool STAGED = MAXS != 0;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
+    const nexg_arp_build& p = a.p;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t first = (uint64_t)blockIdx.x * kBuildTile;
+    const uint64_t left = p.count - first;
+    const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
+    const uint64_t i = first + tid;
+    if (tid < nf) {
+        uint32_t hw[21];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            hw[k] = mac_hw(p.eth_dst, p.def_eth_dst, i, k);
+            hw[3 + k] = mac_hw(p.sender_mac, p.def_sender_mac, i, k);
+        }
+        hw[6] = 0x0608u;  // EtherType 0x0806
+        hw[7] = bswap16(p.hardware_type);
+        hw[8] = bswap16(p.protocol_type);
+        hw[9] = (uint32_t)p.hw_addr_len | ((uint32_t)p.proto_addr_len << 8);
+        hw[10] = bswap16(p.operation);
+#pragma unroll
+        for (int k = 0; k < 3; k++) hw[11 + k] = hw[3 + k];  // sender_hw_addr
+        const uint8_t* sip = p.sender_ip ? p.sender_ip + 4u * i : p.def_sender_ip;
+        const uint8_t* tip = p.target_ip + 4u * i;
+        hw[14] = (uint32_t)sip[0] | ((uint32_t)sip[1] << 8);
+        hw[15] = (uint32_t)sip[2] | ((uint32_t)sip[3] << 8);
+#pragma unroll
+        for (int k = 0; k < 3; k++) hw[16 + k] = mac_hw(p.target_mac, p.def_target_mac, i, k);
+        hw[19] = (uint32_t)tip[0] | ((uint32_t)tip[1] << 8);
+        hw[20] = (uint32_t)tip[2] | ((uint32_t)tip[3] << 8);
+        uint8_t* base = STAGED ? smem : a.out + first * a.out_stride;
+        const uint32_t d0 = tid * a.out_stride;
+        const bool odd = (a.out_stride & 1u) != 0;
+#pragma unroll
+        for (int k = 0; k < 21; k++) put_hw(base, d0 + 2u * k, hw[k], odd);
+        if (STAGED)
+            for (uint32_t k = 42; k < a.out_stride; k++) base[d0 + k] = 0;
+    }
+    if (STAGED) {
+        __syncthreads();
+        build_copy_out(smem, a.out + first * a.out_stride, nf * a.out_stride);
+    }
+}
+
+struct NdpArgs {
+    nexg_ndp_ns_build p;
+    uint8_t* out;
+    uint32_t out_stride;
+};
+
+// builder/ndp.rs:30-84 (NS + SourceLLAddr option, icmpv6::checksum) inside
+// Ipv6PacketBuilder + EthernetPacketBuilder (examples/ndp.rs:82-108)
+template <uint32_t MAXS>
+__global__ __launch_bounds__(256) void k_build_ndp_ns(NdpArgs a) {
+    constexpr bool STAGED = MAXS != 0;
+    constexpr int NH = 43;  // 86 B
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
+    const nexg_ndp_ns_build& p = a.p;
+    const nexg_ip_build& ip = p.ip;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t first = (uint64_t)blockIdx.x * kBuildTile;
+    const uint64_t left = p.count - first;
+    const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
+    const uint64_t i = first + tid;
+    if (tid < nf) {
+        uint32_t sw[4], dw[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            sw[k] = reinterpret_cast<const uint32_t*>(ip.src_ip + 16u * i)[k];
+            dw[k] = reinterpret_cast<const uint32_t*>(ip.dst_ip + 16u * i)[k];
+        }
+        uint32_t hw[NH];
+        const bool mc = p.eth_dst_multicast != 0;
+        // Ethernet: dst (33:33 + target bytes 12..15, or given), src, 0x86DD
+        hw[0] = mc ? 0x3333u : mac_hw(ip.dst_mac, ip.def_dst_mac, i, 0);
+        hw[1] = mc ? (dw[3] & 0xFFFFu) : mac_hw(ip.dst_mac, ip.def_dst_mac, i, 1);
+        hw[2] = mc ? (dw[3] >> 16) : mac_hw(ip.dst_mac, ip.def_dst_mac, i, 2);
+#pragma unroll
+        for (int k = 0; k < 3; k++) hw[3 + k] = mac_hw(ip.src_mac, ip.def_src_mac, i, k);
+        hw[6] = 0xDD86u;
+        // IPv6 header (ipv6.rs:50-75): version 6, traffic class, flow label, payload 32, next 58, hop limit
+        const uint32_t fl = ip.flow_label & 0xFFFFFu, tc = ip.tos;
+        hw[7] = ((6u << 4) | (tc >> 4)) | ((((tc & 0xFu) << 4) | (fl >> 16)) << 8);
+        hw[8] = ((fl >> 8) & 0xFFu) | ((fl & 0xFFu) << 8);
+        hw[9] = bswap16(32u);
+        hw[10] = 58u | ((uint32_t)ip.ttl << 8);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            hw[11 + 2 * k] = sw[k] & 0xFFFFu; hw[12 + 2 * k] = sw[k] >> 16;
+            hw[19 + 2 * k] = dw[k] & 0xFFFFu; hw[20 + 2 * k] = dw[k] >> 16;
+        }
+        // NeighborSolicit: type 135 code 0, checksum, reserved 0, target = dst, option 1 / len 1 / MAC
+        constexpr int L = 27;
+        hw[L + 0] = 135u;
+        hw[L + 2] = 0u; hw[L + 3] = 0u;
+#pragma unroll
+        for (int k = 0; k < 8; k++) hw[L + 4 + k] = hw[19 + k];
+        hw[L + 12] = 0x0101u;
+#pragma unroll
+        for (int k = 0; k < 3; k++) hw[L + 13 + k] = hw[3 + k];
+        // icmpv6::checksum (util.rs:91-137): pseudo-header (src, dst, length 32, next header 58)
+        // + the message with its checksum word skipped; memory-order halfwords are
+        // little-endian, x256 gives the big-endian sum (mod 0xFFFF)
+        uint32_t le = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) le += hw[11 + k];   // src + dst
+#pragma unroll
+        for (int k = 0; k < 8; k++) le += hw[L + 4 + k];  // target
+#pragma unroll
+        for (int k = 0; k < 3; k++) le += hw[L + 13 + k]; // MAC
+        const uint64_t t = 256ull * le + 58u + 32u + (135u << 8) + 0x0101u;
+        hw[L + 1] = bswap16(fold_complement(t));
+        uint8_t* base = STAGED ? smem : a.out + first * a.out_stride;
+        const uint32_t d0 = tid * a.out_stride;
+        const bool odd = (a.out_stride & 1u) != 0;
+#pragma unroll
+        for (int k = 0; k < NH; k++) put_hw(base, d0 + 2u * k, hw[k], odd);
+        if (STAGED)
+            for (uint32_t k = 86; k < a.out_stride; k++) base[d0 + k] = 0;
+    }
+    if (STAGED) {
+        __syncthreads();
+        build_copy_out(smem, a.out + first * a.out_stride, nf * a.out_stride);
+    }
+}
+
+hipError_t launch_build_arp(const nexg_arp_build& p, uint8_t* out, uint32_t out_stride, hipStream_t s) {
+    if (p.count == 0) return hipSuccess;
+    ArpArgs a{p, out, out_stride};
+    const dim3 grid((uint32_t)((p.count + kBuildTile - 1) / kBuildTile)), blk(kBuildTile);
+    const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
+    if (staged && out_stride <= 64u) hipLaunchKernelGGL(k_build_arp<64>, grid, blk, 0, s, a);
+    else if (staged) hipLaunchKernelGGL(k_build_arp<kBuildMaxStride>, grid, blk, 0, s, a);
+    else hipLaunchKernelGGL(k_build_arp<0>, grid, blk, 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_ndp_ns(const nexg_ndp_ns_build& p, uint8_t* out, uint32_t out_stride, hipStream_t s) {
+    if (p.count == 0) return hipSuccess;
+    NdpArgs a{p, out, out_stride};
+    const dim3 grid((uint32_t)((p.count + kBuildTile - 1) / kBuildTile)), blk(kBuildTile);
+    const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
+    if (staged) hipLaunchKernelGGL(k_build_ndp_ns<kBuildMaxStride>, grid, blk, 0, s, a);
+    else hipLaunchKernelGGL(k_build_ndp_ns<0>, grid, blk, 0, s, a);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------- generators
 
 __global__ void k_gen_lengths(int workload, uint64_t seed, uint64_t first, uint64_t count,

@@ -64,6 +64,9 @@ hipError_t launch_build_tcp(const nexg_tcp_build& p, uint8_t* out, uint32_t out_
 hipError_t launch_build_icmp_echo(const nexg_icmp_echo_build& p, uint8_t* out, uint32_t out_stride,
                                   hipStream_t s);
 
+hipError_t launch_build_arp(const nexg_arp_build& p, uint8_t* out, uint32_t out_stride, hipStream_t s);
+hipError_t launch_build_ndp_ns(const nexg_ndp_ns_build& p, uint8_t* out, uint32_t out_stride, hipStream_t s);
+
 hipError_t launch_gen_lengths(int workload, uint64_t seed, uint64_t first, uint64_t count,
                               uint32_t* lengths, hipStream_t s);
 hipError_t launch_gen_frames(int workload, uint64_t seed, uint64_t first, uint64_t count,

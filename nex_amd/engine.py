@@ -413,6 +413,55 @@ class Engine:
         return out
 
     # --- synthetic workloads ----------------------------------------------
+    def build_arp(self, target_ip, sender_ip=None, def_sender_ip=b"\0" * 4, sender_mac=None,
+                  def_sender_mac=b"\0" * 6, target_mac=None, def_target_mac=b"\0" * 6, eth_dst=None,
+                  def_eth_dst=b"\xff" * 6, hardware_type=1, protocol_type=0x0800, operation=1,
+                  hw_addr_len=6, proto_addr_len=4, out_stride=42, out=None, stream=None):
+        """examples/arp.rs:59-67: ArpPacketBuilder::new(sender_mac, sender_ip,
+        target_ip) (builder/arp.rs) behind EthernetPacketBuilder (broadcast
+        destination) on every target. Addresses are (count, 4) / (count, 6)
+        uint8 device tensors or None for the defaults."""
+        torch = _torch()
+        count = target_ip.shape[0]
+        if out is None:
+            out = torch.empty(max(count, 1) * out_stride, dtype=torch.uint8, device=self.torch_device)
+        p = abi.ArpBuild()
+        p.target_ip = target_ip.data_ptr()
+        p.sender_ip = None if sender_ip is None else sender_ip.data_ptr()
+        p.sender_mac = None if sender_mac is None else sender_mac.data_ptr()
+        p.target_mac = None if target_mac is None else target_mac.data_ptr()
+        p.eth_dst = None if eth_dst is None else eth_dst.data_ptr()
+        p.def_sender_ip[:] = list(def_sender_ip)
+        p.def_sender_mac[:] = list(def_sender_mac)
+        p.def_target_mac[:] = list(def_target_mac)
+        p.def_eth_dst[:] = list(def_eth_dst)
+        p.hardware_type, p.protocol_type, p.operation = hardware_type, protocol_type, operation
+        p.hw_addr_len, p.proto_addr_len = hw_addr_len, proto_addr_len
+        p.count = count
+        self._check(self.lib.nexg_build_arp_batch(self.ctx, ctypes.byref(p), _ptr(out), out_stride,
+                                                  self._stream(stream)))
+        return out
+
+    def build_ndp_ns(self, src_ip, target_ip, src_mac=b"\0" * 6, dst_mac=None, hop_limit=255, tos=0,
+                     flow_label=0, out_stride=86, out=None, stream=None):
+        """examples/ndp.rs:82-108: NdpPacketBuilder::new(src_mac, src_ip,
+        target) (builder/ndp.rs) -> Ipv6PacketBuilder (next header 58, hop
+        limit 255) -> EthernetPacketBuilder with destination 33:33 + the
+        target's last four bytes (ipv6_multicast_mac), or `dst_mac` when
+        given. Addresses are (count, 16) uint8 device tensors."""
+        torch = _torch()
+        count = target_ip.shape[0]
+        if out is None:
+            out = torch.empty(max(count, 1) * out_stride, dtype=torch.uint8, device=self.torch_device)
+        p = abi.NdpNsBuild()
+        p.ip = self._ip_build(6, src_ip, target_ip, None, 0, src_mac, dst_mac or b"\0" * 6, hop_limit, 0, tos,
+                              flow_label)
+        p.eth_dst_multicast = 1 if dst_mac is None else 0
+        p.count = count
+        self._check(self.lib.nexg_build_ndp_ns_batch(self.ctx, ctypes.byref(p), _ptr(out), out_stride,
+                                                     self._stream(stream)))
+        return out
+
     def gen_batch(self, workload: int, count: int, seed: int = abi.DEFAULT_SEED,
                   first_index: int = 0, stream=None, record_gap: int = 0) -> FrameBatch:
         """Device-generated SURVEY.md App. C workload (UDP64: fixed 64-B

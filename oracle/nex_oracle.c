@@ -1215,6 +1215,50 @@ int nexo_build_icmp_echo(const nexo_ip_spec* ip, uint8_t type, uint8_t code, uin
     return n;
 }
 
+/* ArpPacketBuilder::build (builder/arp.rs:101-118) -> ArpPacket::to_bytes
+ * (arp.rs:385-399) -> EthernetPacketBuilder (builder/ethernet.rs:63-70,
+ * EtherType Arp), examples/arp.rs:59-67. */
+int nexo_build_arp(const uint8_t eth_dst[6], const uint8_t sender_mac[6], const uint8_t sender_ip[4],
+                   const uint8_t target_mac[6], const uint8_t target_ip[4], uint16_t hardware_type,
+                   uint16_t protocol_type, uint16_t operation, uint8_t hw_len, uint8_t proto_len,
+                   uint8_t* out) {
+    if (hw_len != 6 || proto_len != 4) return -1; /* BuildError::InvalidFieldLength */
+    memcpy(out, eth_dst, 6);
+    memcpy(out + 6, sender_mac, 6); /* examples/arp.rs:60: source = the interface MAC = sender */
+    put16(out + 12, 0x0806);
+    uint8_t* a = out + 14;
+    put16(a, hardware_type);
+    put16(a + 2, protocol_type);
+    a[4] = hw_len;
+    a[5] = proto_len;
+    put16(a + 6, operation);
+    memcpy(a + 8, sender_mac, 6);
+    memcpy(a + 14, sender_ip, 4);
+    memcpy(a + 18, target_mac, 6);
+    memcpy(a + 24, target_ip, 4);
+    return 42;
+}
+
+/* NdpPacketBuilder::build (builder/ndp.rs:48-84): NeighborSolicitPacket
+ * {135, NoCode, checksum 0, reserved 0, target dst_ip, [SourceLLAddr, length
+ * octets_len(6) = 1, the 6 MAC bytes]} -> to_bytes (icmpv6.rs:1385-1400) ->
+ * Icmpv6Packet::from_bytes -> checksum = icmpv6::checksum(src, dst)
+ * (icmpv6.rs:589-599: util::ipv6_checksum over to_bytes, skipword 1); then
+ * Ipv6PacketBuilder (next header 58, hop limit from ip->ttl) and Ethernet. */
+int nexo_build_ndp_ns(const nexo_ip_spec* ip, uint8_t* out) {
+    if (ip->family != 6) return -1;
+    uint8_t m[32];
+    memset(m, 0, sizeof(m));
+    m[0] = 135;
+    m[1] = 0;
+    memcpy(m + 8, ip->dst, 16);
+    m[24] = 1;                      /* NdpOptionTypes::SourceLLAddr */
+    m[25] = (uint8_t)((6 + 7) / 8); /* octets_len(6) */
+    memcpy(m + 26, ip->src_mac, 6);
+    put16(m + 2, nexo_ipv6_checksum(m, sizeof(m), 1, NULL, 0, ip->src, ip->dst, PROTO_ICMPV6));
+    return wrap_ip_eth(ip, PROTO_ICMPV6, m, sizeof(m), out);
+}
+
 /* ======================= synthetic workloads =========================== */
 
 #define PHI 0x9E3779B97F4A7C15ULL

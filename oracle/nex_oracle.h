@@ -88,6 +88,17 @@ int nexo_build_tcp(const nexo_ip_spec* ip, uint16_t sport, uint16_t dport, uint3
 int nexo_build_icmp_echo(const nexo_ip_spec* ip, uint8_t type, uint8_t code, uint16_t ident,
                          uint16_t seqno, const uint8_t* payload, uint32_t payload_len,
                          uint8_t* out);
+/* examples/arp.rs:59-67: ArpPacketBuilder (builder/arp.rs:18-118) behind
+ * Ethernet; -1 on InvalidFieldLength (hw_len != 6 / proto_len != 4). */
+int nexo_build_arp(const uint8_t eth_dst[6], const uint8_t sender_mac[6], const uint8_t sender_ip[4],
+                   const uint8_t target_mac[6], const uint8_t target_ip[4], uint16_t hardware_type,
+                   uint16_t protocol_type, uint16_t operation, uint8_t hw_len, uint8_t proto_len,
+                   uint8_t* out);
+/* examples/ndp.rs:82-108: NdpPacketBuilder (builder/ndp.rs:30-84) inside
+ * Ipv6PacketBuilder + EthernetPacketBuilder; ip->dst is the target; the
+ * Ethernet destination is ip->dst_mac (the caller applies ndp.rs's
+ * ipv6_multicast_mac when it wants it). 86 bytes. */
+int nexo_build_ndp_ns(const nexo_ip_spec* ip, uint8_t* out);
 
 int nexo_build_udp4(const uint8_t src_mac[6], const uint8_t dst_mac[6],
                     uint32_t src_ip, uint32_t dst_ip, uint16_t sport,

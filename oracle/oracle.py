@@ -61,6 +61,10 @@ def lib():
         L.nexo_build_icmp_echo.restype = I
         L.nexo_build_icmp_echo.argtypes = [ctypes.POINTER(IpSpec), ctypes.c_uint8, ctypes.c_uint8,
                                            U16, U16, P, U32, P]
+        L.nexo_build_arp.restype = I
+        L.nexo_build_arp.argtypes = [P, P, P, P, P, U16, U16, U16, ctypes.c_uint8, ctypes.c_uint8, P]
+        L.nexo_build_ndp_ns.restype = I
+        L.nexo_build_ndp_ns.argtypes = [ctypes.POINTER(IpSpec), P]
         L.nexo_build_udp6.restype = I
         L.nexo_build_udp6.argtypes = [P, P, P, P, U16, U16, ctypes.c_uint8, ctypes.c_uint8, U32, P,
                                       U32, P]
@@ -254,6 +258,28 @@ def build_icmp_echo(spec, icmp_type, code, ident, seqno, payload=b""):
     n = lib().nexo_build_icmp_echo(ctypes.byref(spec), icmp_type, code, ident, seqno, pb, pn, out)
     if n < 0:
         raise ValueError("BuildError::LengthOverflow")
+    return out.raw[:n]
+
+
+def build_arp(eth_dst: bytes, sender_mac: bytes, sender_ip: bytes, target_mac: bytes, target_ip: bytes,
+              hardware_type=1, protocol_type=0x0800, operation=1, hw_len=6, proto_len=4):
+    """ArpPacketBuilder -> EthernetPacketBuilder (examples/arp.rs:59-67)."""
+    out = ctypes.create_string_buffer(64)
+    n = lib().nexo_build_arp(bytes(eth_dst), bytes(sender_mac), bytes(sender_ip), bytes(target_mac),
+                             bytes(target_ip), hardware_type, protocol_type, operation, hw_len, proto_len, out)
+    if n < 0:
+        raise ValueError("BuildError::InvalidFieldLength")
+    return out.raw[:n]
+
+
+def build_ndp_ns(spec):
+    """NdpPacketBuilder -> Ipv6PacketBuilder -> EthernetPacketBuilder
+    (examples/ndp.rs:82-108); spec.dst is the target, spec.dst_mac the
+    Ethernet destination."""
+    out = ctypes.create_string_buffer(128)
+    n = lib().nexo_build_ndp_ns(ctypes.byref(spec), out)
+    if n < 0:
+        raise ValueError("NDP needs IPv6")
     return out.raw[:n]
 
 

@@ -339,6 +339,42 @@ int main(int argc, char** argv) {
         auto over = eng->build_udp_ping({t}, big);
         CHECK(over.is_err() && over.error() == BuildError::LengthOverflow);
     }
+    if (gpu) {  // examples/arp.rs / examples/ndp.rs probes, bytes == the oracle's restatement
+        ArpProbeShape as;
+        as.sender_mac = MacAddr{0x02, 0x42, 0xac, 0x11, 0x00, 0x02};
+        as.sender_ip = Ipv4Addr{{192, 168, 1, 10}};
+        const auto arp = eng->build_arp_requests({Ipv4Addr{{192, 168, 1, 1}}, Ipv4Addr{{10, 0, 0, 7}}}, as);
+        CHECK(arp.is_ok() && arp.value().size() == 2 && arp.value()[1].size() == 42);
+        uint8_t want[128];
+        const uint8_t bc[6] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff}, zero6[6] = {0, 0, 0, 0, 0, 0};
+        const uint8_t tip[4] = {10, 0, 0, 7};
+        CHECK(nexo_build_arp(bc, as.sender_mac.data(), as.sender_ip.octets.data(), zero6, tip, 1, 0x0800, 1, 6, 4,
+                             want) == 42);
+        CHECK(arp.is_ok() && memcmp(arp.value()[1].data(), want, 42) == 0);
+        ArpProbeShape bad = as;
+        bad.hw_addr_len = 5;  // builder/arp.rs:101-108
+        const auto e = eng->build_arp_requests({Ipv4Addr{{1, 2, 3, 4}}}, bad);
+        CHECK(e.is_err() && e.error() == BuildError::InvalidFieldLength);
+        NdpProbeShape ns;
+        ns.src_mac = MacAddr{0x02, 0, 0, 0, 0, 0x99};
+        ns.src_ip.octets[0] = 0xfe; ns.src_ip.octets[1] = 0x80; ns.src_ip.octets[15] = 0x01;
+        Ipv6Addr tgt;
+        tgt.octets[0] = 0xfe; tgt.octets[1] = 0x80; tgt.octets[13] = 0xab; tgt.octets[14] = 0xcd; tgt.octets[15] = 0xef;
+        const auto sol = eng->build_ndp_solicits({tgt}, ns);
+        nexo_ip_spec sp{};
+        sp.family = 6;
+        memcpy(sp.src, ns.src_ip.octets.data(), 16);
+        memcpy(sp.dst, tgt.octets.data(), 16);
+        memcpy(sp.src_mac, ns.src_mac.data(), 6);
+        const uint8_t mc[6] = {0x33, 0x33, 0x00, 0xab, 0xcd, 0xef};  // ndp.rs:25-35
+        memcpy(sp.dst_mac, mc, 6);
+        sp.ttl = 255;
+        CHECK(nexo_build_ndp_ns(&sp, want) == 86);
+        CHECK(sol.size() == 1 && sol[0].size() == 86 && memcmp(sol[0].data(), want, 86) == 0);
+        const auto back = eng->try_from_buf(sol[0], ParseOption{}, ParseMode::Lenient);  // it parses and verifies
+        CHECK(back.is_ok() && back.value().ip && back.value().ip->icmpv6 && back.value().ip->icmpv6->icmpv6_type == 135);
+        CHECK(back.is_ok() && back.value().checksums.l4_ok);
+    }
     if (gpu) {  // tcp_ping / icmp_ping builds (builder/tcp.rs:175-228, examples/tcp_ping.rs:111-123,
                 // examples/icmp_ping.rs:67-80) against the oracle's builders, IPv4 and IPv6
         for (int fam : {4, 6}) {

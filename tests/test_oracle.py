@@ -466,3 +466,36 @@ def test_vlan_extension_oracle(oracle):
         if len(f) >= 14 and f[12:14] in (b"\x81\x00", b"\x88\xa8", b"\x91\x00"):
             continue
         assert oracle.parse_frame(f, abi.PARSE_VLAN).tobytes() == oracle.parse_frame(f).tobytes()
+
+
+def test_probe_builders(oracle):
+    """The arp / ndp probe builders' restatement (examples/arp.rs:59-67,
+    examples/ndp.rs:82-108): ARP request layout (arp.rs:385-399) behind a
+    broadcast Ethernet header; InvalidFieldLength for hw / proto lengths
+    (builder/arp.rs:101-118, arp_builder_rejects_non_ethernet_address_length);
+    the NS message is 32 B with a 28-B Icmpv6Packet payload (builder/ndp.rs
+    ndp_builder_produces_aligned_source_link_layer_option), its checksum an
+    independent RFC 1071 sum, and it parses (oracle) as ICMPv6 135 with the
+    checksum verifying."""
+    import pytest
+    mac = bytes([0x02, 0x42, 0xac, 0x11, 0x00, 0x02])
+    f = oracle.build_arp(b"\xff" * 6, mac, bytes([192, 168, 1, 10]), bytes(6), bytes([192, 168, 1, 1]))
+    assert f == (b"\xff" * 6 + mac + b"\x08\x06" + bytes([0, 1, 8, 0, 6, 4, 0, 1]) + mac +
+                 bytes([192, 168, 1, 10]) + bytes(6) + bytes([192, 168, 1, 1]))
+    r = oracle.parse_frame(f)
+    assert int(r["flags"]) & 0x3FF == abi.L_ETHERNET | abi.L_ARP
+    with pytest.raises(ValueError):
+        oracle.build_arp(b"\xff" * 6, mac, bytes(4), bytes(6), bytes(4), hw_len=5)
+    with pytest.raises(ValueError):
+        oracle.build_arp(b"\xff" * 6, mac, bytes(4), bytes(6), bytes(4), proto_len=6)
+    lo = bytes(15) + b"\x01"
+    sp = oracle.ip_spec(6, lo, lo, src_mac=bytes(6), dst_mac=bytes([0x33, 0x33, 0, 0, 0, 1]), ttl=255)
+    g = oracle.build_ndp_ns(sp)
+    assert len(g) == 86 and g[12:14] == b"\x86\xdd" and g[20] == 58 and g[21] == 255
+    msg = g[54:]
+    assert len(msg) - 4 == 28
+    assert msg[0] == 135 and msg[8:24] == lo and msg[24:26] == b"\x01\x01" and msg[26:32] == bytes(6)
+    pseudo = lo + lo + (32).to_bytes(4, "big") + bytes([0, 0, 0, 58])
+    assert int.from_bytes(msg[2:4], "big") == helpers.rfc1071(pseudo + msg[:2] + b"\0\0" + msg[4:])
+    r = oracle.parse_frame(g)
+    assert int(r["l4_type"]) == 135 and int(r["flags"]) & abi.C_L4_OK
