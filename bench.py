@@ -22,6 +22,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+IMIX_WARMUP = 40  # untimed launches before the 6-GB packed batches are timed (see imix_line)
 #: --out name -> nexg out_kind (include/nexg.h NEXG_OUT_*)
 OUT_KINDS = {"desc": 1, "record": 2, "flags": 4, "verdict": 5, "sparse": 6}
 OUT_NOTE = {
@@ -222,11 +223,13 @@ def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
     out = torch.empty(Engine.out_bytes(out_kind, F), dtype=torch.uint8, device=device)
     torch.cuda.synchronize(device)
     alg = batch.total_bytes
-    # a freshly generated 6-GB batch runs its first ~20 launches 5-25 % slow
-    # (profiles/r01_staging/imix_ramp.txt), so the IMIX line warms up longer
+    # the first ~30 launches of a 6-GB batch (about 30 ms of back-to-back
+    # load) run 5-25 % slow before the chip settles (profiles/r01_staging/
+    # imix_ramp.txt, profiles/r03_final/imix_ramp.txt), so the IMIX line warms
+    # up for IMIX_WARMUP untimed launches
     steps = max(1, args.steps // 2)
     elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
-                              steps, max(20, args.warmup), stream, device)
+                              steps, max(IMIX_WARMUP, args.warmup), stream, device)
     tp = dist.throughput(F, alg, steps, elapsed, device)
     per_rank = dist.all_ranks(round(kernel_s * 1e3, 4), device)
     if rank != 0:
@@ -265,7 +268,7 @@ def malformed_line(eng, args, F, first, out_kind, stream, device, rank, world):
     alg = batch.total_bytes
     steps = max(1, args.steps // 2)
     elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
-                              steps, max(20, args.warmup), stream, device)
+                              steps, max(IMIX_WARMUP, args.warmup), stream, device)
     tp = dist.throughput(n, alg, steps, elapsed, device)
     canonical = None
     if out_kind == abi.OUT_SPARSE:  # share of frames with a shape code (no exception slot)
@@ -413,7 +416,7 @@ def main():
         cfg["workload"] += "; END-TO-END: frames in pinned host memory, chunked H2D/parse/D2H"
         cfg["e2e_chunk_frames"] = C
 
-    warm = max(args.warmup, 20) if args.workload in ("imix", "imix_pcap", "malformed") and not args.e2e else args.warmup  # see imix_line
+    warm = max(args.warmup, IMIX_WARMUP) if args.workload in ("imix", "imix_pcap", "malformed") and not args.e2e else args.warmup  # see imix_line
     elapsed, kernel_s, local_s = timed(step, args.steps, warm, stream, device, host_clock=args.e2e, with_local=True)
     tp = dist.throughput(F, alg_bytes, args.steps, elapsed, device)
     # each rank's kernel time and its own timed-region wall time (balance across GPUs)
