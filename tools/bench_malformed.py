@@ -27,10 +27,14 @@ def main():
     ap.add_argument("--tiles", type=int, default=16)
     ap.add_argument("--kinds", default="")
     ap.add_argument("--libs", default="")
+    ap.add_argument("--share", type=float, default=0.5, help="share of frames mutated (kinds other than clean)")
+    ap.add_argument("--unwrap-vlan", action="store_true", help="parse with NEXG_PARSE_VLAN (ParseOption.unwrap_vlan)")
     args = ap.parse_args()
     import torch
     from nex_amd import _lib, abi, workloads
     from nex_amd.engine import Engine
+    from nex_amd.frame import ParseOption
+    opt = ParseOption(unwrap_vlan=True) if args.unwrap_vlan else ParseOption()
     engines = []
     for path in (args.libs.split(",") if args.libs else [_lib.LIB_PATH]):
         _lib._lib, _lib.LIB_PATH = None, os.path.abspath(path)
@@ -39,19 +43,19 @@ def main():
     stream = torch.cuda.current_stream()
     kinds = args.kinds.split(",") if args.kinds else ["clean"] + list(workloads.MUTATIONS) + ["all"]
     for k in kinds:
-        share = 0.0 if k == "clean" else 0.5
+        share = 0.0 if k == "clean" else args.share
         sel = workloads.MUTATIONS if k in ("clean", "all") else (k,)
         mix, counts = workloads.malformed_mix(eng, args.distinct, mutate_share=share, kinds=sel)
         b = workloads.tiled(mix, args.tiles)
         out = torch.empty(Engine.out_bytes(abi.OUT_SPARSE, b.count), dtype=torch.uint8, device="cuda")
         def timed(e):
             for _ in range(args.warmup):
-                e.parse(b, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
+                e.parse(b, opt, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             e0.record(stream)
             for _ in range(args.steps):
-                e.parse(b, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
+                e.parse(b, opt, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
             e1.record(stream)
             torch.cuda.synchronize()
             return e0.elapsed_time(e1) / 1e3 / args.steps
