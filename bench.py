@@ -85,6 +85,39 @@ def cpu_baseline(batch, workload, count, seconds, nthreads=1):
 
 
 SER_MACS = (b"\x02\0\0\0\0\1", b"\x02\0\0\0\0\2")  # udp_ping's interface MACs (synthetic)
+SER_SRC_IP = 0xC0A80164  # udp_ping's interface address (synthetic: 192.168.1.100)
+SER_PORTS = (53443, 33435)  # udp_ping.rs:30-31 SRC_PORT / DST_PORT
+
+
+def ser_probe_params(p):
+    """The udp_ping probe batch's tuples as the oracle takes them: the batch's
+    destinations, udp_ping's one source address and port pair, id 0 (the
+    Ipv4PacketBuilder default, builder/ipv4.rs:34)."""
+    import torch
+    n = p[1].numel()
+    full = lambda v, dt: torch.full((n,), v, dtype=dt)
+    return (full(SER_SRC_IP - (1 << 32), torch.int32), p[1], full(SER_PORTS[0] - (1 << 16), torch.int16),
+            full(SER_PORTS[1] - (1 << 16), torch.int16), full(0, torch.int16))
+
+
+def ser_step(eng, p, out, stream, shape):
+    """One serialize launch: `probe` = the udp_ping probe batch (a destination
+    per frame, src_ip NULL -> one source, ports / id from the batch defaults:
+    4 B of parameters read per frame); `tuples` = a full per-frame 5-tuple +
+    IPv4 id (14 B read per frame)."""
+    if shape == "probe":
+        return lambda: eng.build_udp4(None, p[1], def_src_ip=SER_SRC_IP, def_src_port=SER_PORTS[0],
+                                      def_dst_port=SER_PORTS[1], src_mac=SER_MACS[0], dst_mac=SER_MACS[1],
+                                      ip_flags=2, out=out, stream=stream)
+    return lambda: eng.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=SER_MACS[0], dst_mac=SER_MACS[1],
+                                  ip_flags=2, out=out, stream=stream)
+
+
+SER_SHAPE_NOTE = {
+    "probe": "udp_ping probe batch: a destination IPv4 per frame (4 B read), udp_ping's one source "
+             "address, SRC_PORT/DST_PORT and id 0 from the batch defaults",
+    "tuples": "a full per-frame tuple (src/dst IPv4, ports, IPv4 id: 14 B read)"}
+SER_READ = {"probe": 4, "tuples": 14}
 
 
 def cpu_baseline_ser(params, count, seconds, nthreads=1):
@@ -120,39 +153,46 @@ def write_ceiling(eng, out, args, stream, device):
 
 
 def ser_line(eng, args, F, first, stream, device, rank, world):
-    """configs[3] beside the default run: build+checksum F udp_ping-shape
-    frames (42 B) per GPU from device-resident tuples, with the write-only
-    stream ceiling of the same buffer and the oracle builder on the host."""
+    """configs[3] beside the default run: build+checksum F udp_ping frames
+    (42 B) per GPU — the probe batch (a destination per frame, as udp_ping.rs
+    builds them) with the full-tuple form nested under "tuples" — with the
+    write-only stream ceiling of the same buffer and the oracle builder on
+    the host."""
     import torch
     from nex_amd import dist
     p = eng.gen_udp4_params(F, first_index=first)
     out = torch.empty(F * 42, dtype=torch.uint8, device=device)
     torch.cuda.synchronize(device)
     alg = F * 42
-    step = lambda: eng.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=SER_MACS[0], dst_mac=SER_MACS[1],
-                                  ip_flags=2, out=out, stream=stream)
-    elapsed, kernel_s = timed(step, args.steps, args.warmup, stream, device)
-    tp = dist.throughput(F, alg, args.steps, elapsed, device)
     ceil = write_ceiling(eng, out, args, stream, device)
+    res = {}
+    for shape in ("probe", "tuples"):
+        elapsed, kernel_s = timed(ser_step(eng, p, out, stream, shape), args.steps, args.warmup, stream, device)
+        tp = dist.throughput(F, alg, args.steps, elapsed, device)
+        if rank != 0:
+            continue
+        ach = alg / kernel_s / 1e9
+        r = {"workload": f"configs[3]: build+checksum {F} udp_ping Eth/IPv4/UDP frames (42 B) per GPU, "
+                         + SER_SHAPE_NOTE[shape],
+             "value": tp["value"], "unit": "Mpkt/s", "steps": args.steps, "ms_per_step": tp["ms_per_step"],
+             "gib_s": tp["gib_s"], "bytes_per_gpu": alg,
+             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(ach / HBM_PEAK_GBS, 4),
+                          "traffic": load_traffic("ser" if shape == "tuples" else "ser_probe", "desc"),
+                          "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg,
+                          "basis": f"bytes written (SURVEY.md 8(d) SER); parameter reads ({SER_READ[shape]} "
+                                   "B/frame) not counted",
+                          "stream_ceilings": dict(ceil, frac_of_write_only=round(ach / ceil["write_only_gbs"], 4))}}
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                hp = ser_probe_params(p) if shape == "probe" else p
+                r["cpu_baseline"] = cpu_baseline_ser(hp, 1 << 20, args.cpu_seconds / 4, host_threads())
+            except Exception as e:
+                r["cpu_baseline"] = {"value": None, "error": repr(e)}
+        res[shape] = r
     if rank != 0:
         return None
-    ach = alg / kernel_s / 1e9
-    ceil["frac_of_write_only"] = round(ach / ceil["write_only_gbs"], 4)
-    r = {"workload": f"configs[3]: build+checksum {F} udp_ping-shape Eth/IPv4/UDP frames (42 B) per GPU "
-                     "from device-resident parameter tuples (src/dst IPv4, ports, IPv4 id: 14 B read)",
-         "value": tp["value"], "unit": "Mpkt/s", "steps": args.steps, "ms_per_step": tp["ms_per_step"],
-         "gib_s": tp["gib_s"], "bytes_per_gpu": alg,
-         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("ser", "desc"),
-                      "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg,
-                      "basis": "bytes written (SURVEY.md 8(d) SER); parameter reads (14 B/frame) not counted",
-                      "stream_ceilings": ceil}}
-    if world == 1 and not args.no_cpu_baseline:
-        try:
-            r["cpu_baseline"] = cpu_baseline_ser(p, 1 << 20, args.cpu_seconds / 2, host_threads())
-        except Exception as e:
-            r["cpu_baseline"] = {"value": None, "error": repr(e)}
-    return r
+    return dict(res["probe"], tuples=res["tuples"])
 
 
 def load_traffic(workload, out_kind):
@@ -302,6 +342,8 @@ def main():
                     help="skip the malformed-mix line (fallback cost) reported beside the default run")
     ap.add_argument("--no-ser", action="store_true",
                     help="skip the configs[3] serialize line reported beside the default run")
+    ap.add_argument("--ser-shape", choices=["probe", "tuples"], default="probe",
+                    help="--workload ser: udp_ping probe batch (a destination per frame) or full tuples")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true",
@@ -365,11 +407,9 @@ def main():
         alg_bytes = F * 42
         batch = None
 
-        def step():
-            eng.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=SER_MACS[0], dst_mac=SER_MACS[1],
-                           ip_flags=2, out=out, stream=stream)
-        cfg = {"workload": f"configs[3]: build+checksum {F} udp_ping-shape Eth/IPv4/UDP frames "
-                           "(42 B) per GPU from device-resident parameter tuples"}
+        step = ser_step(eng, p, out, stream, args.ser_shape)
+        cfg = {"workload": f"configs[3]: build+checksum {F} udp_ping Eth/IPv4/UDP frames (42 B) per GPU, "
+                           + SER_SHAPE_NOTE[args.ser_shape]}
 
     cfg.update({"frames_per_gpu": F, "bytes_per_gpu": alg_bytes, "output": args.out,
                 "parallelism": f"{world} ranks x index-range shards, no collective",
@@ -463,12 +503,15 @@ def main():
                      "algorithmic_bytes_per_launch": alg_bytes},
     }
     if args.workload == "ser":
-        res["roofline"]["basis"] = "bytes written (SURVEY.md 8(d) SER); parameter reads (14 B/frame) not counted"
-        res["roofline"]["traffic"] = load_traffic("ser", "desc")  # the build has no output kind; tools/pmc.sh records it as ser.desc
+        res["roofline"]["basis"] = (f"bytes written (SURVEY.md 8(d) SER); parameter reads "
+                                    f"({SER_READ[args.ser_shape]} B/frame) not counted")
+        # the build has no output kind; tools/pmc.sh records it as ser.desc / ser_probe.desc
+        res["roofline"]["traffic"] = load_traffic("ser" if args.ser_shape == "tuples" else "ser_probe", "desc")
         if world == 1 and not args.no_cpu_baseline:
             try:
-                res["cpu_baseline"] = cpu_baseline_ser(p, 1 << 20, args.cpu_seconds / 2, host_threads())
-                res["cpu_baseline"]["single_thread"] = cpu_baseline_ser(p, 1 << 20, args.cpu_seconds / 2, 1)
+                hp = ser_probe_params(p) if args.ser_shape == "probe" else p
+                res["cpu_baseline"] = cpu_baseline_ser(hp, 1 << 20, args.cpu_seconds / 2, host_threads())
+                res["cpu_baseline"]["single_thread"] = cpu_baseline_ser(hp, 1 << 20, args.cpu_seconds / 2, 1)
             except Exception as e:
                 res["cpu_baseline"] = {"value": None, "error": repr(e)}
     if world == 1 and not args.no_cpu_baseline and batch is not None:

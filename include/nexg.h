@@ -468,7 +468,8 @@ int nexg_probe_stream(nexg_ctx* ctx, const void* data, uint64_t bytes, uint32_t 
 
 /* ---- serialize path (udp_ping.rs:68-109 shape) -------------------------- */
 typedef struct nexg_udp4_build {
-    const uint32_t* src_ip;   /* per frame, IPv4 address as BE u32 value     */
+    const uint32_t* src_ip;   /* per frame, IPv4 address as BE u32 value, or
+                                 NULL -> def_src_ip (udp_ping: one source)   */
     const uint32_t* dst_ip;   /* per frame                                    */
     const uint16_t* src_port; /* per frame, or NULL -> def_src_port           */
     const uint16_t* dst_port; /* per frame, or NULL -> def_dst_port           */
@@ -483,6 +484,8 @@ typedef struct nexg_udp4_build {
     uint8_t ip_flags; /* 3-bit flags; udp_ping uses DontFragment = 0b010     */
     uint8_t dscp_ecn; /* dscp<<2|ecn, builder default 0                      */
     uint8_t reserved;
+    uint32_t def_src_ip; /* source when src_ip is NULL (BE u32 value); sits in
+                            what was padding, so the struct is unchanged in size */
     uint64_t count;
 } nexg_udp4_build;
 

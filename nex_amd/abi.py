@@ -208,6 +208,7 @@ class Udp4Build(ctypes.Structure):
         ("ip_flags", ctypes.c_uint8),
         ("dscp_ecn", ctypes.c_uint8),
         ("reserved", ctypes.c_uint8),
+        ("def_src_ip", ctypes.c_uint32),
         ("count", ctypes.c_uint64),
     ]
 

@@ -259,7 +259,7 @@ int nexg_build_udp4_batch(nexg_ctx* ctx, const nexg_udp4_build* p, uint8_t* out,
     if (!ctx || !p) return NEXG_EINVAL;
     if (28ull + p->payload_len > 65535ull)
         return fail(ctx, NEXG_ERANGE, "UDP/IPv4 length overflow%s", nullptr);
-    if (p->count && (!p->src_ip || !p->dst_ip || !out))
+    if (p->count && (!p->dst_ip || !out))
         return fail(ctx, NEXG_EINVAL, "NULL address array or output%s", nullptr);
     if (p->payload_len && !p->payload) return fail(ctx, NEXG_EINVAL, "NULL payload%s", nullptr);
     if (out_stride < 42u + p->payload_len)
@@ -274,7 +274,7 @@ int nexg_build_udp6_batch(nexg_ctx* ctx, const nexg_udp6_build* p, uint8_t* out,
     if (!ctx || !p) return NEXG_EINVAL;
     if (8ull + p->payload_len > 65535ull)
         return fail(ctx, NEXG_ERANGE, "UDP/IPv6 length overflow%s", nullptr);
-    if (p->count && (!p->src_ip || !p->dst_ip || !out))
+    if (p->count && (!p->dst_ip || !out))
         return fail(ctx, NEXG_EINVAL, "NULL address array or output%s", nullptr);
     if (((reinterpret_cast<uint64_t>(p->src_ip) | reinterpret_cast<uint64_t>(p->dst_ip)) & 3u) != 0)
         return fail(ctx, NEXG_EINVAL, "address arrays must be 4-B aligned%s", nullptr);

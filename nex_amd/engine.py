@@ -282,18 +282,22 @@ class Engine:
     def build_udp4(self, src_ip, dst_ip, src_port=None, dst_port=None, ip_id=None,
                    def_src_port=0, def_dst_port=0, def_ip_id=0,
                    src_mac=b"\0" * 6, dst_mac=b"\0" * 6, ttl=64, ip_flags=0, dscp_ecn=0,
-                   payload=None, out_stride=None, out=None, stream=None):
+                   payload=None, out_stride=None, out=None, stream=None, def_src_ip=0):
         """UdpPacketBuilder -> Ipv4PacketBuilder -> EthernetPacketBuilder
         (udp_ping.rs:68-109) on every tuple. Tensors are int32/int16 device
-        tensors holding the u32/u16 values."""
+        tensors holding the u32/u16 values; src_ip=None takes def_src_ip (a
+        u32 value) for every frame — with no other array, the udp_ping probe
+        batch: one source, one port pair, a destination per frame."""
         torch = _torch()
-        count = src_ip.numel()
+        count = dst_ip.numel()
         plen = 0 if payload is None else payload.numel()
         stride = out_stride or (42 + plen)
         if out is None:
             out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
         p = abi.Udp4Build()
-        p.src_ip, p.dst_ip = src_ip.data_ptr(), dst_ip.data_ptr()
+        p.src_ip = None if src_ip is None else src_ip.data_ptr()
+        p.dst_ip = dst_ip.data_ptr()
+        p.def_src_ip = def_src_ip & 0xFFFFFFFF
         p.src_port = None if src_port is None else src_port.data_ptr()
         p.dst_port = None if dst_port is None else dst_port.data_ptr()
         p.ip_id = None if ip_id is None else ip_id.data_ptr()
@@ -322,7 +326,9 @@ class Engine:
         if out is None:
             out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
         p = abi.Udp6Build()
-        p.src_ip, p.dst_ip = src_ip.data_ptr(), dst_ip.data_ptr()
+        p.src_ip = None if src_ip is None else src_ip.data_ptr()
+        p.dst_ip = dst_ip.data_ptr()
+        p.def_src_ip = def_src_ip & 0xFFFFFFFF
         p.src_port = None if src_port is None else src_port.data_ptr()
         p.dst_port = None if dst_port is None else dst_port.data_ptr()
         p.src_mac = p.dst_mac = None

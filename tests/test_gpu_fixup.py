@@ -196,15 +196,26 @@ def test_fixup_full_size_imix(engine, oracle):
             d1.cpu().numpy().view(abi.DESC_DTYPE)["payload_off"]).all()
 
 
-def test_ser_full_size_verifies(engine, oracle):
-    """configs[3] at its full size (16M udp_ping frames): every built frame
-    verifies through the GPU parse path, and a 65536-frame random sample is
-    byte-identical to the oracle's builder."""
+@pytest.mark.parametrize("shape", ["tuples", "probe"])
+def test_ser_full_size_verifies(engine, oracle, shape):
+    """configs[3] at its full size (16M udp_ping frames), in both bench forms
+    (a full tuple per frame; the udp_ping probe batch: a destination per
+    frame, one source and port pair): every built frame verifies through the
+    GPU parse path, and a 65536-frame random sample is byte-identical to the
+    oracle's builder."""
     import torch
     n = 16 << 20
     p = engine.gen_udp4_params(n)
     smac, dmac = b"\x02\0\0\0\0\1", b"\x02\0\0\0\0\2"
-    out = engine.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=smac, dst_mac=dmac, ip_flags=2)
+    if shape == "probe":
+        src, sport, dport = 0xC0A80164, 53443, 33435
+        out = engine.build_udp4(None, p[1], def_src_ip=src, def_src_port=sport, def_dst_port=dport,
+                                src_mac=smac, dst_mac=dmac, ip_flags=2)
+        p = [torch.full((n,), src - (1 << 32), dtype=torch.int32), p[1],
+             torch.full((n,), sport - (1 << 16), dtype=torch.int16),
+             torch.full((n,), dport - (1 << 16), dtype=torch.int16), torch.zeros(n, dtype=torch.int16)]
+    else:
+        out = engine.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=smac, dst_mac=dmac, ip_flags=2)
     sp = engine.parse(FrameBatch(data=out, count=n, stride=42), out_kind=abi.OUT_SPARSE)
     torch.cuda.synchronize()
     codes = sp[:n].cpu().numpy()

@@ -397,6 +397,17 @@ def test_build_udp4_default_fields(engine, oracle):
             want = oracle.build_udp4(smac, dmac, int(host[0][i]) & 0xFFFFFFFF, int(host[1][i]) & 0xFFFFFFFF,
                                      sp, dp, ident, 64, 2, 0, b"")
             assert bytes(data[i]) == want, (sorted(kw), i)
+    # the udp_ping probe batch (src_ip NULL: one source, ports and id from the
+    # defaults, a destination per frame), at the full-tile and a ragged count
+    for m in (n, 257):
+        out = engine.build_udp4(None, p[1][:m], def_src_ip=0xC0A80164, def_src_port=53443, def_dst_port=33435,
+                                src_mac=smac, dst_mac=dmac, ttl=64, ip_flags=2)
+        torch.cuda.synchronize()
+        data = out.cpu().numpy()[: m * 42].reshape(m, 42)
+        for i in list(range(0, m, 29)) + [m - 1]:
+            want = oracle.build_udp4(smac, dmac, 0xC0A80164, int(host[1][i]) & 0xFFFFFFFF,
+                                     53443, 33435, 0, 64, 2, 0, b"")
+            assert bytes(data[i]) == want, ("probe", m, i)
 
 
 def test_probe_stream(engine):

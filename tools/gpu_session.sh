@@ -23,7 +23,8 @@ for s in ${STEPS:-tests}; do
     bench) step bench_udp64 500 python bench.py --steps 50 --cpu-seconds 5 ;;
     malformed) step bench_malformed 500 python tools/bench_malformed.py ;;
     benchpcap) step bench_pcap 400 python bench.py --workload imix_pcap --steps 20 --cpu-seconds 5 ;;
-    ser) step bench_ser 300 python bench.py --workload ser --steps 50 --no-cpu-baseline ;;
+    ser) step bench_ser 300 python bench.py --workload ser --steps 50 --no-cpu-baseline
+         step bench_ser_tuples 300 python bench.py --workload ser --ser-shape tuples --steps 50 --no-cpu-baseline ;;
     e2e) step bench_e2e 400 python bench.py --e2e --steps 5 --warmup 2 --no-cpu-baseline
          step bench_e2e_imix 400 python bench.py --e2e --workload imix --steps 3 --warmup 1 --no-cpu-baseline ;;
     rehearse2) step rehearse2 600 env NEXG_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 2 ;;
@@ -34,7 +35,8 @@ for s in ${STEPS:-tests}; do
           step prof_pcap 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pcap -o run -- python3 bench.py --workload imix_pcap --steps 60 --warmup 25 --no-cpu-baseline
           step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 60 --warmup 25 --no-cpu-baseline
           step prof_malformed 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_malformed -o run -- python3 bench.py --workload malformed --steps 60 --warmup 25 --no-cpu-baseline
-          step prof_ser 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser -o run -- python3 bench.py --workload ser --steps 60 --warmup 25 --no-cpu-baseline ;;
+          step prof_ser 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser -o run -- python3 bench.py --workload ser --steps 60 --warmup 25 --no-cpu-baseline
+          step prof_ser_tuples 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser_tuples -o run -- python3 bench.py --workload ser --ser-shape tuples --steps 60 --warmup 25 --no-cpu-baseline ;;
   esac
 done
 echo done
