@@ -60,7 +60,17 @@ def main():
             torch.cuda.synchronize()
             return e0.elapsed_time(e1) / 1e3 / args.steps
         rounds = 2 if len(engines) > 1 else 1
-        times = [[timed(e) for e in engines] for _ in range(rounds)]
+        times, same = [], []
+        for _ in range(rounds):
+            row = []
+            for j, e in enumerate(engines):
+                row.append(timed(e))
+                if len(engines) > 1:  # every build's output equals the first build's, byte for byte
+                    if j == 0:
+                        ref = out.clone()
+                    else:
+                        same.append(bool(torch.equal(out, ref)))
+            times.append(row)
         s = min(t[0] for t in times)
         exc = float((out[: b.count] == 0).float().mean().item())
         line = {"kind": k, "frames": b.count, "bytes": b.total_bytes, "kernel_ms": round(s * 1e3, 4),
@@ -68,6 +78,7 @@ def main():
                 "exception_share": round(exc, 4), "mutated": counts.get(k, None)}
         if len(engines) > 1:
             line["kernel_ms_by_lib"] = [[round(x * 1e3, 4) for x in t] for t in times]
+            line["outputs_equal"] = all(same)
         print(json.dumps(line), flush=True)
         del b, mix, out
         torch.cuda.empty_cache()
