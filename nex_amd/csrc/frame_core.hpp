@@ -223,6 +223,9 @@ NEXG_HD uint32_t span_tail_end(uint32_t b12, uint32_t b16, uint32_t len, uint32_
     return (e >= 84u && e < len) ? e : len;
 }
 
+#ifndef NEXG_SPAN_PROBE
+#define NEXG_SPAN_PROBE(k, c)
+#endif
 struct SpanFrame {
     static constexpr uint32_t kSlot = 80;
     static constexpr uint32_t kDefer = 64;
@@ -236,6 +239,7 @@ struct SpanFrame {
 
     // one generic (flat) byte load from the slot or HBM: no divergent branch
     NEXG_HD uint32_t u8(uint32_t i) const {
+        NEXG_SPAN_PROBE(0, i >= kSlot);  // host harness counters (no-op in the library)
         const uint8_t* p = i < kSlot ? slot + i : g + i;
         return *p;
     }
@@ -257,6 +261,7 @@ struct SpanFrame {
                 d.rng = ga | (gb - ga) << 16;
                 pend = true;
             } else {
+                NEXG_SPAN_PROBE(1, true);
                 acc += global_le_sum(base + ga, base + gb);
             }
         }

@@ -35,6 +35,16 @@ def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share
     torch.cuda.synchronize(engine.torch_device)
     offs = base.offsets.cpu().numpy().astype(np.int64)
     data = base.data.cpu().numpy()[: offs[-1]]
+    out, new_offs, counts = mutate_packed(data, offs, seed, mutate_share, kinds)
+    dev = torch.from_numpy(np.concatenate([out, np.zeros(16, np.uint8)])).to(engine.torch_device)
+    doffs = torch.from_numpy(new_offs).to(engine.torch_device)
+    return FrameBatch(data=dev[: int(new_offs[-1])], count=count, offsets=doffs), counts
+
+
+def mutate_packed(data, offs, seed: int = abi.DEFAULT_SEED, mutate_share: float = 0.5, kinds=MUTATIONS):
+    """The mutations of malformed_mix on a host packed batch (bytes, count+1
+    offsets): (mutated bytes, new offsets, dict of per-mutation counts)."""
+    count = len(offs) - 1
     lens = np.diff(offs)
     rng = np.random.default_rng(seed)
     pick = np.array([_ALL.index(k) for k in kinds])
@@ -118,11 +128,9 @@ def malformed_mix(engine, count: int, seed: int = abi.DEFAULT_SEED, mutate_share
             g[18], g[19] = pl >> 8, pl & 0xFF
             f = np.concatenate([g[:54], np.array([nh, 0, 0, 0, 0, 0, 0, 0], np.uint8), g[54:]])
         out[new_offs[j]:new_offs[j] + len(f)] = f
-    dev = torch.from_numpy(np.concatenate([out, np.zeros(16, np.uint8)])).to(engine.torch_device)
-    doffs = torch.from_numpy(new_offs).to(engine.torch_device)
     counts = {m: int((kind == k).sum()) for k, m in enumerate(_ALL) if m in kinds}
     counts["unmodified"] = int((kind < 0).sum())
-    return FrameBatch(data=dev[: int(new_offs[-1])], count=count, offsets=doffs), counts
+    return out, new_offs, counts
 
 
 def _ramp(lengths):

@@ -496,3 +496,15 @@ def tcp_option_sweep(oracle, rng, bases):
             if j == 1:
                 out.append(bytes(g[: l4 + 20 + int(rng.integers(0, len(opts)))]))
     return out
+
+
+def host_malformed_mix(oracle, count, seed=77, mutate_share=0.5, kinds=None):
+    """The bench's malformed mix built on the host: IMIX frames from the
+    oracle's generator (the device generator's restatement), mutated by
+    nex_amd.workloads.mutate_packed. (bytes, count+1 offsets, counts)."""
+    from nex_amd import abi, workloads
+    frames = [oracle.gen_frame(abi.WL_IMIX, i, seed=seed) for i in range(count)]
+    offs = np.zeros(count + 1, np.int64)
+    np.cumsum([len(f) for f in frames], out=offs[1:])
+    data = np.frombuffer(b"".join(bytes(f) for f in frames), np.uint8)
+    return workloads.mutate_packed(data, offs, seed, mutate_share, kinds or workloads.MUTATIONS)

@@ -5,6 +5,9 @@
 // against the oracle run without a GPU. Not part of the product library.
 #include <string.h>
 
+// SpanFrame's HBM touches past its LDS bytes, counted by harness_span_groups
+static unsigned long long g_span_probe[2];
+#define NEXG_SPAN_PROBE(k, c) (g_span_probe[k] += (c) ? 1u : 0u)
 #include "../../nex_amd/csrc/parse_kernels.hpp"
 
 extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uint64_t* offsets,
@@ -145,5 +148,84 @@ extern "C" int harness_sparse_decode(const uint8_t* codes, const uint32_t* lens,
         dev_desc[i] = d;
         hdr_desc[i] = h;
     }
+    return 0;
+}
+
+// k_parse_span's generic section for packed batches, group by group, on the
+// host: the workgroup's LDS slots emulated by one 20480-B heap block (so an
+// AddressSanitizer build catches any slot access outside it), the fast path on
+// every frame's head window with the scanned tail sum, declined frames
+// bucketed in lane order, the generic core on SpanFrame, deferred ranges
+// patched; harness_span_stats counts what the generic section does.
+// Records out (the record form of what the sparse kernel encodes). Frames of a
+// group that is not packed (or a batch that is not) return -1.
+static uint64_t g_span_stats[6];  // declined, declined past 80 B, deferred ranges, groups with a declined
+                                  // frame, HBM byte loads, inline HBM range sums (the last two: NEXG_SPAN_PROBE)
+extern "C" const uint64_t* harness_span_stats() {
+    g_span_stats[4] = g_span_probe[0];
+    g_span_stats[5] = g_span_probe[1];
+    return g_span_stats;
+}
+extern "C" void harness_span_stats_reset() {
+    for (auto& v : g_span_stats) v = 0;
+    g_span_probe[0] = g_span_probe[1] = 0;
+}
+extern "C" int harness_span_groups(const uint8_t* data, uint64_t data_bytes, const uint64_t* offsets,
+                                   uint64_t count, uint32_t flags, uint32_t ip_offset, nexg_record* out) {
+    constexpr uint32_t T = nexg::kTile, S = nexg::SpanFrame::kSlot, W = nexg::kLaneWin;
+    uint8_t* lds = static_cast<uint8_t*>(aligned_alloc(16, T * S));
+    const uint64_t base = reinterpret_cast<uint64_t>(data);
+    for (uint64_t f0 = 0; f0 < count; f0 += T) {
+        const uint32_t nf = count - f0 < T ? (uint32_t)(count - f0) : T;
+        const uint64_t lo = offsets[f0], hi = offsets[f0 + nf];
+        if (hi < lo || hi > data_bytes) { free(lds); return -1; }
+        const uint64_t A0 = (base + lo) & ~15ull;
+        memset(lds, 0xA5, T * S);
+        bool gen[T] = {};
+        uint32_t key[T] = {}, hr[T] = {}, len[T] = {}, qend[T] = {}, tq[T] = {};
+        for (uint32_t t = 0; t < nf; t++) {
+            const uint64_t off = offsets[f0 + t], l = offsets[f0 + t + 1] - off;
+            if (l > 65535 || off < lo || off + l > hi) { free(lds); return -1; }
+            len[t] = (uint32_t)l;
+            hr[t] = (uint32_t)(base + off - A0);
+            const uint8_t* g = data + off;
+            uint32_t w[20] = {0};
+            memcpy(w, g, l < W ? l : W);
+            qend[t] = nexg::span_tail_end(w[3], w[4], len[t], flags);
+            uint32_t q = 0;  // absolute-parity LE sum of [80, qend): Q(end) - Q(start + 80)
+            for (uint32_t k = W; k < qend[t]; k++) q += (uint32_t)g[k] << (((base + off + k) & 1u) ? 8u : 0u);
+            tq[t] = len[t] > W ? q : 0u;
+            nexg_record r{};
+            const uint64_t tail = ((base + off) & 1u) ? (uint64_t)tq[t] * 256u : (uint64_t)tq[t];
+            if (nexg::fast_canonical80(w, len[t], flags, tail, qend[t], r)) {
+                out[f0 + t] = r;
+            } else {
+                gen[t] = true;
+                key[t] = nexg::span_bucket(w[3], w[5], flags);
+                memcpy(lds + S * t, w, S);
+            }
+        }
+        // items in bucket order (lane order inside a bucket)
+        uint32_t ngen = 0, items[T];
+        for (uint32_t b = 0; b < nexg::kBuckets; b++)
+            for (uint32_t t = 0; t < nf; t++)
+                if (gen[t] && key[t] == b) items[ngen++] = t;
+        g_span_stats[3] += ngen > 0;
+        for (uint32_t ii = 0; ii < ngen; ii++) {
+            const uint32_t t = items[ii];
+            nexg_record rr{};
+            nexg::SpanFrame f{lds + S * t, reinterpret_cast<const uint8_t*>(A0 + hr[t]), qend[t], hr[t] & 1u, tq[t]};
+            nexg::parse_frame(f, hr[t] & 1u, len[t], flags, ip_offset, rr);
+            g_span_stats[0]++;
+            g_span_stats[1] += len[t] > W;
+            g_span_stats[2] += f.d.which() != 0;
+            if (f.d.which()) {
+                const uint64_t A = A0 + hr[t] + f.d.off();
+                nexg::span_patch(f.d, nexg::global_le_sum(A, A + f.d.bytes()), rr);
+            }
+            out[f0 + t] = rr;
+        }
+    }
+    free(lds);
     return 0;
 }

@@ -26,6 +26,8 @@ def lib():
         L.harness_sparse_decode.argtypes = [P, P, U64, U32, U32, P, P]
         L.harness_slice.restype = ctypes.c_int
         L.harness_slice.argtypes = [P, U64, P, P, U32, U64, U32, U32, U32, P]
+        L.harness_span_groups.restype = ctypes.c_int
+        L.harness_span_groups.argtypes = [P, U64, P, U64, U32, U32, P]
         _lib = L
     return _lib
 
@@ -87,3 +89,16 @@ def sparse_decode(codes, lens, flags=0, ip_offset=0):
     assert lib().harness_sparse_decode(codes.ctypes.data, lens.ctypes.data, n, flags, ip_offset,
                                        dd.ctypes.data, hd.ctypes.data) == 0
     return dd[:n], hd[:n]
+
+
+def span_groups(data, offsets, flags=0, ip_offset=0):
+    """k_parse_span's fast path + generic section (slots, free-slot extension
+    windows, bucketed items) emulated group by group over a packed batch."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    count = len(offs) - 1
+    recs = np.zeros(count, dtype=abi.RECORD_DTYPE)
+    rc = lib().harness_span_groups(data.ctypes.data, data.nbytes, offs.ctypes.data, count, flags, ip_offset,
+                                   recs.ctypes.data)
+    assert rc == 0, f"harness_span_groups: {rc}"
+    return recs

@@ -199,3 +199,19 @@ def test_parse_core_memory_safe_random_inputs(tmp_path, oracle):
                                              UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1"))
     assert r.returncode == 0, (r.stdout[-500:], r.stderr[-3000:])
     assert "mismatches 0" in r.stdout
+
+
+@pytest.mark.parametrize("kinds", [None, ("l4_length", "ver_ihl", "ipv6_hbh"), ("tcp_sack", "tcp_ts", "pad")])
+def test_span_groups_match_oracle(oracle, kinds):
+    """k_parse_span's fast path and generic section emulated per 256-frame
+    group (80-B slots, bucketed items, deferred ranges) over the malformed
+    mix, at two byte alignments of the batch: every record equals the
+    oracle's."""
+    data, offs, _ = helpers.host_malformed_mix(oracle, 6000, seed=77, kinds=kinds)
+    frames = [bytes(data[a:b]) for a, b in zip(offs[:-1], offs[1:])]
+    want = oracle.parse_frames(frames)
+    for shift in (0, 5):
+        buf = np.zeros(len(data) + shift + 16, np.uint8)
+        buf[shift:shift + len(data)] = data
+        got = harness.span_groups(buf, offs + shift)
+        helpers.records_equal(got, want, frames, f"span groups shift {shift}")
