@@ -326,9 +326,7 @@ class Engine:
         if out is None:
             out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
         p = abi.Udp6Build()
-        p.src_ip = None if src_ip is None else src_ip.data_ptr()
-        p.dst_ip = dst_ip.data_ptr()
-        p.def_src_ip = def_src_ip & 0xFFFFFFFF
+        p.src_ip, p.dst_ip = src_ip.data_ptr(), dst_ip.data_ptr()
         p.src_port = None if src_port is None else src_port.data_ptr()
         p.dst_port = None if dst_port is None else dst_port.data_ptr()
         p.src_mac = p.dst_mac = None
