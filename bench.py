@@ -24,10 +24,13 @@ if ROOT not in sys.path:
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 IMIX_WARMUP = 40  # untimed launches before the 6-GB packed batches are timed (see imix_line)
 #: --out name -> nexg out_kind (include/nexg.h NEXG_OUT_*)
-OUT_KINDS = {"desc": 1, "record": 2, "flags": 4, "verdict": 5, "sparse": 6}
+OUT_KINDS = {"desc": 1, "record": 2, "flags": 4, "verdict": 5, "sparse": 6, "grouped": 7}
 OUT_NOTE = {
     "sparse": "lossless sparse descriptors (NEXG_OUT_SPARSE: 1-B shape code per frame + 8-B "
               "exceptions; expands to nexg_desc bit-exactly)",
+    "grouped": "lossless grouped descriptors (NEXG_OUT_GROUPED: NEXG_OUT_SPARSE with each 64-frame group "
+               "of one shape stored as a head byte + 2 verdict bits per frame; expands to nexg_desc "
+               "bit-exactly)",
     "desc": "8-B nexg_desc per frame", "record": "64-B nexg_record per frame",
     "flags": "4-B flags word per frame (no payload location)",
     "verdict": "2-B lossless flags per frame (no payload location)"}
@@ -230,7 +233,9 @@ def stream_ceilings(eng, batch, args, stream, device):
     (nexg_probe_stream, the parse kernels' load shape): read only, and
     64 B read / 8 B written (the descriptor stream's shape)."""
     import torch
-    out = torch.empty(max(batch.data.numel() // 8, batch.count * 8 + 16), dtype=torch.uint8, device=device)
+    from nex_amd.engine import Engine
+    need = max(Engine.out_bytes(k, batch.count) for k in (1, 4, 5, 6, 7))
+    out = torch.empty(max(batch.data.numel() // 8, need + 16), dtype=torch.uint8, device=device)
     nbytes = batch.data.numel() // 16384 * 16384
     r = {}
     for key, w8 in (("read_only_gbs", False), ("read64_write8_gbs", True)):
@@ -238,10 +243,11 @@ def stream_ceilings(eng, batch, args, stream, device):
                       args.steps, args.warmup, stream, device)
         r[key] = round(nbytes / ks / 1e9, 1)
     r["source"] = "nexg_probe_stream on this batch, same steps/warmup, HIP events on the launch stream"
-    if args.out in ("sparse", "desc"):  # the same parse with the other output kinds
+    if args.out in ("sparse", "desc", "grouped"):  # the same parse with the other output kinds
         from nex_amd import abi
         for key, kind in (("desc_output", abi.OUT_DESC), ("flags_output", abi.OUT_FLAGS),
-                          ("verdict_output", abi.OUT_VERDICT), ("sparse_output", abi.OUT_SPARSE)):
+                          ("verdict_output", abi.OUT_VERDICT), ("sparse_output", abi.OUT_SPARSE),
+                          ("grouped_output", abi.OUT_GROUPED)):
             if OUT_KINDS[args.out] == kind:
                 continue
             _, ks = timed(lambda: eng.parse(batch, out_kind=kind, out=out, stream=stream),
@@ -313,6 +319,9 @@ def malformed_line(eng, args, F, first, out_kind, stream, device, rank, world):
     canonical = None
     if out_kind == abi.OUT_SPARSE:  # share of frames with a shape code (no exception slot)
         canonical = round(float((out[:n] != 0).float().mean().item()), 4)
+    elif out_kind == abi.OUT_GROUPED:
+        torch.cuda.synchronize(device)
+        canonical = round(float((abi.grouped_codes(out.cpu().numpy(), n) != 0).mean()), 4)
     if rank != 0:
         return None
     ach = alg / kernel_s / 1e9
@@ -334,8 +343,8 @@ def main():
                          "slow (clock ramp), profiles/r01_staging/imix_ramp.txt")
     ap.add_argument("--workload", choices=["udp64", "imix", "imix_pcap", "malformed", "ser"], default="udp64")
     ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
-    ap.add_argument("--out", choices=list(OUT_KINDS), default="sparse",
-                    help="output kind (default: lossless sparse descriptors, NEXG_OUT_SPARSE)")
+    ap.add_argument("--out", choices=list(OUT_KINDS), default="grouped",
+                    help="output kind (default: lossless grouped descriptors, NEXG_OUT_GROUPED)")
     ap.add_argument("--no-imix", action="store_true",
                     help="skip the configs[2] IMIX line reported beside the default UDP64 run")
     ap.add_argument("--no-malformed", action="store_true",
@@ -368,7 +377,7 @@ def main():
     first = rank * F
     stream = torch.cuda.current_stream(device)
     out_kind = OUT_KINDS[args.out]
-    width = {"desc": 8, "record": 64, "flags": 4, "verdict": 2, "sparse": 1}[args.out]
+    width = {"desc": 8, "record": 64, "flags": 4, "verdict": 2, "sparse": 1, "grouped": 1}[args.out]
 
     if args.workload in ("udp64", "imix", "imix_pcap", "malformed"):
         wl = abi.WL_UDP64 if args.workload == "udp64" else abi.WL_IMIX

@@ -292,6 +292,45 @@ static inline int nexg_sparse_decode(uint8_t code, uint32_t len, uint32_t parse_
     return 1;
 }
 
+/* Grouped sparse descriptors (out_kind NEXG_OUT_GROUPED): NEXG_OUT_SPARSE's
+ * codes with the common part of each 64-frame group g = i / 64 stored once.
+ * A group whose frames all share one non-exception code up to its two
+ * verdict bits is "uniform": heads[g] = that code with bits 4..5 clear, and
+ * its verdicts are two 64-bit masks (bit i % 64 = NEXG_SPARSE_IP_OK /
+ * NEXG_SPARSE_L4_OK of frame i); nothing else of the group is written
+ * (17 B per 64 frames on single-shape traffic). Any other group has heads[g]
+ * = 0 and stores its 1-B codes and exceptions as NEXG_OUT_SPARSE does. Every
+ * area is written densely (a head byte per group, 16 B of masks per group):
+ * interleaving them with the codes costs partial-line writes.
+ * `out` (16-B aligned) holds
+ *   heads : uint8_t[G]                     at out            (G = groups)
+ *   masks : uint32_t[G][4] {ip lo, ip hi, l4 lo, l4 hi} at out + NEXG_GROUPED_MASK_OFFSET(count)
+ *   codes : uint8_t[count]                 at out + NEXG_GROUPED_CODE_OFFSET(count)
+ *   exc   : nexg_desc[count] (capacity)    at out + NEXG_GROUPED_EXC_OFFSET(count)
+ * nexg_grouped_code gives frame i's NEXG_OUT_SPARSE code (then
+ * nexg_sparse_decode, exceptions at exc[64 * g + k]); nexg_grouped_expand
+ * restores nexg_desc[count] on the device. */
+#define NEXG_OUT_GROUPED 7
+#define NEXG_GROUPED_GROUPS(count) ((((uint64_t)(count)) + 63u) >> 6)
+#define NEXG_GROUPED_MASK_OFFSET(count) ((NEXG_GROUPED_GROUPS(count) + 15u) & ~(uint64_t)15u)
+#define NEXG_GROUPED_CODE_OFFSET(count) (NEXG_GROUPED_MASK_OFFSET(count) + 16u * NEXG_GROUPED_GROUPS(count))
+#define NEXG_GROUPED_EXC_OFFSET(count) ((NEXG_GROUPED_CODE_OFFSET(count) + (uint64_t)(count) + 15u) & ~(uint64_t)15u)
+#define NEXG_GROUPED_BYTES(count) (NEXG_GROUPED_EXC_OFFSET(count) + 8u * (uint64_t)(count))
+
+/* frame i's NEXG_OUT_SPARSE code from a NEXG_OUT_GROUPED output (host side) */
+static inline uint8_t nexg_grouped_code(const void* out, uint64_t count, uint64_t i) {
+    const uint8_t* o = (const uint8_t*)out;
+    const uint64_t g = i >> 6;
+    const uint8_t head = o[g];
+    if (!head) return o[NEXG_GROUPED_CODE_OFFSET(count) + i];
+    const uint8_t* m = o + NEXG_GROUPED_MASK_OFFSET(count) + 16u * g;
+    const uint32_t b = (uint32_t)(i & 63u), w = b >> 5, sh = b & 31u;
+    uint32_t ip, l4;
+    __builtin_memcpy(&ip, m + 4u * w, 4);
+    __builtin_memcpy(&l4, m + 8u + 4u * w, 4);
+    return (uint8_t)(head | (((ip >> sh) & 1u) ? NEXG_SPARSE_IP_OK : 0u) | (((l4 >> sh) & 1u) ? NEXG_SPARSE_L4_OK : 0u));
+}
+
 /* FrameSlice::try_from_buf (frame.rs:84-287) per frame, out_kind
  * NEXG_OUT_SLICE, 16 bytes: layer boundaries only, no checksums. FrameSlice
  * has no ParseMode (NEXG_PARSE_STRICT is ignored) and reports every inner
@@ -382,6 +421,9 @@ int nexg_checksum_batch(nexg_ctx* ctx, const nexg_frames* bufs,
  * option (codes + exceptions, layout above). Stream-ordered, device pointers. */
 int nexg_sparse_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
                        const void* sparse, nexg_desc* out, void* stream);
+/* The same from a NEXG_OUT_GROUPED result. */
+int nexg_grouped_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
+                        const void* grouped, nexg_desc* out, void* stream);
 
 /* ---- in-place checksum fix-up (mutable views) -------------
  * Rewrites checksum fields inside the frames, with the raw-buffer semantics

@@ -42,6 +42,7 @@ def load():
         "nexg_parse_batch": (I, [P, ctypes.POINTER(abi.Frames), ctypes.POINTER(abi.ParseOptionC), I, P, P]),
         "nexg_checksum_batch": (I, [P, ctypes.POINTER(abi.Frames), U32, P, P]),
         "nexg_sparse_expand": (I, [P, ctypes.POINTER(abi.Frames), ctypes.POINTER(abi.ParseOptionC), P, P, P]),
+        "nexg_grouped_expand": (I, [P, ctypes.POINTER(abi.Frames), ctypes.POINTER(abi.ParseOptionC), P, P, P]),
         "nexg_recompute_checksums_batch": (I, [P, ctypes.POINTER(abi.Frames), ctypes.POINTER(abi.ParseOptionC),
                                                U32, P, P]),
         "nexg_probe_stream": (I, [P, P, U64, U32, P, P]),

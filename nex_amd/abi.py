@@ -49,6 +49,7 @@ OUT_SLICE = 3
 OUT_FLAGS = 4  # nexg_desc.flags only (include/nexg.h)
 OUT_VERDICT = 5  # lossless 2-B form of the flags word (include/nexg.h)
 OUT_SPARSE = 6  # 1-B shape codes + per-64-frame exception slots (include/nexg.h)
+OUT_GROUPED = 7  # SPARSE with uniform 64-frame groups as a head byte + 2 verdict masks
 
 # NEXG_FRAMES_* hints (nexg_frames.hints)
 FRAMES_MONOTONE = 0x1
@@ -80,13 +81,53 @@ def sparse_bytes(count):
     return sparse_exc_offset(count) + 8 * int(count)
 
 
+def grouped_offsets(count):
+    """NEXG_GROUPED_{MASK,CODE,EXC}_OFFSET and NEXG_GROUPED_BYTES."""
+    g = (int(count) + 63) >> 6
+    mask = (g + 15) & ~15
+    code = mask + 16 * g
+    exc = (code + int(count) + 15) & ~15
+    return mask, code, exc, exc + 8 * int(count)
+
+
+def grouped_codes(buf, count):
+    """Every frame's NEXG_OUT_SPARSE code from a NEXG_OUT_GROUPED output
+    (nexg_grouped_code, vectorised)."""
+    buf = np.asarray(buf, np.uint8)
+    mask, code, _, _ = grouped_offsets(count)
+    G = (count + 63) >> 6
+    i = np.arange(count)
+    g = i >> 6
+    head = buf[:G].astype(np.int64)[g]
+    m = buf[mask:mask + 16 * G].copy().view("<u8").reshape(-1, 2)
+    b = (i & 63).astype(np.uint64)
+    ip = (m[g, 0] >> b) & np.uint64(1)
+    l4 = (m[g, 1] >> b) & np.uint64(1)
+    uni = head | np.where(ip != 0, SPARSE_IP_OK, 0) | np.where(l4 != 0, SPARSE_L4_OK, 0)
+    return np.where(head != 0, uni, buf[code:code + count].astype(np.int64))
+
+
+def grouped_to_desc(buf, count, lengths, parse_flags=0, ip_offset=0):
+    """nexg_desc[count] from a NEXG_OUT_GROUPED output (uint8 host array)."""
+    buf = np.asarray(buf, np.uint8)
+    _, _, exc, _ = grouped_offsets(count)
+    return codes_to_desc(grouped_codes(buf, count), buf[exc:exc + 8 * count].view(DESC_DTYPE), count, lengths,
+                         parse_flags, ip_offset)
+
+
 def sparse_to_desc(buf, count, lengths, parse_flags=0, ip_offset=0):
     """nexg_desc[count] from a NEXG_OUT_SPARSE output (uint8 host array):
     nexg_sparse_decode per code, exceptions looked up per 64-frame group.
     `lengths` = every frame's length (int array)."""
     buf = np.asarray(buf, np.uint8)
-    codes = buf[:count].astype(np.int64)
-    exc = buf[sparse_exc_offset(count):sparse_exc_offset(count) + 8 * count].view(DESC_DTYPE)
+    return codes_to_desc(buf[:count].astype(np.int64),
+                         buf[sparse_exc_offset(count):sparse_exc_offset(count) + 8 * count].view(DESC_DTYPE),
+                         count, lengths, parse_flags, ip_offset)
+
+
+def codes_to_desc(codes, exc, count, lengths, parse_flags=0, ip_offset=0):
+    """nexg_sparse_decode over every code; code-0 frames take the k-th
+    exception of their 64-frame group (exc = the exception slots)."""
     lengths = np.asarray(lengths, np.int64)[:count]
     shape, tags = codes & 0xF, (codes >> SPARSE_TAG_SHIFT) & 3
     out = np.zeros(count, DESC_DTYPE)
@@ -299,13 +340,13 @@ FIXUP_DTYPE = np.dtype([("done", "u1"), ("proto", "u1"), ("ip_csum", "<u2"), ("l
 assert FIXUP_DTYPE.itemsize == 8
 
 #: static inline helpers of include/nexg.h (header-only, not exported)
-HEADER_INLINE = ("nexg_sparse_decode",)
+HEADER_INLINE = ("nexg_sparse_decode", "nexg_grouped_code")
 
 #: every symbol include/nexg.h declares (tests check the .so exports them)
 EXPORTED_SYMBOLS = (
     "nexg_abi_version", "nexg_strerror", "nexg_ctx_create", "nexg_ctx_destroy",
     "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch", "nexg_decode_options", "nexg_probe_stream",
-    "nexg_sparse_expand", "nexg_recompute_checksums_batch",
+    "nexg_sparse_expand", "nexg_grouped_expand", "nexg_recompute_checksums_batch",
     "nexg_rx_config_default", "nexg_rx_open", "nexg_rx_next_batch", "nexg_rx_stats", "nexg_rx_close",
     "nexg_tpacket3_walk", "nexg_tx_open", "nexg_tx_send_batch", "nexg_tx_close",
     "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_build_tcp_batch",

@@ -161,7 +161,8 @@ int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_
     if (!ctx) return NEXG_EINVAL;
     if (!frames_valid(frames)) return fail(ctx, NEXG_EINVAL, "invalid frame batch%s", nullptr);
     if (out_kind != NEXG_OUT_DESC && out_kind != NEXG_OUT_RECORD && out_kind != NEXG_OUT_SLICE &&
-        out_kind != NEXG_OUT_FLAGS && out_kind != NEXG_OUT_VERDICT && out_kind != NEXG_OUT_SPARSE)
+        out_kind != NEXG_OUT_FLAGS && out_kind != NEXG_OUT_VERDICT && out_kind != NEXG_OUT_SPARSE &&
+        out_kind != NEXG_OUT_GROUPED)
         return fail(ctx, NEXG_EINVAL, "invalid out_kind%s", nullptr);
     if (frames->count && !out) return fail(ctx, NEXG_EINVAL, "NULL output%s", nullptr);
     const uint64_t align_mask = out_kind == NEXG_OUT_VERDICT ? 1u : out_kind == NEXG_OUT_FLAGS ? 3u
@@ -186,8 +187,8 @@ int nexg_parse_batch(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_
     return hip_status(ctx, nexg::launch_parse(v, a, out_kind, st), NEXG_ELAUNCH);
 }
 
-int nexg_sparse_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
-                       const void* sparse, nexg_desc* out, void* stream) {
+static int sparse_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
+                         const void* sparse, nexg_desc* out, bool grouped, void* stream) {
     if (!ctx) return NEXG_EINVAL;
     if (!frames_valid(frames)) return fail(ctx, NEXG_EINVAL, "invalid frame batch%s", nullptr);
     if (frames->count && (!sparse || !out)) return fail(ctx, NEXG_EINVAL, "NULL sparse input or output%s", nullptr);
@@ -197,9 +198,19 @@ int nexg_sparse_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_pars
     nexg::ParseArgs a = to_args(frames);
     a.opt_flags = option ? option->flags : 0u;
     a.ip_offset = option ? option->ip_offset : 0u;
-    return hip_status(ctx, nexg::launch_sparse_expand(a, static_cast<const uint8_t*>(sparse), out,
+    return hip_status(ctx, nexg::launch_sparse_expand(a, static_cast<const uint8_t*>(sparse), out, grouped,
                                                       static_cast<hipStream_t>(stream)),
                       NEXG_ELAUNCH);
+}
+
+int nexg_sparse_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
+                       const void* sparse, nexg_desc* out, void* stream) {
+    return sparse_expand(ctx, frames, option, sparse, out, false, stream);
+}
+
+int nexg_grouped_expand(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
+                        const void* grouped, nexg_desc* out, void* stream) {
+    return sparse_expand(ctx, frames, option, grouped, out, true, stream);
 }
 
 int nexg_recompute_checksums_batch(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,

@@ -38,14 +38,16 @@ hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStr
 // TwoPass hands each frame's tail sum to pass 2 through its own output
 // element; outputs narrower than 4 B need a.tail (count u32) instead.
 inline bool parse_needs_tail(ParseVariant v, int out_kind) {
-    return v == ParseVariant::TwoPass && (out_kind == NEXG_OUT_VERDICT || out_kind == NEXG_OUT_SPARSE);
+    return v == ParseVariant::TwoPass &&
+           (out_kind == NEXG_OUT_VERDICT || out_kind == NEXG_OUT_SPARSE || out_kind == NEXG_OUT_GROUPED);
 }
 uint32_t tile_order_for(const ParseArgs& a);
 ParseVariant choose_parse_variant(const ParseArgs& a);
 
 hipError_t launch_checksum(const ParseArgs& a, uint32_t skipword, uint16_t* out, hipStream_t s);
 
-hipError_t launch_sparse_expand(const ParseArgs& a, const uint8_t* sparse, nexg_desc* out, hipStream_t s);
+hipError_t launch_sparse_expand(const ParseArgs& a, const uint8_t* sparse, nexg_desc* out, bool grouped,
+                                hipStream_t s);
 
 hipError_t launch_recompute(const ParseArgs& a, uint32_t which, nexg_fixup* out, hipStream_t s);
 

@@ -48,6 +48,13 @@ ParseVariant choose_parse_variant(const ParseArgs& a) {
     return ParseVariant::TwoPass;
 }
 
+#ifndef NEXG_SPAN_SUB
+#define NEXG_SPAN_SUB 20480  // span kernel sub-tile bytes (A/B builds override)
+#endif
+#ifndef NEXG_SPAN_WPE
+#define NEXG_SPAN_WPE 6  // span kernel waves per SIMD (its VGPR cap)
+#endif
+
 template <int OUT>
 static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream_t s) {
     const uint64_t blocks = (a.count + kTile - 1) / kTile;
@@ -71,7 +78,7 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             // (Two-barrier / double-buffered generations measured slower,
             // 0.66-0.69 vs 0.75: tools/kbench.hip keeps them for A/B.)
             if (OUT == NEXG_OUT_RECORD) hipLaunchKernelGGL((k_parse_span<OUT, 1, 16384, 1>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((k_parse_span<OUT, 1, 20480, 6>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_parse_span<OUT, 1, NEXG_SPAN_SUB, NEXG_SPAN_WPE>), grid, block, 0, s, a);
             break;
         case ParseVariant::TwoPass:
             hipLaunchKernelGGL((k_tail_sums<OUT, 4>), grid, block, 0, s, a);
@@ -104,31 +111,55 @@ hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStr
     if (parse_needs_tail(v, out_kind) && !a.tail) return hipErrorInvalidValue;
     if (out_kind == NEXG_OUT_VERDICT) return launch_parse_out<NEXG_OUT_VERDICT>(v, a, s);
     if (out_kind == NEXG_OUT_SPARSE) return launch_parse_out<NEXG_OUT_SPARSE>(v, a, s);
+    if (out_kind == NEXG_OUT_GROUPED) return launch_parse_out<NEXG_OUT_GROUPED>(v, a, s);
     return out_kind == NEXG_OUT_DESC ? launch_parse_out<NEXG_OUT_DESC>(v, a, s)
                                      : launch_parse_out<NEXG_OUT_RECORD>(v, a, s);
 }
 
-// nexg_sparse_expand: lane per frame; code -> nexg_desc (include/nexg.h
-// table), exception codes take the group's next exception in frame order.
+// nexg_sparse_expand / nexg_grouped_expand: lane per frame; code -> nexg_desc
+// (include/nexg.h table), exception codes take the group's next exception in
+// frame order. GROUPED: a uniform group's code is its head plus the frame's
+// two mask bits; a mixed group's codes and exceptions sit where SPARSE keeps
+// them, past the heads and masks.
+template <bool GROUPED>
 __global__ __launch_bounds__(256) void k_sparse_expand(ParseArgs a, const uint8_t* sparse, nexg_desc* out) {
     const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
     const bool valid = idx < a.count;
-    const uint32_t code = valid ? sparse[idx] : 0xFFu;
+    uint32_t code = 0xFFu;
+    const uint8_t* codes = sparse;
+    const nexg_desc* exc = reinterpret_cast<const nexg_desc*>(sparse + NEXG_SPARSE_EXC_OFFSET(a.count));
+    if (GROUPED) {
+        codes = sparse + NEXG_GROUPED_CODE_OFFSET(a.count);
+        exc = reinterpret_cast<const nexg_desc*>(sparse + NEXG_GROUPED_EXC_OFFSET(a.count));
+    }
+    if (valid) {
+        const uint32_t head = GROUPED ? sparse[idx >> 6] : 0u;
+        if (head) {
+            const uint4 m = reinterpret_cast<const uint4*>(sparse + NEXG_GROUPED_MASK_OFFSET(a.count))[idx >> 6];
+            const uint32_t b = (uint32_t)idx & 63u;
+            const uint32_t ip = b < 32u ? m.x : m.y, l4 = b < 32u ? m.z : m.w;
+            code = head | (((ip >> (b & 31u)) & 1u) ? NEXG_SPARSE_IP_OK : 0u) |
+                   (((l4 >> (b & 31u)) & 1u) ? NEXG_SPARSE_L4_OK : 0u);
+        } else {
+            code = codes[idx];
+        }
+    }
     const uint64_t m = __ballot(code == 0u);
     if (!valid) return;
     uint64_t off;
     uint32_t len = 0;
     frame_extent(a, idx, off, len);
     nexg_desc d;
-    if (!sparse_decode(code, len, a.opt_flags, a.ip_offset, d))
-        d = reinterpret_cast<const nexg_desc*>(sparse + NEXG_SPARSE_EXC_OFFSET(a.count))[(idx & ~63ull) + lanes_below(m)];
+    if (!sparse_decode(code, len, a.opt_flags, a.ip_offset, d)) d = exc[(idx & ~63ull) + lanes_below(m)];
     out[idx] = d;
 }
 
-hipError_t launch_sparse_expand(const ParseArgs& a, const uint8_t* sparse, nexg_desc* out, hipStream_t s) {
+hipError_t launch_sparse_expand(const ParseArgs& a, const uint8_t* sparse, nexg_desc* out, bool grouped,
+                                hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const uint64_t blocks = (a.count + kTile - 1) / kTile;
-    hipLaunchKernelGGL(k_sparse_expand, dim3((uint32_t)blocks), dim3(kTile), 0, s, a, sparse, out);
+    if (grouped) hipLaunchKernelGGL(k_sparse_expand<true>, dim3((uint32_t)blocks), dim3(kTile), 0, s, a, sparse, out);
+    else hipLaunchKernelGGL(k_sparse_expand<false>, dim3((uint32_t)blocks), dim3(kTile), 0, s, a, sparse, out);
     return hipGetLastError();
 }
 

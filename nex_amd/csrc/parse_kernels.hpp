@@ -54,48 +54,50 @@ __device__ __forceinline__ void store_result(void* out, uint64_t idx, const nexg
     }
 }
 
+// the 1-B-code outputs (NEXG_OUT_SPARSE and its grouped form): whole-wave stores
+constexpr bool sparse_like(int out) { return out == NEXG_OUT_SPARSE || out == NEXG_OUT_GROUPED; }
+
 // rank of this lane among the set lanes of m below it (v_mbcnt)
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// NEXG_OUT_SPARSE store (include/nexg.h). Called by all 64 lanes of a wave
+// NEXG_OUT_SPARSE / NEXG_OUT_GROUPED store (include/nexg.h) of a code already
+// known for every lane (0: exception). Called by all 64 lanes of a wave
 // together (valid = the lane holds frame idx; idx = 64-frame-group base +
-// lane): a ballot compacts the wave's exceptions into exc[group*64 + rank];
-// the 1-B codes of lanes 4q..4q+3 are gathered by DPP quad broadcasts and
-// stored as one non-temporal dword by lane 4q.
-__device__ __forceinline__ void store_sparse(const ParseArgs& a, uint64_t idx, bool valid, const nexg_record& r,
-                                             uint32_t known = 0u) {
-    // known: the code when the caller already proved the shape (fast paths)
-    const uint32_t code = !valid ? 0u : known ? known : sparse_encode(r, a.opt_flags, a.ip_offset);
-    const bool exc = valid && code == 0u;
-    const uint64_t m = __ballot(exc);
-    uint8_t* codes = reinterpret_cast<uint8_t*>(a.out);
-    if (exc) {
-        uint2* x = reinterpret_cast<uint2*>(codes + NEXG_SPARSE_EXC_OFFSET(a.count));
-        x[(idx & ~63ull) + lanes_below(m)] =
-            make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
-    }
-    const uint32_t c1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)code, 0x55, 0xF, 0xF, false);  // quad_perm 1111
-    const uint32_t c2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)code, 0xAA, 0xF, 0xF, false);  // quad_perm 2222
-    const uint32_t c3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)code, 0xFF, 0xF, 0xF, false);  // quad_perm 3333
-    if ((idx & 3u) == 0u && idx < a.count)
-        __builtin_nontemporal_store(code | (c1 << 8) | (c2 << 16) | (c3 << 24),
-                                    reinterpret_cast<uint32_t*>(codes + idx));
-}
-
-// store_sparse with the code already known (0: exception) for every lane
+// lane). SPARSE: a ballot compacts the wave's exceptions into exc[group*64 +
+// rank]; the 1-B codes of lanes 4q..4q+3 are gathered by DPP quad broadcasts
+// and stored as one non-temporal dword by lane 4q. GROUPED: a group whose
+// valid lanes share one non-exception code up to the verdict bits stores that
+// code as its head byte and its verdicts as two 64-bit ballots (16 B); any
+// other group stores head 0, then what SPARSE stores, past the heads and masks.
+template <int OUT>
 __device__ __forceinline__ void store_sparse_coded(const ParseArgs& a, uint64_t idx, bool valid,
                                                    const nexg_record& r, uint32_t code) {
+    uint8_t* const o = reinterpret_cast<uint8_t*>(a.out);
+    const uint32_t c = valid ? code : 0u;
+    uint8_t* codes = o;
+    uint2* x = reinterpret_cast<uint2*>(o + NEXG_SPARSE_EXC_OFFSET(a.count));
+    if constexpr (OUT == NEXG_OUT_GROUPED) {
+        if ((idx & ~63ull) >= a.count) return;  // a wave past the last group (wave-uniform)
+        const uint32_t base = c & ~(NEXG_SPARSE_IP_OK | NEXG_SPARSE_L4_OK);
+        const uint32_t c0 = __builtin_amdgcn_readfirstlane(base);  // lane 0 holds the group's first frame
+        const bool uniform = __all(!valid || base == c0) && (c0 & 0xFu) != 0u;
+        const uint64_t g = idx >> 6;
+        if ((idx & 63u) == 0u) o[g] = (uint8_t)(uniform ? c0 : 0u);
+        if (uniform) {
+            const uint64_t mi = __ballot(c & NEXG_SPARSE_IP_OK), ml = __ballot(c & NEXG_SPARSE_L4_OK);
+            if ((idx & 63u) == 0u)
+                __builtin_nontemporal_store(u32x4{(uint32_t)mi, (uint32_t)(mi >> 32), (uint32_t)ml, (uint32_t)(ml >> 32)},
+                                            reinterpret_cast<u32x4*>(o + NEXG_GROUPED_MASK_OFFSET(a.count)) + g);
+            return;
+        }
+        codes = o + NEXG_GROUPED_CODE_OFFSET(a.count);
+        x = reinterpret_cast<uint2*>(o + NEXG_GROUPED_EXC_OFFSET(a.count));
+    }
     const bool exc = valid && code == 0u;
     const uint64_t m = __ballot(exc);
-    uint8_t* codes = reinterpret_cast<uint8_t*>(a.out);
-    if (exc) {
-        uint2* x = reinterpret_cast<uint2*>(codes + NEXG_SPARSE_EXC_OFFSET(a.count));
-        x[(idx & ~63ull) + lanes_below(m)] =
-            make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
-    }
-    const uint32_t c = valid ? code : 0u;
+    if (exc) x[(idx & ~63ull) + lanes_below(m)] = make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
     const uint32_t c1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x55, 0xF, 0xF, false);  // quad_perm 1111
     const uint32_t c2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xAA, 0xF, 0xF, false);  // quad_perm 2222
     const uint32_t c3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xFF, 0xF, 0xF, false);  // quad_perm 3333
@@ -103,10 +105,19 @@ __device__ __forceinline__ void store_sparse_coded(const ParseArgs& a, uint64_t 
         __builtin_nontemporal_store(c | (c1 << 8) | (c2 << 16) | (c3 << 24), reinterpret_cast<uint32_t*>(codes + idx));
 }
 
+// store_sparse_coded with the code taken from the record (known: the code
+// when the caller already proved the shape, the fast paths)
+template <int OUT>
+__device__ __forceinline__ void store_sparse(const ParseArgs& a, uint64_t idx, bool valid, const nexg_record& r,
+                                             uint32_t known = 0u) {
+    const uint32_t code = !valid ? 0u : known ? known : sparse_encode(r, a.opt_flags, a.ip_offset);
+    store_sparse_coded<OUT>(a, idx, valid, r, code);
+}
+
 // every lane of the wave calls this together (see store_sparse)
 template <int OUT>
 __device__ __forceinline__ void store_out(const ParseArgs& a, uint64_t idx, bool valid, const nexg_record& r) {
-    if constexpr (OUT == NEXG_OUT_SPARSE) store_sparse(a, idx, valid, r);
+    if constexpr (sparse_like(OUT)) store_sparse<OUT>(a, idx, valid, r);
     else if (valid) store_result<OUT>(a.out, idx, r);
 }
 
@@ -195,7 +206,7 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
         }
     } else {
         // SPARSE stores need every lane of the wave; other outputs leave early
-        if (OUT != NEXG_OUT_SPARSE && tid >= nf) return;
+        if (!sparse_like(OUT) && tid >= nf) return;
         const uint64_t off = tid < nf ? (a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride) : 0u;
         const uint64_t l64 = tid >= nf ? 0u
                              : a.lengths ? (uint64_t)a.lengths[idx]
@@ -257,15 +268,15 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
             }
         }
         if (kStaged) stage_record(slot, r);  // own slot: no other thread reads it
-        else if constexpr (OUT != NEXG_OUT_SPARSE) store_result<OUT>(a.out, idx, r);
+        else if constexpr (!sparse_like(OUT)) store_result<OUT>(a.out, idx, r);
     }
-    if constexpr (OUT == NEXG_OUT_SPARSE) {
+    if constexpr (sparse_like(OUT)) {
         // fast_udp4_64 proved IPv4/UDP with the datagram to the frame end (payload
         // [42, 64)): the code is the shape and the two verdicts
         const uint32_t known = have ? NEXG_SHAPE_V4_UDP | ((r.flags & NEXG_C_IP_OK) ? NEXG_SPARSE_IP_OK : 0u) |
                                           ((r.flags & NEXG_C_L4_OK) ? NEXG_SPARSE_L4_OK : 0u)
                                     : 0u;
-        store_sparse(a, idx, tid < nf, r, known);
+        store_sparse<OUT>(a, idx, tid < nf, r, known);
     }
     if (kStaged) {
         __syncthreads();
@@ -288,7 +299,7 @@ constexpr uint32_t kLaneWin = 80;  // register window of k_parse_lane80
 // Outputs narrower than 4 B (verdict, sparse codes) hand off through a.tail.
 template <int OUT>
 __device__ __forceinline__ uint32_t* handoff_slot(const ParseArgs& a, uint64_t idx) {
-    if (OUT == NEXG_OUT_VERDICT || OUT == NEXG_OUT_SPARSE) return a.tail + idx;
+    if (OUT == NEXG_OUT_VERDICT || sparse_like(OUT)) return a.tail + idx;
     return reinterpret_cast<uint32_t*>(a.out) + idx * (OUT == NEXG_OUT_FLAGS ? 1u : OUT == NEXG_OUT_DESC ? 2u : 16u);
 }
 
@@ -437,7 +448,7 @@ template <int OUT>
 __global__ __launch_bounds__(256) void k_parse_lane80(ParseArgs a) {
     const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
     const bool valid = idx < a.count;
-    if (OUT != NEXG_OUT_SPARSE && !valid) return;  // sparse stores need the whole wave
+    if (!sparse_like(OUT) && !valid) return;  // sparse stores need the whole wave
     uint64_t off = 0;
     uint32_t len = 0;
     nexg_record r{};
@@ -713,7 +724,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // frame-relative LE sum: x256 (mod 0xFFFF) for a frame at an odd address
         const uint64_t tail = (sh & 1u) ? (uint64_t)tq * 256u : (uint64_t)tq;
         if (fast_canonical80(w, len, a.opt_flags, tail, qend, r)) {
-            if (OUT == NEXG_OUT_SPARSE) code = canonical80_code(r);
+            if (sparse_like(OUT)) code = canonical80_code(r);
             if (OUT == NEXG_OUT_RECORD) stage_record(slots + SpanFrame::kSlot * t, r);
         } else {  // declined: the window goes to this lane's slot for pass (B)
             gen = true;
@@ -805,7 +816,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             if (OUT == NEXG_OUT_RECORD) {
                 stage_record(os, rr);
             } else {
-                const uint32_t c = OUT == NEXG_OUT_SPARSE ? sparse_encode(rr, a.opt_flags, a.ip_offset) : 0u;
+                const uint32_t c = sparse_like(OUT) ? sparse_encode(rr, a.opt_flags, a.ip_offset) : 0u;
                 *reinterpret_cast<uint4*>(os) =
                     make_uint4(rr.flags, (uint32_t)rr.payload_off | ((uint32_t)rr.payload_len << 16), c, 0u);
             }
@@ -819,7 +830,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             code = v.z;
         }
     }
-    if (OUT == NEXG_OUT_SPARSE) store_sparse_coded(a, idx, have, r, code);
+    if (sparse_like(OUT)) store_sparse_coded<OUT>(a, idx, have, r, code);
     else if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
     if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the slots (pitch 80 B)
         static_assert(kStage >= kTile * SpanFrame::kSlot, "record staging needs 20 KiB");

@@ -192,34 +192,37 @@ class Engine:
         """Bytes of a nexg_parse_batch output of `out_kind` for `count` frames."""
         if out_kind == abi.OUT_SPARSE:
             return abi.sparse_bytes(count)
+        if out_kind == abi.OUT_GROUPED:
+            return abi.grouped_offsets(count)[3]
         return count * {abi.OUT_DESC: 8, abi.OUT_RECORD: 64, abi.OUT_SLICE: 16, abi.OUT_FLAGS: 4,
                         abi.OUT_VERDICT: 2}[out_kind]
 
     def parse_to_numpy(self, batch, option=ParseOption(), mode=ParseMode.Lenient,
                        out_kind=abi.OUT_RECORD):
-        """Host copy of the parse output; OUT_SPARSE comes back decoded on the
-        host into nexg_desc (abi.sparse_to_desc)."""
+        """Host copy of the parse output; OUT_SPARSE / OUT_GROUPED come back
+        decoded on the host into nexg_desc (abi.sparse_to_desc / grouped_to_desc)."""
         out = self.parse(batch, option, mode, out_kind)
         _torch().cuda.synchronize(self.torch_device)
-        if out_kind == abi.OUT_SPARSE:
-            return abi.sparse_to_desc(out.cpu().numpy(), batch.count, batch.frame_lengths(),
-                                      option.flags(mode), option.offset)
+        if out_kind in (abi.OUT_SPARSE, abi.OUT_GROUPED):
+            dec = abi.sparse_to_desc if out_kind == abi.OUT_SPARSE else abi.grouped_to_desc
+            return dec(out.cpu().numpy(), batch.count, batch.frame_lengths(), option.flags(mode), option.offset)
         dt = {abi.OUT_DESC: abi.DESC_DTYPE, abi.OUT_RECORD: abi.RECORD_DTYPE,
               abi.OUT_SLICE: abi.SLICE_DTYPE, abi.OUT_FLAGS: abi.FLAGS_DTYPE,
               abi.OUT_VERDICT: abi.VERDICT_DTYPE}[out_kind]
         return out.cpu().numpy()[: batch.count * dt.itemsize].view(dt)
 
     def sparse_expand(self, batch: FrameBatch, sparse, option: ParseOption = ParseOption(),
-                      mode: ParseMode = ParseMode.Lenient, out=None, stream=None):
+                      mode: ParseMode = ParseMode.Lenient, out=None, stream=None, grouped=False):
         """nexg_desc[count] (uint8 device tensor) from a NEXG_OUT_SPARSE output
-        of the same batch and option (nexg_sparse_expand)."""
+        (grouped=True: NEXG_OUT_GROUPED) of the same batch and option
+        (nexg_sparse_expand / nexg_grouped_expand)."""
         torch = _torch()
         if out is None:
             out = torch.empty(max(batch.count, 1) * 8, dtype=torch.uint8, device=self.torch_device)
         fr = batch.to_c()
         opt = abi.ParseOptionC(option.flags(mode), option.offset)
-        self._check(self.lib.nexg_sparse_expand(self.ctx, ctypes.byref(fr), ctypes.byref(opt), _ptr(sparse),
-                                                _ptr(out), self._stream(stream)))
+        fn = self.lib.nexg_grouped_expand if grouped else self.lib.nexg_sparse_expand
+        self._check(fn(self.ctx, ctypes.byref(fr), ctypes.byref(opt), _ptr(sparse), _ptr(out), self._stream(stream)))
         return out
 
     def recompute_checksums(self, batch: FrameBatch, which: int = abi.FIX_IP | abi.FIX_L4,

@@ -39,6 +39,8 @@ def test_malformed_mix_matches_oracle(engine, oracle, mix):
         d[n] = want[n]
     got = engine.parse_to_numpy(batch, out_kind=abi.OUT_SPARSE)
     helpers.records_equal(got, d, frames, "malformed mix sparse")
+    got = engine.parse_to_numpy(batch, out_kind=abi.OUT_GROUPED)
+    helpers.records_equal(got, d, frames, "malformed mix grouped")
     # the mutations leave the canonical shapes (exception slots) and reach
     # the error statuses (lenient parsing turns most into shorter layer stacks)
     codes = engine.parse(batch, out_kind=abi.OUT_SPARSE)[: batch.count].cpu().numpy()

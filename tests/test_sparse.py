@@ -86,3 +86,63 @@ def test_synthetic_workloads_need_no_exceptions(oracle, workload):
     helpers.records_equal(dev, desc_of(recs), frames, "synthetic")
     if workload == abi.WL_UDP64:
         assert set(np.unique(codes & 0xF)) == {1}  # NEXG_SHAPE_V4_UDP
+
+
+def host_grouped_buffer(codes, recs):
+    """The NEXG_OUT_GROUPED byte layout a kernel writes for these codes
+    (include/nexg.h): uniform 64-frame groups as head + verdict masks, the
+    rest as NEXG_OUT_SPARSE codes and exceptions past them."""
+    n = len(codes)
+    mask, code, exc_off, total = abi.grouped_offsets(n)
+    buf = np.zeros(total, np.uint8)
+    exc = buf[exc_off:].view(abi.DESC_DTYPE)
+    d = desc_of(recs)
+    for g in range(0, n, 64):
+        c = np.asarray(codes[g:g + 64], np.int64)
+        base = c & ~(abi.SPARSE_IP_OK | abi.SPARSE_L4_OK)
+        if (base == base[0]).all() and (base[0] & 0xF) != 0:
+            buf[g // 64] = base[0]
+            ip = sum(1 << k for k in range(len(c)) if c[k] & abi.SPARSE_IP_OK)
+            l4 = sum(1 << k for k in range(len(c)) if c[k] & abi.SPARSE_L4_OK)
+            buf[mask + 16 * (g // 64):mask + 16 * (g // 64) + 16] = np.frombuffer(
+                ip.to_bytes(8, "little") + l4.to_bytes(8, "little"), np.uint8)
+            continue
+        buf[code + g:code + g + len(c)] = c
+        for k, i in enumerate([i for i in range(g, min(g + 64, n)) if codes[i] == 0]):
+            exc[g + k] = d[i]
+    return buf
+
+
+def test_grouped_roundtrip_both_decoders(oracle, corpus, tmp_path):
+    """NEXG_OUT_GROUPED over uniform groups (64-B UDP frames, both verdicts
+    varying), groups one frame off uniform, partial last groups and the mixed
+    corpus: the numpy decoder restores every descriptor and the header's
+    inline nexg_grouped_code gives every frame's NEXG_OUT_SPARSE code."""
+    import os
+    import subprocess
+    rng = np.random.default_rng(5)
+    udp = [bytearray(oracle.gen_frame(abi.WL_UDP64, i)) for i in range(64 * 5 + 40)]
+    for f in udp[::3]:
+        f[rng.integers(42, 64)] ^= 0x5A  # UDP checksum fails: L4 verdict varies inside a group
+    for f in udp[1::7]:
+        f[24] ^= 0x01  # IPv4 header checksum fails
+    udp[64 * 2 + 9] = bytearray(oracle.gen_frame(abi.WL_IMIX, 3))  # one group no longer uniform
+    frames = [bytes(f) for f in udp] + corpus[:1000]
+    recs = oracle.parse_frames(frames)
+    codes, _, _ = harness.sparse(recs, 0, 0)
+    buf = host_grouped_buffer(codes, recs)
+    assert (buf[:5] != 0).sum() >= 3  # uniform groups present
+    lens = np.array([len(f) for f in frames])
+    helpers.records_equal(abi.grouped_to_desc(buf, len(frames), lens), desc_of(recs), frames, "grouped numpy")
+    assert (abi.grouped_codes(buf, len(frames)) == codes).all()
+    src = tmp_path / "g.c"
+    src.write_text('#include <stdio.h>\n#include <stdlib.h>\n#include "%s"\n'
+                   'int main(int c, char** v) { FILE* f = fopen(v[1], "rb"); static unsigned char b[1 << 22];'
+                   ' if (!f || fread(b, 1, sizeof b, f) == 0) return 2; unsigned long long n = strtoull(v[2], 0, 10);'
+                   ' for (unsigned long long i = 0; i < n; i++) printf("%%u\\n", nexg_grouped_code(b, n, i));'
+                   ' return 0; }\n' % os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                   "include", "nexg.h"))
+    subprocess.check_call(["gcc", "-O1", "-std=c99", "-Wall", "-Werror", "-o", str(tmp_path / "g"), str(src)])
+    buf.tofile(tmp_path / "b.bin")
+    out = subprocess.check_output([str(tmp_path / "g"), str(tmp_path / "b.bin"), str(len(frames))]).split()
+    assert [int(x) for x in out] == [int(x) for x in codes]

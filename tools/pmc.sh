@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 run() { local name=$1 secs=$2; shift 2
   timeout -s KILL "$secs" "$@" > "gpurun_out/pmc/$name.log" 2>&1; local rc=$?
   echo "$name rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
-CONFIGS=${CONFIGS:-"udp64.sparse imix.sparse imix_pcap.sparse malformed.sparse udp64.desc imix.desc ser.desc ser_probe.desc"}
+CONFIGS=${CONFIGS:-"udp64.grouped imix.grouped imix_pcap.grouped malformed.grouped udp64.sparse imix.sparse udp64.desc ser.desc ser_probe.desc"}
 for cfg in $CONFIGS; do
   wl=${cfg%.*}; out=${cfg#*.}; extra=""
   # ser = the full-tuple build, ser_probe = the udp_ping probe batch (bench.py --ser-shape)
