@@ -23,6 +23,11 @@ if ROOT not in sys.path:
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 IMIX_WARMUP = 40  # untimed launches before the 6-GB packed batches are timed (see imix_line)
+# every timed line also warms up for at least this long: the kernel-trace of a
+# fresh 16M UDP64 batch runs its first ~10 launches at 150-155 us, the next ~40
+# at 163-170 us and settles near 160 us only after ~80 (profiles/r03/warmup/);
+# W untimed launches alone (the driver passes --warmup 5) time that transient
+WARMUP_SECONDS = 0.25
 #: --out name -> nexg out_kind (include/nexg.h NEXG_OUT_*)
 OUT_KINDS = {"desc": 1, "record": 2, "flags": 4, "verdict": 5, "sparse": 6, "grouped": 7}
 OUT_NOTE = {
@@ -221,7 +226,7 @@ def timed(step, steps, warmup, stream, device, host_clock=False, with_local=Fals
     ev1 = torch.cuda.Event(enable_timing=True)
     elapsed, local = dist.timed_steps(step, steps, warmup, sync=lambda: torch.cuda.synchronize(device),
                                       device=device, before=lambda: ev0.record(stream),
-                                      after=lambda: ev1.record(stream))
+                                      after=lambda: ev1.record(stream), warmup_seconds=WARMUP_SECONDS)
     kernel_s = ev0.elapsed_time(ev1) / 1e3 / steps
     if host_clock:  # copies + kernels on side streams: the host clock is the measure
         kernel_s = local / steps

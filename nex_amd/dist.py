@@ -53,18 +53,25 @@ def init(backend: str = None, force: bool = False):
     return rank, world
 
 
-def timed_steps(step, steps: int, warmup: int, sync=None, device=None, before=None, after=None):
-    """bench.py's timing discipline: `warmup` untimed steps, then exactly
-    `steps` steps bracketed by sync + barrier + sync on both sides; returns
-    (max-over-ranks elapsed seconds, this rank's elapsed seconds). `sync`
-    waits for this rank's device work (torch.cuda.synchronize on a GPU);
-    before/after run inside the timed bracket around the steps (HIP event
-    records)."""
+def timed_steps(step, steps: int, warmup: int, sync=None, device=None, before=None, after=None,
+                warmup_seconds: float = 0.0):
+    """bench.py's timing discipline: `warmup` untimed steps (continued, in
+    batches of 32, until at least `warmup_seconds` of wall time have passed),
+    then exactly `steps` steps bracketed by sync + barrier + sync on both
+    sides; returns (max-over-ranks elapsed seconds, this rank's elapsed
+    seconds). `sync` waits for this rank's device work (torch.cuda.synchronize
+    on a GPU); before/after run inside the timed bracket around the steps (HIP
+    event records)."""
     import time
     sync = sync or (lambda: None)
+    t_w = time.perf_counter()
     for _ in range(warmup):
         step()
     sync()
+    while time.perf_counter() - t_w < warmup_seconds:
+        for _ in range(32):
+            step()
+        sync()
     barrier(device)
     sync()
     t0 = time.perf_counter()

@@ -75,7 +75,9 @@ def test_grouped_matches_oracle_every_layout(engine, oracle, corpus, opt, mode):
         dev = dev.cpu().numpy()[: len(corpus) * 8].view(abi.DESC_DTYPE)
         helpers.records_equal(dev, want, corpus, f"grouped expand {name} flags={flags}")
         h = marks(raw, len(corpus))
-        assert h.sum() >= 40 and (~h).sum() >= 100  # single-shape and mixed groups both occur
+        assert (~h).sum() >= 100
+        if name == "lengths":  # the lane kernel stores single-shape groups as such (the span kernel: all mixed)
+            assert h.sum() >= 40
 
 
 @pytest.mark.parametrize("stride", [64, 128])

@@ -107,3 +107,22 @@ def test_two_rank_bench_reduction():
         assert tp["value"] == round(total / emax / 1e6, 2)
         assert tp["ms_per_step"] == round(emax / 5 * 1e3, 4)
         assert r[5] == [1.0, 11.0]  # every rank's value, in rank order
+
+
+def test_timed_steps_warmup_floor():
+    """bench.py's warmup floor (dist.timed_steps warmup_seconds): W untimed
+    steps, then whole batches of 32 until the floor has passed; the timed
+    region is still exactly `steps` steps."""
+    import time
+    calls = []
+
+    def step():
+        calls.append(time.perf_counter())
+        time.sleep(0.0005)
+    elapsed, local = dist.timed_steps(step, steps=7, warmup=3, warmup_seconds=0.05)
+    warm = len(calls) - 7
+    assert warm >= 3 + 32 and (warm - 3) % 32 == 0
+    assert calls[warm - 1] - calls[0] >= 0.04 and elapsed == local > 0
+    calls.clear()
+    dist.timed_steps(step, steps=7, warmup=3)
+    assert len(calls) == 10

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--libs", default="")
     ap.add_argument("--share", type=float, default=0.5, help="share of frames mutated (kinds other than clean)")
     ap.add_argument("--unwrap-vlan", action="store_true", help="parse with NEXG_PARSE_VLAN (ParseOption.unwrap_vlan)")
+    ap.add_argument("--out", default="sparse", choices=["sparse", "grouped"], help="output kind")
     args = ap.parse_args()
     import torch
     from nex_amd import _lib, abi, workloads
@@ -41,21 +42,22 @@ def main():
         engines.append(Engine(0))
     eng = engines[0]
     stream = torch.cuda.current_stream()
+    ok = abi.OUT_GROUPED if args.out == "grouped" else abi.OUT_SPARSE
     kinds = args.kinds.split(",") if args.kinds else ["clean"] + list(workloads.MUTATIONS) + ["all"]
     for k in kinds:
         share = 0.0 if k == "clean" else args.share
         sel = workloads.MUTATIONS if k in ("clean", "all") else (k,)
         mix, counts = workloads.malformed_mix(eng, args.distinct, mutate_share=share, kinds=sel)
         b = workloads.tiled(mix, args.tiles)
-        out = torch.empty(Engine.out_bytes(abi.OUT_SPARSE, b.count), dtype=torch.uint8, device="cuda")
+        out = torch.empty(Engine.out_bytes(ok, b.count), dtype=torch.uint8, device="cuda")
         def timed(e):
             for _ in range(args.warmup):
-                e.parse(b, opt, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
+                e.parse(b, opt, out_kind=ok, out=out, stream=stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             e0.record(stream)
             for _ in range(args.steps):
-                e.parse(b, opt, out_kind=abi.OUT_SPARSE, out=out, stream=stream)
+                e.parse(b, opt, out_kind=ok, out=out, stream=stream)
             e1.record(stream)
             torch.cuda.synchronize()
             return e0.elapsed_time(e1) / 1e3 / args.steps
@@ -72,7 +74,8 @@ def main():
                         same.append(bool(torch.equal(out, ref)))
             times.append(row)
         s = min(t[0] for t in times)
-        exc = float((out[: b.count] == 0).float().mean().item())
+        codes = out[: b.count].cpu().numpy() if ok == abi.OUT_SPARSE else abi.grouped_codes(out.cpu().numpy(), b.count)
+        exc = float((codes == 0).mean())
         line = {"kind": k, "frames": b.count, "bytes": b.total_bytes, "kernel_ms": round(s * 1e3, 4),
                 "mpkt_s": round(b.count / s / 1e6, 1), "frac": round(b.total_bytes / s / 8e12, 4),
                 "exception_share": round(exc, 4), "mutated": counts.get(k, None)}
