@@ -668,7 +668,15 @@ NEXG_HD uint32_t wle16(const uint32_t (&w)[20], uint32_t i) { return (w[i >> 2] 
 
 NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t opt_flags,
                               uint64_t tail_sum, uint32_t tail_end, nexg_record& r) {
-    if ((opt_flags & NEXG_PARSE_FROM_IP) || len < 14u) return false;
+    if (opt_flags & NEXG_PARSE_FROM_IP) return false;
+    if (len < 14u) {  // Q2 (ethernet.rs:310-316), exactly as parse_frame reports it
+        r = nexg_record{};
+        r.flags = (uint32_t)NEXG_ERR_BUFFER_TOO_SHORT << NEXG_STATUS_SHIFT;
+        r.l4_type = NEXG_CTX_ETHERNET_PACKET;
+        r.ip_src = 14u;
+        r.ip_dst = len;
+        return true;
+    }
     const uint32_t et = wbe16(w0, 12);
     const bool v6 = et == 0x86DDu, v4 = et == 0x0800u;
     const bool strict = (opt_flags & NEXG_PARSE_STRICT) != 0;
@@ -702,7 +710,31 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     const uint32_t e = 14u + ipl;                      // >= l4
     const uint32_t raw = v6 ? wbyte(w0, 20) : wbyte(w0, 23);
     const uint32_t pv = ip_next_protocol_value(raw);
-    if (v6 && (pv == 0u || pv == 43u || pv == 44u || pv == 60u)) return false;  // extension headers
+    if (v6 && (pv == 0u || pv == 43u || pv == 44u || pv == 60u)) {
+        // one extension header (hop-by-hop, routing, fragment, destination
+        // options) ahead of a non-extension header, inside the IP bytes: the
+        // walk of ipv6.rs:217-384 (parse_ipv6) ends after it, and the Frame
+        // dispatches on the first next header (Q10): no transport layer and
+        // no checksum, the payload follows the extension header
+        const uint32_t nh2 = ip_next_protocol_value(wbyte(w0, 54)), el = wbyte(w0, 55);
+        const uint32_t tl = pv == 44u ? 8u : 8u + 8u * el;
+        if (ipl < 42u || 40u + tl > ipl || nh2 == 0u || nh2 == 43u || nh2 == 44u || nh2 == 60u) return false;
+        r = nexg_record{};
+        const uint32_t w6 = (wbe16(w0, 14) << 16) | wbe16(w0, 16);
+        r.flags = NEXG_L_ETHERNET | NEXG_L_IP | NEXG_L_IPV6;
+        r.ip_ver_ihl = 0x60;
+        r.ip_tos = (uint8_t)(w6 >> 20);
+        r.ip_length = (uint16_t)(decl - 40u);
+        r.ip_word = w6 & 0xFFFFFu;
+        r.ip_ttl = (uint8_t)wbyte(w0, 21);
+        r.ip_proto = (uint8_t)pv;
+        r.ip_nopt = 1;
+        r.packet_len = (uint16_t)len;
+        r.ethertype = (uint16_t)et;
+        r.l3_off = 14;
+        set_payload(r, 54u + tl, ipl - 40u - tl);
+        return true;
+    }
     const bool inwin = e <= 80u;  // checksummed bytes all in the window
     if (e != len && e != tail_end && !inwin) return false;
     const uint32_t n = e - l4;
@@ -715,8 +747,15 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     auto LE = [&](uint32_t k) { return v6 ? wle16(w, 54u + k) : wle16(w, 34u + k); };
     const bool tcp = pv == 6u, udp = pv == 17u, icmp = pv == (v6 ? 58u : 1u);
     const uint32_t doff = L(12) >> 12, ulen = L(4);
-    const bool tfail = tcp && (n < 20u || doff < 5u || 4u * doff > n);  // no TcpPacket
-    const bool q14 = udp && (n < 8u || ulen < 8u || ulen > n);          // no UdpPacket
+    const uint32_t o0 = v6 ? w[18] : w[13], o1 = v6 ? w[19] : w[14];
+    const uint32_t b20 = (o0 >> 16) & 0xFFu, b21 = o0 >> 24, b22 = o1 & 0xFFu, b23 = (o1 >> 8) & 0xFFu;
+    const uint32_t olen = 4u * doff - 20u;  // used when doff > 5
+    // an option list whose first option is a TLV with a length below 2 or
+    // past the data offset ends the walk of tcp.rs:767-818 with an error
+    // (InvalidLength / Truncated): no TcpPacket (Q13), like a short header
+    const bool walkfail = doff > 5u && b20 >= 2u && (b21 < 2u || b21 > olen);
+    const bool tfail = tcp && (n < 20u || doff < 5u || 4u * doff > n || walkfail);  // no TcpPacket
+    const bool q14 = udp && (n < 8u || ulen < 8u || ulen > n);                       // no UdpPacket
     // TCP option lists of one TLV, alone (MSS of a SYN-ACK: 02 04 ..) or
     // behind NOP, NOP (timestamps, RFC 7323's layout for most data segments;
     // SACK blocks), exactly filling the data offset: the option walk
@@ -724,9 +763,6 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     // bytes and data offset (tcp.rs:521-575), so the checksum sums the raw
     // bytes from l4 + 20 on like a payload; only the four layout bytes
     // (l4 + 20..23, inside the window for both families) are read
-    const uint32_t o0 = v6 ? w[18] : w[13], o1 = v6 ? w[19] : w[14];
-    const uint32_t b20 = (o0 >> 16) & 0xFFu, b21 = o0 >> 24, b22 = o1 & 0xFFu, b23 = (o1 >> 8) & 0xFFu;
-    const uint32_t olen = 4u * doff - 20u;  // used when doff > 5
     const bool one = b20 >= 2u && b21 >= 2u && b21 == olen;
     const bool nnx = b20 == 1u && b21 == 1u && b22 >= 2u && b23 >= 2u && 2u + b23 == olen;
     const bool tsopt = tcp && !tfail && doff > 5u && (one || nnx);
@@ -844,6 +880,7 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
 // without a packet (Q14) is an exception (0), as sparse_encode would make it
 NEXG_HD uint32_t canonical80_code(const nexg_record& r) {
     const uint32_t f = r.flags;
+    if (f >> NEXG_STATUS_SHIFT) return 10u + ((f >> NEXG_STATUS_SHIFT) & 7u);  // BufferTooShort (len < 14): 11
     if (!(f & (NEXG_L_IPV4 | NEXG_L_IPV6))) return (f & NEXG_L_IP) ? (uint32_t)NEXG_SHAPE_IP_NONE : (uint32_t)NEXG_SHAPE_ETH_ONLY;
     const bool v6 = (f & NEXG_L_IPV6) != 0, l4 = (f & NEXG_C_L4_CHECKED) != 0;
     const uint32_t shape = !l4 ? (v6 ? 9u : 8u) : ((v6 ? 4u : 1u) + ((f & NEXG_L_UDP) ? 0u : (f & NEXG_L_TCP) ? 1u : 2u));

@@ -159,6 +159,8 @@ extern "C" int harness_sparse_decode(const uint8_t* codes, const uint32_t* lens,
 // patched; harness_span_stats counts what the generic section does.
 // Records out (the record form of what the sparse kernel encodes). Frames of a
 // group that is not packed (or a batch that is not) return -1.
+static uint8_t* g_span_declined;  // optional per-frame output: 1 = the generic core parsed it
+extern "C" void harness_span_declined(uint8_t* out) { g_span_declined = out; }
 static uint64_t g_span_stats[6];  // declined, declined past 80 B, deferred ranges, groups with a declined
                                   // frame, HBM byte loads, inline HBM range sums (the last two: NEXG_SPAN_PROBE)
 extern "C" const uint64_t* harness_span_stats() {
@@ -201,6 +203,7 @@ extern "C" int harness_span_groups(const uint8_t* data, uint64_t data_bytes, con
                 out[f0 + t] = r;
             } else {
                 gen[t] = true;
+                if (g_span_declined) g_span_declined[f0 + t] = 1;
                 key[t] = nexg::span_bucket(w[3], w[5], flags);
                 memcpy(lds + S * t, w, S);
             }
