@@ -508,3 +508,35 @@ def host_malformed_mix(oracle, count, seed=77, mutate_share=0.5, kinds=None):
     np.cumsum([len(f) for f in frames], out=offs[1:])
     data = np.frombuffer(b"".join(bytes(f) for f in frames), np.uint8)
     return workloads.mutate_packed(data, offs, seed, mutate_share, kinds or workloads.MUTATIONS)
+
+
+def fastpath_edge_frames(rng):
+    """The register fast path's round-3 shapes and their near misses:
+    frames of 0..13 B (Q2); IPv6 with one extension header (hop-by-hop,
+    routing, fragment, destination options) of every small length, ahead of
+    TCP / UDP / ICMPv6 / no-next-header / another extension, with payload
+    lengths that end exactly at, one before and past its end; TCP data offsets
+    6..15 whose first option is a TLV of length 0, 1, 2, the list's length,
+    one past it and 255 (walk fails or goes on), behind NOP / EOL too."""
+    f = [bytes(rng.integers(0, 256, n, dtype=np.uint8)) for n in range(14)]
+    f += [bytes(range(12)) + bytes([0x86, 0xDD]) + bytes(rng.integers(0, 256, k, dtype=np.uint8)) for k in (0, 39, 41)]
+    for nh in (0, 43, 44, 60):
+        for el in (0, 1, 2, 5):
+            for nh2 in (6, 17, 58, 59, 0, 60, 200):
+                tl = 8 if nh == 44 else 8 + 8 * el
+                ext = bytes([nh2, el]) + bytes(rng.integers(0, 256, tl - 2, dtype=np.uint8))
+                body = bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8))
+                pl = len(ext) + len(body)
+                for plen in (pl, tl, tl - 1, 1, 0, pl + 9, 1500):
+                    f.append(_eth(_ipv6(ext + body, nh, plen=plen), 0x86DD))
+                f.append(_eth(_ipv6(ext[:tl - 3], nh, plen=tl), 0x86DD))  # header cut by the frame end
+    for fam in (4, 6):
+        for doff in range(6, 16):
+            olen = 4 * doff - 20
+            for first in (0, 1, 2, 3, 8, 30, 200):
+                for ln in sorted({0, 1, 2, 3, olen - 1, olen, olen + 1, 255}):
+                    opts = bytes([first, ln & 255]) + bytes(rng.integers(0, 256, olen - 2, dtype=np.uint8))
+                    pay = bytes(rng.integers(0, 256, int(rng.choice([0, 5, 40, 600])), dtype=np.uint8))
+                    seg = _tcp(pay, opts, doff=doff)
+                    f.append(_eth(_ipv4(seg, 6)) if fam == 4 else _eth(_ipv6(seg, 6), 0x86DD))
+    return f

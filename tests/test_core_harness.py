@@ -215,3 +215,26 @@ def test_span_groups_match_oracle(oracle, kinds):
         buf[shift:shift + len(data)] = data
         got = harness.span_groups(buf, offs + shift)
         helpers.records_equal(got, want, frames, f"span groups shift {shift}")
+
+
+def test_fastpath_edge_shapes_match_oracle(oracle):
+    """The fast path's round-3 shapes (Q2 short frames, one IPv6 extension
+    header, TCP option walks failing at the first TLV) and their near misses,
+    lenient and strict, through the lane kernel's path (aligned) and the span
+    kernel's arithmetic at every byte alignment, and through the span-group
+    emulation: records equal the oracle's."""
+    frames = helpers.fastpath_edge_frames(np.random.default_rng(31))
+    assert len(frames) > 1500
+    buf, offs, lens = pack(frames, 4)
+    for flags in (0, abi.PARSE_STRICT):
+        want = oracle.parse_packed(buf, offs, lens, flags=flags)
+        got = harness.parse_packed(buf, offs, lens, flags=flags, use_fast=4)
+        helpers.records_equal(got, want, frames, f"edge shapes flags={flags}")
+    for shift in (1, 2, 3):
+        buf, offs, lens = pack(frames, 1, shift)
+        got = harness.parse_packed(buf, offs, lens, use_fast=5)
+        helpers.records_equal(got, oracle.parse_packed(buf, offs, lens), frames, f"edge span shift={shift}")
+    po = np.zeros(len(frames) + 1, np.int64)
+    np.cumsum([len(x) for x in frames], out=po[1:])
+    data = np.frombuffer(b"".join(frames) + bytes(16), np.uint8)
+    helpers.records_equal(harness.span_groups(data, po), oracle.parse_frames(frames), frames, "edge span groups")

@@ -80,3 +80,32 @@ def test_tcp_timestamps_match_oracle(engine, oracle):
         d[n] = want[n]
     got = engine.parse_to_numpy(batch, out_kind=abi.OUT_SPARSE)
     helpers.records_equal(got, d, frames, "tcp_ts sparse")
+
+
+def test_fastpath_edge_shapes_on_gpu(engine, oracle):
+    """The register fast path's round-3 shapes (frames under 14 B, one IPv6
+    extension header, TCP option walks failing at the first TLV) and their
+    near misses on the GPU: span kernel (packed at 0-3 byte shifts, capture
+    gaps with the monotone hint) and lane kernel (explicit lengths), record
+    and grouped output, lenient and strict, equal the oracle."""
+    import torch
+    from nex_amd.engine import FrameBatch
+    from nex_amd.frame import ParseMode, ParseOption
+    frames = helpers.fastpath_edge_frames(np.random.default_rng(31))
+    for mode in (ParseMode.Lenient, ParseMode.Strict):
+        opt = ParseOption()
+        want = oracle.parse_frames(frames, opt.flags(mode))
+        d = np.zeros(len(frames), abi.DESC_DTYPE)
+        for n in abi.DESC_DTYPE.names:
+            d[n] = want[n]
+        batches = [FrameBatch.from_packed(frames, shift=s) for s in (0, 1, 2, 3)]
+        batches.append(FrameBatch.from_frames(frames, pad_to=4))
+        b = FrameBatch.from_frames(frames, pad_to=16)
+        b.hints = abi.FRAMES_MONOTONE
+        batches.append(b)
+        for k, batch in enumerate(batches):
+            helpers.records_equal(engine.parse_to_numpy(batch, opt, mode, abi.OUT_RECORD), want, frames,
+                                  f"edge record layout {k} {mode}")
+            helpers.records_equal(engine.parse_to_numpy(batch, opt, mode, abi.OUT_GROUPED), d, frames,
+                                  f"edge grouped layout {k} {mode}")
+    torch.cuda.synchronize()
