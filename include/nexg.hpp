@@ -904,6 +904,72 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         return out;
     }
 
+    // The parse result of every host frame as nexg_desc (layers, checksum
+    // verdicts, payload location: what Frame::try_from_buf reports, without
+    // the header fields), through the grouped output the bench times
+    // (NEXG_OUT_GROUPED: 17 B per 64 single-shape frames) decoded on the host
+    std::vector<nexg_desc> descriptors(const std::vector<std::vector<uint8_t>>& frames, ParseOption option = {},
+                                       ParseMode mode = ParseMode::Lenient) {
+        DeviceScope ds(device_);
+        const uint64_t n = frames.size();
+        std::vector<nexg_desc> out(n);
+        if (n == 0) return out;
+        HostBatch hb(*this, frames);
+        const uint64_t bytes = NEXG_GROUPED_BYTES(n);
+        void* d_g = scratch(3, bytes);
+        parse(hb.fb, option, mode, NEXG_OUT_GROUPED, d_g);
+        std::vector<uint8_t> g(bytes);
+        check_hip(hipMemcpyAsync(g.data(), d_g, bytes, hipMemcpyDeviceToHost, stream_), "D2H");
+        check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+        const nexg_desc* exc = reinterpret_cast<const nexg_desc*>(g.data() + NEXG_GROUPED_EXC_OFFSET(n));
+        const uint32_t fl = option.flags(mode);
+        for (uint64_t g0 = 0; g0 < n; g0 += 64) {
+            uint32_t k = 0;  // the group's exceptions, in frame order
+            for (uint64_t i = g0; i < n && i < g0 + 64; i++)
+                if (!nexg_sparse_decode(nexg_grouped_code(g.data(), n, i), (uint32_t)frames[i].size(), fl,
+                                        (uint32_t)option.offset, &out[i]))
+                    out[i] = exc[g0 + k++];
+        }
+        return out;
+    }
+
+    // udp_ping's probe batch: one source address and port pair (udp_ping.rs:30-31,
+    // 54-66) and a destination per target, identification 0 (the
+    // Ipv4PacketBuilder default): the builder reads 4 B per frame
+    Result<std::vector<std::vector<uint8_t>>, BuildError> build_udp_probes(const Ipv4Addr& source,
+                                                                           const std::vector<Ipv4Addr>& targets,
+                                                                           uint16_t src_port, uint16_t dst_port,
+                                                                           const UdpPingShape& shape) {
+        DeviceScope ds(device_);
+        if (28ull + shape.payload.size() > 65535ull) return BuildError::LengthOverflow;
+        const uint64_t n = targets.size();
+        const uint32_t L = 42u + (uint32_t)shape.payload.size();
+        if (n == 0) return std::vector<std::vector<uint8_t>>{};
+        std::vector<uint32_t> dst(n);
+        for (uint64_t i = 0; i < n; i++) {
+            const auto& b = targets[i].octets;
+            dst[i] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+        }
+        void* d_dst = upload(6, dst.data(), n * 4);
+        void* d_pl = shape.payload.empty() ? nullptr : upload(10, shape.payload.data(), shape.payload.size());
+        void* d_out = scratch(11, (uint64_t)n * L);
+        nexg_udp4_build p{};
+        p.dst_ip = static_cast<const uint32_t*>(d_dst);
+        p.def_src_ip = (uint32_t)source.octets[0] << 24 | (uint32_t)source.octets[1] << 16 |
+                       (uint32_t)source.octets[2] << 8 | source.octets[3];
+        p.def_src_port = src_port;
+        p.def_dst_port = dst_port;
+        p.payload = static_cast<const uint8_t*>(d_pl);
+        p.payload_len = (uint32_t)shape.payload.size();
+        memcpy(p.def_src_mac, shape.src_mac.data(), 6);
+        memcpy(p.def_dst_mac, shape.dst_mac.data(), 6);
+        p.ttl = shape.ttl;
+        p.ip_flags = shape.ip_flags;
+        p.count = n;
+        check(nexg_build_udp4_batch(ctx_, &p, static_cast<uint8_t*>(d_out), L, stream_), "nexg_build_udp4_batch");
+        return download_frames(d_out, n, L);
+    }
+
     // udp_ping's build (udp_ping.rs:68-109) for every tuple: 42 + payload bytes
     // each; BuildError::LengthOverflow when the UDP / IPv4 length would pass
     // 65535 (builder/udp.rs:83, builder/ipv4.rs:153)

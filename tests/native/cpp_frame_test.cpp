@@ -338,6 +338,33 @@ int main(int argc, char** argv) {
         big.payload.assign(65535 - 28 + 1, 0);
         auto over = eng->build_udp_ping({t}, big);
         CHECK(over.is_err() && over.error() == BuildError::LengthOverflow);
+        // udp_ping's probe batch (one source and port pair, a destination per
+        // target): the tuple builder's bytes for the same tuples, 300 targets
+        std::vector<Ipv4Addr> targets;
+        std::vector<UdpPingTuple> tuples;
+        for (uint32_t k = 0; k < 300; k++) {
+            targets.push_back(Ipv4Addr{{10, (uint8_t)(k >> 8), (uint8_t)k, 7}});
+            UdpPingTuple u = t;
+            u.destination = targets.back();
+            tuples.push_back(u);
+        }
+        auto probes = eng->build_udp_probes(t.source, targets, 53443, 33435, shape);
+        auto same = eng->build_udp_ping(tuples, shape);
+        CHECK(probes.is_ok() && same.is_ok() && probes.value() == same.value());
+        // descriptors through the grouped output == the records' descriptors,
+        // single-shape groups (the probes) and mixed groups (the golden frames)
+        std::vector<std::vector<uint8_t>> mix = probes.value();
+        for (int k = 0; k < 3; k++)
+            for (const auto& kv : fx)
+                if (kv.second.flags == 0) mix.push_back(kv.second.bytes);  // the golden frames parsed by default
+        const auto desc = eng->descriptors(mix);
+        std::vector<nexg_record> rec(mix.size());
+        for (size_t i = 0; i < mix.size(); i++) nexo_parse_frame(mix[i].data(), (uint32_t)mix[i].size(), 0, 0, &rec[i]);
+        bool eq = desc.size() == mix.size();
+        for (size_t i = 0; eq && i < mix.size(); i++)
+            eq = desc[i].flags == rec[i].flags && desc[i].payload_off == rec[i].payload_off &&
+                 desc[i].payload_len == rec[i].payload_len;
+        CHECK(eq);
     }
     if (gpu) {  // examples/arp.rs / examples/ndp.rs probes, bytes == the oracle's restatement
         ArpProbeShape as;
