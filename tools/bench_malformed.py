@@ -63,12 +63,16 @@ def main():
             return e0.elapsed_time(e1) / 1e3 / args.steps
         rounds = 2 if len(engines) > 1 else 1
         times, same = [], []
-        for _ in range(rounds):
-            row = []
-            for j, e in enumerate(engines):
-                row.append(timed(e))
+        ref = None
+        for rnd in range(rounds):
+            # A B, then B A: the build measured first in a round pays for the
+            # batch's first launches, so the order alternates
+            order = list(range(len(engines)))[:: -1 if rnd % 2 else 1]
+            row = [0.0] * len(engines)
+            for j in order:
+                row[j] = timed(engines[j])
                 if len(engines) > 1:  # every build's output equals the first build's, byte for byte
-                    if j == 0:
+                    if ref is None:
                         ref = out.clone()
                     else:
                         same.append(bool(torch.equal(out, ref)))

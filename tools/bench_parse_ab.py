@@ -47,8 +47,9 @@ def main():
                 ref = out.clone() if ref is None else ref
                 assert torch.equal(out, ref), f"{l}: output differs"
         times = {l: [] for l in libs}
-        for _ in range(args.rounds):
-            for l, e in zip(libs, engines):
+        for rnd in range(args.rounds):
+            pairs = list(zip(libs, engines))
+            for l, e in (pairs[::-1] if rnd % 2 else pairs):  # alternate the order (first-measured bias)
                 for _ in range(args.warmup):
                     e.parse(b, out_kind=ok, out=out, stream=s)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
