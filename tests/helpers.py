@@ -539,4 +539,37 @@ def fastpath_edge_frames(rng):
                     pay = bytes(rng.integers(0, 256, int(rng.choice([0, 5, 40, 600])), dtype=np.uint8))
                     seg = _tcp(pay, opts, doff=doff)
                     f.append(_eth(_ipv4(seg, 6)) if fam == 4 else _eth(_ipv6(seg, 6), 0x86DD))
+    f += ipv4_option_frames(rng)
+    return f
+
+
+def ipv4_option_frames(rng):
+    """IPv4 headers with options (IHL 6..15) ahead of UDP / TCP / ICMP / other
+    protocols: Router Alert, NOP runs, EOL early (re-serialised header shorter
+    than IHL: payload bytes in its checksum, Q17 when the payload is shorter
+    still), timestamps, TLVs of length 0 / 1 / past the header / cut by it,
+    random bytes; total lengths exact, 0, short of the frame (padding) and
+    past it; payloads of 0..600 B."""
+    f = []
+    for ihl in range(6, 16):
+        ol = 4 * (ihl - 5)
+        lists = [bytes([0x94, 4, 0, 0]) + bytes([1] * (ol - 4)), bytes([1] * ol), bytes([0]) + bytes([7] * (ol - 1)),
+                 bytes([1] * (ol - 1)) + bytes([0x44]), bytes([0x44, ol, 5, 0x10]) + bytes(ol - 4),
+                 bytes([0x83, 0]) + bytes(ol - 2), bytes([0x83, 1]) + bytes(ol - 2),
+                 bytes([0x83, ol + 1]) + bytes(ol - 2), bytes([1, 0x88, 3, 9, 9]) + bytes([0]) * (ol - 5) if ol >= 8
+                 else bytes([0x88, 4, 9, 9]), bytes([1, 1, 0]) + bytes([0xFF]) * (ol - 3),
+                 bytes(rng.integers(0, 256, ol, dtype=np.uint8))]
+        for opts in lists:
+            for proto in (17, 6, 1, 200):
+                for plen in (0, 3, 7, 9, 20, 45, 600):
+                    body = bytes(rng.integers(0, 256, plen, dtype=np.uint8))
+                    seg = (_udp(body) if proto == 17 else _tcp(body) if proto == 6 and plen >= 20 else
+                           _tcp(body[:4], bytes([1, 1, 8, 10]) + body[4:12]) if proto == 6 and plen == 9 else
+                           bytes([8, 0, 0, 0]) + body if proto == 1 else body)
+                    ip = _ipv4(seg, proto, ihl=ihl, opts=opts)
+                    f.append(_eth(ip))
+                    tot = len(ip)
+                    for t in (0, tot - 1, tot + 5, 4 * ihl):
+                        f.append(_eth(_ipv4(seg, proto, ihl=ihl, opts=opts, total=t)))
+                    f.append(_eth(ip) + bytes(rng.integers(0, 256, int(rng.integers(1, 30)), dtype=np.uint8)))
     return f
