@@ -517,7 +517,8 @@ def fastpath_edge_frames(rng):
     TCP / UDP / ICMPv6 / no-next-header / another extension, with payload
     lengths that end exactly at, one before and past its end; TCP data offsets
     6..15 whose first option is a TLV of length 0, 1, 2, the list's length,
-    one past it and 255 (walk fails or goes on), behind NOP / EOL too."""
+    one past it and 255 (walk fails or goes on), behind NOP / EOL too; IPv4
+    option lists (ipv4_option_frames: declined to the generic walk)."""
     f = [bytes(rng.integers(0, 256, n, dtype=np.uint8)) for n in range(14)]
     f += [bytes(range(12)) + bytes([0x86, 0xDD]) + bytes(rng.integers(0, 256, k, dtype=np.uint8)) for k in (0, 39, 41)]
     for nh in (0, 43, 44, 60):
