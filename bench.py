@@ -216,17 +216,20 @@ def load_traffic(workload, out_kind):
         return None
 
 
-def timed(step, steps, warmup, stream, device, host_clock=False, with_local=False):
-    """W untimed steps, then exactly K steps bracketed by barrier + sync on
-    both sides (nex_amd.dist.timed_steps). Returns (max-over-ranks elapsed
-    seconds, per-launch kernel seconds from HIP events on the launch stream)."""
+def timed(step, steps, warmup, stream, device, host_clock=False, with_local=False, stats=None):
+    """W untimed steps (continued until WARMUP_SECONDS have passed), then
+    exactly K steps bracketed by barrier + sync on both sides
+    (nex_amd.dist.timed_steps). Returns (max-over-ranks elapsed seconds,
+    per-launch kernel seconds from HIP events on the launch stream); `stats`
+    receives the warmup actually run."""
     import torch
     from nex_amd import dist
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     elapsed, local = dist.timed_steps(step, steps, warmup, sync=lambda: torch.cuda.synchronize(device),
                                       device=device, before=lambda: ev0.record(stream),
-                                      after=lambda: ev1.record(stream), warmup_seconds=WARMUP_SECONDS)
+                                      after=lambda: ev1.record(stream), warmup_seconds=WARMUP_SECONDS,
+                                      stats=stats)
     kernel_s = ev0.elapsed_time(ev1) / 1e3 / steps
     if host_clock:  # copies + kernels on side streams: the host clock is the measure
         kernel_s = local / steps
@@ -263,44 +266,69 @@ def stream_ceilings(eng, batch, args, stream, device):
     return r
 
 
-def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world):
-    """configs[2] beside the default configs[1] run (the metric names both
-    64B and IMIX): 16M IMIX frames per GPU, same output kind, same timing
-    discipline. Returns the object rank 0 adds to the JSON line."""
+def parse_object(eng, args, batch, out_kind, stream, device, rank, world, workload, traffic_key,
+                 warmup, steps, cpu_label=None, extra=None):
+    """One parse workload beside the default run, same output kind and timing
+    discipline: W untimed launches (+ the warmup floor), K timed, max over
+    ranks. Returns the object rank 0 adds to the JSON line (None elsewhere)."""
     import torch
-    from nex_amd import abi, dist
+    from nex_amd import dist
     from nex_amd.engine import Engine
-    batch = eng.gen_batch(abi.WL_IMIX, F, first_index=first)
-    out = torch.empty(Engine.out_bytes(out_kind, F), dtype=torch.uint8, device=device)
+    n = batch.count
+    out = torch.empty(Engine.out_bytes(out_kind, n), dtype=torch.uint8, device=device)
     torch.cuda.synchronize(device)
     alg = batch.total_bytes
-    # the first ~30 launches of a 6-GB batch (about 30 ms of back-to-back
-    # load) run 5-25 % slow before the chip settles (profiles/r01_staging/
-    # imix_ramp.txt, profiles/r03_final/imix_ramp.txt), so the IMIX line warms
-    # up for IMIX_WARMUP untimed launches
-    steps = max(1, args.steps // 2)
+    wstats = {}
     elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
-                              steps, max(IMIX_WARMUP, args.warmup), stream, device)
-    tp = dist.throughput(F, alg, steps, elapsed, device)
+                              steps, warmup, stream, device, stats=wstats)
+    tp = dist.throughput(n, alg, steps, elapsed, device)
     per_rank = dist.all_ranks(round(kernel_s * 1e3, 4), device)
+    share = None
+    if extra is not None and extra.pop("shape_share", False):  # share of frames with a shape code
+        from nex_amd import abi
+        torch.cuda.synchronize(device)
+        if out_kind == abi.OUT_SPARSE:
+            share = round(float((out[:n] != 0).float().mean().item()), 4)
+        elif out_kind == abi.OUT_GROUPED:
+            share = round(float((abi.grouped_codes(out.cpu().numpy(), n) != 0).mean()), 4)
     if rank != 0:
         return None
     ach = alg / kernel_s / 1e9
-    r = {"workload": f"configs[2]: {F} IMIX frames per GPU (64/576/1500 at 7:4:1, "
-                     "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table; " + OUT_NOTE[args.out],
-         "value": tp["value"], "unit": "Mpkt/s", "steps": steps, "ms_per_step": tp["ms_per_step"],
-         "gib_s": tp["gib_s"], "bytes_per_gpu": alg,
+    r = {"workload": workload, "value": tp["value"], "unit": "Mpkt/s", "steps": steps,
+         "ms_per_step": tp["ms_per_step"], "gib_s": tp["gib_s"], "frames_per_gpu": n, "bytes_per_gpu": alg,
+         "warmup_run": wstats,
          "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("imix", args.out),
+                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic(traffic_key, args.out),
                       "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg}}
+    if share is not None:
+        r["sparse_shape_share"] = share
+    if extra:
+        r.update(extra)
     if world > 1:
         r["per_rank_kernel_ms"] = per_rank
-    if world == 1 and not args.no_cpu_baseline:
+    if cpu_label and world == 1 and not args.no_cpu_baseline:
         try:
-            r["cpu_baseline"] = cpu_baseline(batch, "imix", 1 << 20, args.cpu_seconds / 2, host_threads())
+            r["cpu_baseline"] = cpu_baseline(batch, cpu_label, 1 << 20, args.cpu_seconds / 2, host_threads())
         except Exception as e:
             r["cpu_baseline"] = {"value": None, "error": repr(e)}
     return r
+
+
+IMIX_DESC = "(64/576/1500 at 7:4:1, {IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table; "
+
+
+def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world):
+    """configs[2] beside the default configs[1] run (the metric names both
+    64B and IMIX): 16M IMIX frames per GPU, same output kind, same timing
+    discipline. The first ~30 launches of a 6-GB batch (about 30 ms of
+    back-to-back load) run 5-25 % slow before the chip settles
+    (profiles/r01_staging/imix_ramp.txt, profiles/r03_final/imix_ramp.txt),
+    so the IMIX objects warm up for IMIX_WARMUP untimed launches."""
+    from nex_amd import abi
+    batch = eng.gen_batch(abi.WL_IMIX, F, first_index=first)
+    return parse_object(eng, args, batch, out_kind, stream, device, rank, world,
+                        f"configs[2]: {F} IMIX frames per GPU " + IMIX_DESC + OUT_NOTE[args.out], "imix",
+                        max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2), cpu_label="imix")
 
 
 def malformed_line(eng, args, F, first, out_kind, stream, device, rank, world):
@@ -308,35 +336,49 @@ def malformed_line(eng, args, F, first, out_kind, stream, device, rank, world):
     IMIX frames carry one structural mutation) at the configs[2] size, same
     output kind and timing: the cost of the frames that leave the canonical
     fast paths for the generic parse core. 1M distinct frames tiled to F."""
-    import torch
-    from nex_amd import abi, dist, workloads
-    from nex_amd.engine import Engine
+    from nex_amd import abi, workloads
     distinct = min(F, 1 << 20)
     mix, counts = workloads.malformed_mix(eng, distinct, seed=abi.DEFAULT_SEED + first)
     batch = workloads.tiled(mix, max(1, F // distinct))
-    n = batch.count
-    out = torch.empty(Engine.out_bytes(out_kind, n), dtype=torch.uint8, device=device)
-    alg = batch.total_bytes
-    steps = max(1, args.steps // 2)
-    elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
-                              steps, max(IMIX_WARMUP, args.warmup), stream, device)
-    tp = dist.throughput(n, alg, steps, elapsed, device)
-    canonical = None
-    if out_kind == abi.OUT_SPARSE:  # share of frames with a shape code (no exception slot)
-        canonical = round(float((out[:n] != 0).float().mean().item()), 4)
-    elif out_kind == abi.OUT_GROUPED:
-        torch.cuda.synchronize(device)
-        canonical = round(float((abi.grouped_codes(out.cpu().numpy(), n) != 0).mean()), 4)
-    if rank != 0:
-        return None
-    ach = alg / kernel_s / 1e9
-    return {"workload": f"SURVEY App. C malformed mix: {n} frames per GPU ({distinct} distinct, tiled), "
-                        f"IMIX with half the frames mutated {counts}; " + OUT_NOTE[args.out],
-            "value": tp["value"], "unit": "Mpkt/s", "steps": steps, "ms_per_step": tp["ms_per_step"],
-            "gib_s": tp["gib_s"], "bytes_per_gpu": alg, "sparse_shape_share": canonical,
-            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("malformed", args.out),
-                         "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg}}
+    return parse_object(eng, args, batch, out_kind, stream, device, rank, world,
+                        f"SURVEY App. C malformed mix: {batch.count} frames per GPU ({distinct} distinct, tiled), "
+                        f"IMIX with half the frames mutated {counts}; " + OUT_NOTE[args.out], "malformed",
+                        max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2), extra={"shape_share": True})
+
+
+def real_traffic_batch(eng, F, first):
+    from nex_amd import abi, workloads
+    distinct = min(F, 1 << 20)
+    mix, counts = workloads.real_traffic(eng, distinct, seed=abi.DEFAULT_SEED + 7 + first)
+    batch = workloads.tiled(mix, max(1, F // distinct))
+    desc = (f"real-traffic TCP shapes: {batch.count} IMIX frames per GPU ({distinct} distinct, tiled) whose TCP "
+            f"segments carry option lists ({int(workloads.REAL_TRAFFIC_SHARE * 100)} %: NOP NOP timestamps, "
+            f"NOP NOP SACK 1-4 blocks, MSS alone; tcp.rs:731-836) {counts}, checksums made valid by "
+            "nexg_recompute_checksums_batch; ")
+    return batch, desc
+
+
+def real_traffic_line(eng, args, F, first, out_kind, stream, device, rank, world):
+    """IMIX with the TCP option lists real segments carry (VERDICT r03
+    missing 3), same output kind and timing as the IMIX object."""
+    batch, desc = real_traffic_batch(eng, F, first)
+    return parse_object(eng, args, batch, out_kind, stream, device, rank, world, desc + OUT_NOTE[args.out],
+                        "real_traffic", max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2),
+                        cpu_label="real_traffic", extra={"shape_share": True})
+
+
+LARGE_FRAMES = 52 << 20  # 3.25 GiB of 64-B frames: 13x the 256-MiB Infinity Cache
+
+
+def large_line(eng, args, first, out_kind, stream, device, rank, world):
+    """The UDP64 headline at 52M frames (3.25 GiB, 13x the 256-MiB MALL): a
+    batch no cache can hold between launches, so its rate is HBM's."""
+    from nex_amd import abi
+    batch = eng.gen_batch(abi.WL_UDP64, LARGE_FRAMES, first_index=first * (LARGE_FRAMES // (16 << 20)))
+    return parse_object(eng, args, batch, out_kind, stream, device, rank, world,
+                        f"configs[1] at {LARGE_FRAMES} x 64-B Eth/IPv4/UDP frames per GPU (3.25 GiB, 13x the "
+                        "256-MiB Infinity Cache: no cross-launch cache reuse possible); " + OUT_NOTE[args.out],
+                        "udp64_large", args.warmup, args.steps)
 
 
 def main():
@@ -346,7 +388,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=25,
                     help="untimed steps; a freshly generated batch runs its first launches "
                          "slow (clock ramp), profiles/r01_staging/imix_ramp.txt")
-    ap.add_argument("--workload", choices=["udp64", "imix", "imix_pcap", "malformed", "ser"], default="udp64")
+    ap.add_argument("--workload", choices=["udp64", "imix", "imix_pcap", "malformed", "real_traffic", "ser"], default="udp64")
     ap.add_argument("--frames", type=int, default=16 << 20, help="frames per GPU")
     ap.add_argument("--out", choices=list(OUT_KINDS), default="grouped",
                     help="output kind (default: lossless grouped descriptors, NEXG_OUT_GROUPED)")
@@ -354,6 +396,10 @@ def main():
                     help="skip the configs[2] IMIX line reported beside the default UDP64 run")
     ap.add_argument("--no-malformed", action="store_true",
                     help="skip the malformed-mix line (fallback cost) reported beside the default run")
+    ap.add_argument("--no-real", action="store_true",
+                    help="skip the real-traffic TCP-options line reported beside the default run")
+    ap.add_argument("--no-large", action="store_true",
+                    help="skip the 52M-frame (3.25 GiB) UDP64 line reported beside the default run")
     ap.add_argument("--no-ser", action="store_true",
                     help="skip the configs[3] serialize line reported beside the default run")
     ap.add_argument("--ser-shape", choices=["probe", "tuples"], default="probe",
@@ -366,13 +412,17 @@ def main():
     ap.add_argument("--e2e-chunk", type=int, default=1 << 20, help="frames per pipelined chunk")
     args = ap.parse_args()
 
+    # --gpus N > 1 outside torchrun: start N ranks as a child process and relay
+    # rank 0's line (this process makes no GPU call); exits unless this
+    # process is the bench itself (--gpus 1, or a rank whose WORLD_SIZE == N)
+    from nex_amd import launch
+    launch.main_or_spawn(sys.argv[1:], args.gpus, os.path.abspath(__file__))
+
     import torch
     from nex_amd import abi, dist
     from nex_amd.engine import Engine
 
     rank, world, local = dist.env_rank_world()
-    if world != args.gpus and rank == 0:
-        log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
     local = dist.device_index(local)  # 1:1 on a full node; folded for a shared-GPU rehearsal
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
@@ -384,13 +434,16 @@ def main():
     out_kind = OUT_KINDS[args.out]
     width = {"desc": 8, "record": 64, "flags": 4, "verdict": 2, "sparse": 1, "grouped": 1}[args.out]
 
-    if args.workload in ("udp64", "imix", "imix_pcap", "malformed"):
+    if args.workload in ("udp64", "imix", "imix_pcap", "malformed", "real_traffic"):
         wl = abi.WL_UDP64 if args.workload == "udp64" else abi.WL_IMIX
         if args.workload == "malformed":  # the malformed object's batch as the main workload (PMC / rocprof)
             from nex_amd import workloads
             distinct = min(F, 1 << 20)
             mix, mcounts = workloads.malformed_mix(eng, distinct, seed=abi.DEFAULT_SEED + first)
             batch = workloads.tiled(mix, max(1, F // distinct))
+            F = batch.count
+        elif args.workload == "real_traffic":  # the real_traffic object's batch (PMC / rocprof)
+            batch, rdesc = real_traffic_batch(eng, F, first)
             F = batch.count
         else:
             batch = eng.gen_batch(wl, F, first_index=first, record_gap=16 if args.workload == "imix_pcap" else 0)
@@ -408,9 +461,10 @@ def main():
         elif args.workload == "malformed":
             cfg = {"workload": f"SURVEY App. C malformed mix: {F} frames per GPU ({distinct} distinct, tiled), "
                                f"IMIX with half the frames mutated {mcounts}; " + OUT_NOTE[args.out]}
+        elif args.workload == "real_traffic":
+            cfg = {"workload": rdesc + OUT_NOTE[args.out]}
         elif args.workload == "imix":
-            cfg = {"workload": f"configs[2]: {F} IMIX frames per GPU (64/576/1500 at 7:4:1, "
-                               "{IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table; " + OUT_NOTE[args.out]}
+            cfg = {"workload": f"configs[2]: {F} IMIX frames per GPU " + IMIX_DESC + OUT_NOTE[args.out]}
         else:
             cfg = {"workload": f"configs[4] ingest shape: {F} IMIX frames per GPU, each after a 16-B "
                                "capture record header (nexg_pcap_read_raw layout: offsets + lengths + "
@@ -470,8 +524,10 @@ def main():
         cfg["workload"] += "; END-TO-END: frames in pinned host memory, chunked H2D/parse/D2H"
         cfg["e2e_chunk_frames"] = C
 
-    warm = max(args.warmup, IMIX_WARMUP) if args.workload in ("imix", "imix_pcap", "malformed") and not args.e2e else args.warmup  # see imix_line
-    elapsed, kernel_s, local_s = timed(step, args.steps, warm, stream, device, host_clock=args.e2e, with_local=True)
+    warm = max(args.warmup, IMIX_WARMUP) if args.workload in ("imix", "imix_pcap", "malformed", "real_traffic") and not args.e2e else args.warmup  # see imix_line
+    wstats = {}
+    elapsed, kernel_s, local_s = timed(step, args.steps, warm, stream, device, host_clock=args.e2e, with_local=True,
+                                       stats=wstats)
     tp = dist.throughput(F, alg_bytes, args.steps, elapsed, device)
     # each rank's kernel time and its own timed-region wall time (balance across GPUs)
     per_rank = {"kernel_ms": dist.all_ranks(round(kernel_s * 1e3, 4), device),
@@ -487,14 +543,21 @@ def main():
     malformed = None
     if args.workload == "udp64" and not args.e2e and not args.no_malformed and F == 16 << 20:
         malformed = malformed_line(eng, args, F, first, out_kind, stream, device, rank, world)
+    real = None
+    if args.workload == "udp64" and not args.e2e and not args.no_real and F == 16 << 20:
+        real = real_traffic_line(eng, args, F, first, out_kind, stream, device, rank, world)
     ser = None
     if args.workload == "udp64" and not args.e2e and not args.no_ser and F == 16 << 20:
         ser = ser_line(eng, args, F, first, stream, device, rank, world)
+    large = None
+    if args.workload == "udp64" and not args.e2e and not args.no_large and F == 16 << 20:
+        large = large_line(eng, args, first, out_kind, stream, device, rank, world)
 
     if rank != 0:
         return
     achieved = alg_bytes / kernel_s / 1e9
-    traffic = load_traffic(args.workload, args.out)
+    traffic = load_traffic("udp64_large" if args.workload == "udp64" and F == LARGE_FRAMES else args.workload,
+                           args.out)
     res = {
         "metric": METRIC if args.workload != "ser" else "Mpkt/s build+checksum udp_ping-shape frames",
         "value": tp["value"],
@@ -510,6 +573,9 @@ def main():
         "data": "synthetic: SURVEY.md App. C generator (splitmix64, seed 0x6E6578), generated on device",
         "config": cfg,
         "gib_s": tp["gib_s"],
+        # untimed launches actually run before the K timed ones: W, continued
+        # in batches of 32 until WARMUP_SECONDS have passed
+        "warmup_run": dict(wstats, floor_s=WARMUP_SECONDS),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
@@ -549,8 +615,12 @@ def main():
         res["imix"] = imix
     if malformed is not None:
         res["malformed"] = malformed
+    if real is not None:
+        res["real_traffic"] = real
     if ser is not None:
         res["ser"] = ser
+    if large is not None:
+        res["large"] = large
     print(json.dumps(res), flush=True)
 
 

@@ -324,11 +324,11 @@ static inline uint8_t nexg_grouped_code(const void* out, uint64_t count, uint64_
     const uint8_t head = o[g];
     if (!head) return o[NEXG_GROUPED_CODE_OFFSET(count) + i];
     const uint8_t* m = o + NEXG_GROUPED_MASK_OFFSET(count) + 16u * g;
-    const uint32_t b = (uint32_t)(i & 63u), w = b >> 5, sh = b & 31u;
-    uint32_t ip, l4;
-    __builtin_memcpy(&ip, m + 4u * w, 4);
-    __builtin_memcpy(&l4, m + 8u + 4u * w, 4);
-    return (uint8_t)(head | (((ip >> sh) & 1u) ? NEXG_SPARSE_IP_OK : 0u) | (((l4 >> sh) & 1u) ? NEXG_SPARSE_L4_OK : 0u));
+    /* the masks are little-endian words: bit b of a 64-bit mask is bit b % 8
+     * of its byte b / 8 */
+    const uint32_t b = (uint32_t)(i & 63u), byte = b >> 3, sh = b & 7u;
+    const uint32_t ip = (m[byte] >> sh) & 1u, l4 = (m[8u + byte] >> sh) & 1u;
+    return (uint8_t)(head | (ip ? NEXG_SPARSE_IP_OK : 0u) | (l4 ? NEXG_SPARSE_L4_OK : 0u));
 }
 
 /* FrameSlice::try_from_buf (frame.rs:84-287) per frame, out_kind

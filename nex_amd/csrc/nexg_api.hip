@@ -285,7 +285,8 @@ int nexg_build_udp6_batch(nexg_ctx* ctx, const nexg_udp6_build* p, uint8_t* out,
     if (!ctx || !p) return NEXG_EINVAL;
     if (8ull + p->payload_len > 65535ull)
         return fail(ctx, NEXG_ERANGE, "UDP/IPv6 length overflow%s", nullptr);
-    if (p->count && (!p->dst_ip || !out))
+    // src_ip is per frame here (no def_src_ip: only the IPv4 probe batch has one)
+    if (p->count && (!p->src_ip || !p->dst_ip || !out))
         return fail(ctx, NEXG_EINVAL, "NULL address array or output%s", nullptr);
     if (((reinterpret_cast<uint64_t>(p->src_ip) | reinterpret_cast<uint64_t>(p->dst_ip)) & 3u) != 0)
         return fail(ctx, NEXG_EINVAL, "address arrays must be 4-B aligned%s", nullptr);

@@ -54,24 +54,29 @@ def init(backend: str = None, force: bool = False):
 
 
 def timed_steps(step, steps: int, warmup: int, sync=None, device=None, before=None, after=None,
-                warmup_seconds: float = 0.0):
+                warmup_seconds: float = 0.0, stats=None):
     """bench.py's timing discipline: `warmup` untimed steps (continued, in
     batches of 32, until at least `warmup_seconds` of wall time have passed),
     then exactly `steps` steps bracketed by sync + barrier + sync on both
     sides; returns (max-over-ranks elapsed seconds, this rank's elapsed
     seconds). `sync` waits for this rank's device work (torch.cuda.synchronize
     on a GPU); before/after run inside the timed bracket around the steps (HIP
-    event records)."""
+    event records). A `stats` dict receives the warmup actually run
+    (`warmup_steps`, `warmup_s`)."""
     import time
     sync = sync or (lambda: None)
     t_w = time.perf_counter()
+    n_w = warmup
     for _ in range(warmup):
         step()
     sync()
     while time.perf_counter() - t_w < warmup_seconds:
         for _ in range(32):
             step()
+        n_w += 32
         sync()
+    if stats is not None:
+        stats.update(warmup_steps=n_w, warmup_s=round(time.perf_counter() - t_w, 4))
     barrier(device)
     sync()
     t0 = time.perf_counter()

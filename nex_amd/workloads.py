@@ -155,3 +155,25 @@ def tiled(batch, times: int):
                      [torch.tensor([times * span], dtype=base.dtype, device=base.device)])
     pad = torch.zeros(16, dtype=data.dtype, device=data.device)
     return FrameBatch(data=torch.cat([data, pad])[: times * span], count=n * times, offsets=offs)
+
+
+#: the real-traffic TCP option shapes of tcp.rs:731-836 timed in bench.py's
+#: `real_traffic` object: 70 % of the IMIX's TCP segments carry one of them
+REAL_TRAFFIC_KINDS = EXTRA
+REAL_TRAFFIC_SHARE = 0.7
+
+
+def real_traffic(engine, count: int, seed: int = abi.DEFAULT_SEED, fix_checksums: bool = True):
+    """IMIX whose TCP segments carry the option lists of real traffic
+    (timestamps, SACK blocks, MSS; `malformed_mix` kinds tcp_ts / tcp_sack /
+    tcp_mss at REAL_TRAFFIC_SHARE), with the IP and L4 checksums made valid
+    again on the device by nexg_recompute_checksums_batch (the mutable views'
+    recompute_checksum, ipv4.rs:669-679 / tcp.rs:1009-1040), as a capture of
+    healthy traffic would hold them. (FrameBatch, per-kind counts)."""
+    import torch
+    batch, counts = malformed_mix(engine, count, seed=seed, mutate_share=REAL_TRAFFIC_SHARE,
+                                  kinds=REAL_TRAFFIC_KINDS)
+    if fix_checksums:
+        engine.recompute_checksums(batch, report=False)
+        torch.cuda.synchronize(engine.torch_device)
+    return batch, counts

@@ -154,3 +154,24 @@ def test_ndp_ns_rejects_ipv4(engine, ns_inputs):
     import ctypes
     rc = engine.lib.nexg_build_ndp_ns_batch(engine.ctx, ctypes.byref(p), ctypes.c_void_p(out.data_ptr()), 86, None)
     assert rc == abi.EINVAL
+
+
+def test_udp6_rejects_null_src_ip(engine):
+    """nexg_build_udp6_batch has no def_src_ip (only the IPv4 probe batch
+    does): a NULL per-frame source array is NEXG_EINVAL, not a device fault."""
+    import ctypes
+
+    import torch
+    dst = torch.zeros((4, 16), dtype=torch.uint8, device="cuda")
+    out = torch.empty(4 * 62, dtype=torch.uint8, device="cuda")
+    p = abi.Udp6Build()
+    p.src_ip, p.dst_ip = None, dst.data_ptr()
+    p.src_port = p.dst_port = p.src_mac = p.dst_mac = p.payload = None
+    p.payload_len, p.count, p.hop_limit = 0, 4, 64
+    rc = engine.lib.nexg_build_udp6_batch(engine.ctx, ctypes.byref(p), ctypes.c_void_p(out.data_ptr()), 62, None)
+    assert rc == abi.EINVAL
+    # the same call with the source array builds
+    p.src_ip = dst.data_ptr()
+    rc = engine.lib.nexg_build_udp6_batch(engine.ctx, ctypes.byref(p), ctypes.c_void_p(out.data_ptr()), 62, None)
+    assert rc == 0
+    torch.cuda.synchronize()

@@ -21,20 +21,25 @@ for s in ${STEPS:-tests}; do
     tests) step pytest_gpu 900 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench_udp64 500 python bench.py --steps 50 --cpu-seconds 5 ;;
+    driverbench) step bench_driver 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    newtests4) step pytest_new4 600 python -u -m pytest tests/test_gpu_tcp_options.py tests/test_gpu_build_probe.py -q -x --timeout 300 --timeout-method thread ;;
     malformed) step bench_malformed 500 python tools/bench_malformed.py ;;
     benchpcap) step bench_pcap 400 python bench.py --workload imix_pcap --steps 20 --cpu-seconds 5 ;;
     ser) step bench_ser 300 python bench.py --workload ser --steps 50 --no-cpu-baseline
          step bench_ser_tuples 300 python bench.py --workload ser --ser-shape tuples --steps 50 --no-cpu-baseline ;;
     e2e) step bench_e2e 400 python bench.py --e2e --steps 5 --warmup 2 --no-cpu-baseline
          step bench_e2e_imix 400 python bench.py --e2e --workload imix --steps 3 --warmup 1 --no-cpu-baseline ;;
-    rehearse2) step rehearse2 600 env NEXG_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 2 ;;
-    rehearse8) step rehearse8 900 env NEXG_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 8 --steps 10 --warmup 3 --cpu-seconds 2 ;;
+    # bench.py --gpus N starts its own N ranks (nex_amd/launch.py); gloo folds them onto the one GPU
+    rehearse2) step rehearse2 600 env NEXG_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 2 ;;
+    rehearse8) step rehearse8 900 env NEXG_DIST_BACKEND=gloo python bench.py --gpus 8 --steps 10 --warmup 3 --cpu-seconds 2 --no-large ;;
     benchimix) step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5 ;;
     pmc) step pmc 900 bash tools/pmc.sh ;;
-    prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed --no-ser
+    prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed --no-real --no-large --no-ser
           step prof_pcap 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pcap -o run -- python3 bench.py --workload imix_pcap --steps 60 --warmup 25 --no-cpu-baseline
           step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 60 --warmup 25 --no-cpu-baseline
           step prof_malformed 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_malformed -o run -- python3 bench.py --workload malformed --steps 60 --warmup 25 --no-cpu-baseline
+          step prof_real 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_real -o run -- python3 bench.py --workload real_traffic --steps 60 --warmup 25 --no-cpu-baseline
+          step prof_large 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_large -o run -- python3 bench.py --frames 54525952 --steps 60 --warmup 25 --no-cpu-baseline
           step prof_ser 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser -o run -- python3 bench.py --workload ser --steps 60 --warmup 25 --no-cpu-baseline
           step prof_ser_tuples 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser_tuples -o run -- python3 bench.py --workload ser --ser-shape tuples --steps 60 --warmup 25 --no-cpu-baseline ;;
   esac

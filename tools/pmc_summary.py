@@ -5,7 +5,8 @@ bytes for the parse path of each workload.
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. On gfx950, FETCH_SIZE counts
 exactly half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md
 §HBM), so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
-Only nexg:: kernels count; generator kernels (k_gen_*), calibration streams (k_probe_*) and torch setup kernels are skipped.
+Only nexg:: kernels count; generator kernels (k_gen_*), calibration streams (k_probe_*), the
+real-traffic batch's one checksum fix-up (k_recompute) and torch setup kernels are skipped.
 
 usage: tools/pmc_summary.py <pmc dir> <out dir>   (writes pmc_summary.json and
        traffic.json into <out dir>)
@@ -29,7 +30,8 @@ def main():
         vals = defaultdict(list)
         with open(path) as f:
             for r in csv.DictReader(f):
-                if "nexg::" not in r["Kernel_Name"] or "k_gen_" in r["Kernel_Name"] or "k_probe_" in r["Kernel_Name"]:
+                if "nexg::" not in r["Kernel_Name"] or "k_gen_" in r["Kernel_Name"] or "k_probe_" in r["Kernel_Name"] \
+                        or "k_recompute" in r["Kernel_Name"]:
                     continue
                 vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
         for kern, v in vals.items():
