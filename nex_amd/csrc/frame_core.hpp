@@ -237,7 +237,12 @@ struct SpanFrame {
     mutable SpanDeferred d{};
     mutable bool pend = false;
 
-    // one generic (flat) byte load from the slot or HBM: no divergent branch
+    // one generic (flat) byte load from the slot or HBM: no divergent branch.
+    // Only object start + non-negative index here: the compiler keeps one VGPR
+    // base per byte run and folds the run's index into the FLAT immediate, and
+    // a FLAT access takes its aperture from that VGPR base — a negative
+    // displacement of the LDS pointer (round 3's extension windows) put the
+    // base below the shared aperture and faulted (profiles/r03/ext_attempt/)
     NEXG_HD uint32_t u8(uint32_t i) const {
         NEXG_SPAN_PROBE(0, i >= kSlot);  // host harness counters (no-op in the library)
         const uint8_t* p = i < kSlot ? slot + i : g + i;
