@@ -113,6 +113,9 @@ def ser_step(eng, p, out, stream, shape):
     per frame, src_ip NULL -> one source, ports / id from the batch defaults:
     4 B of parameters read per frame); `tuples` = a full per-frame 5-tuple +
     IPv4 id (14 B read per frame)."""
+    if shape == "tuples_aos":  # p[5]: the same tuples packed as 16-B records
+        return lambda: eng.build_udp4_tuples(p[5], src_mac=SER_MACS[0], dst_mac=SER_MACS[1], ip_flags=2, out=out,
+                                             stream=stream)
     if shape == "probe":
         return lambda: eng.build_udp4(None, p[1], def_src_ip=SER_SRC_IP, def_src_port=SER_PORTS[0],
                                       def_dst_port=SER_PORTS[1], src_mac=SER_MACS[0], dst_mac=SER_MACS[1],
@@ -124,8 +127,19 @@ def ser_step(eng, p, out, stream, shape):
 SER_SHAPE_NOTE = {
     "probe": "udp_ping probe batch: a destination IPv4 per frame (4 B read), udp_ping's one source "
              "address, SRC_PORT/DST_PORT and id 0 from the batch defaults",
-    "tuples": "a full per-frame tuple (src/dst IPv4, ports, IPv4 id: 14 B read)"}
-SER_READ = {"probe": 4, "tuples": 14}
+    "tuples": "a full per-frame tuple (src/dst IPv4, ports, IPv4 id: 14 B read from five arrays)",
+    "tuples_aos": "a full per-frame tuple as one 16-B record (nexg_build_udp4_tuples: 16 B read, one "
+                  "dwordx4 load per frame)"}
+SER_READ = {"probe": 4, "tuples": 14, "tuples_aos": 16}
+#: tools/pmc.sh records the builds as <key>.desc (the build has no output kind)
+SER_TRAFFIC_KEY = {"probe": "ser_probe", "tuples": "ser", "tuples_aos": "ser_aos"}
+
+
+def ser_params(eng, F, first, shape):
+    """The serialize batch's parameters: the five SoA tuple arrays, plus the
+    same tuples packed as 16-B records for the AoS shape."""
+    p = eng.gen_udp4_params(F, first_index=first)
+    return tuple(p) + ((eng.pack_udp4_tuples(*p),) if shape == "tuples_aos" else ())
 
 
 def cpu_baseline_ser(params, count, seconds, nthreads=1):
@@ -168,13 +182,13 @@ def ser_line(eng, args, F, first, stream, device, rank, world):
     the host."""
     import torch
     from nex_amd import dist
-    p = eng.gen_udp4_params(F, first_index=first)
+    p = ser_params(eng, F, first, "tuples_aos")
     out = torch.empty(F * 42, dtype=torch.uint8, device=device)
     torch.cuda.synchronize(device)
     alg = F * 42
     ceil = write_ceiling(eng, out, args, stream, device)
     res = {}
-    for shape in ("probe", "tuples"):
+    for shape in ("probe", "tuples", "tuples_aos"):
         elapsed, kernel_s = timed(ser_step(eng, p, out, stream, shape), args.steps, args.warmup, stream, device)
         tp = dist.throughput(F, alg, args.steps, elapsed, device)
         if rank != 0:
@@ -186,21 +200,21 @@ def ser_line(eng, args, F, first, stream, device, rank, world):
              "gib_s": tp["gib_s"], "bytes_per_gpu": alg,
              "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(ach / HBM_PEAK_GBS, 4),
-                          "traffic": load_traffic("ser" if shape == "tuples" else "ser_probe", "desc"),
+                          "traffic": load_traffic(SER_TRAFFIC_KEY[shape], "desc"),
                           "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg,
                           "basis": f"bytes written (SURVEY.md 8(d) SER); parameter reads ({SER_READ[shape]} "
                                    "B/frame) not counted",
                           "stream_ceilings": dict(ceil, frac_of_write_only=round(ach / ceil["write_only_gbs"], 4))}}
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and shape != "tuples_aos":  # same tuples as "tuples"
             try:
-                hp = ser_probe_params(p) if shape == "probe" else p
+                hp = ser_probe_params(p) if shape == "probe" else p[:5]
                 r["cpu_baseline"] = cpu_baseline_ser(hp, 1 << 20, args.cpu_seconds / 4, host_threads())
             except Exception as e:
                 r["cpu_baseline"] = {"value": None, "error": repr(e)}
         res[shape] = r
     if rank != 0:
         return None
-    return dict(res["probe"], tuples=res["tuples"])
+    return dict(res["probe"], tuples=res["tuples"], tuples_aos=res["tuples_aos"])
 
 
 def load_traffic(workload, out_kind):
@@ -402,7 +416,7 @@ def main():
                     help="skip the 52M-frame (3.25 GiB) UDP64 line reported beside the default run")
     ap.add_argument("--no-ser", action="store_true",
                     help="skip the configs[3] serialize line reported beside the default run")
-    ap.add_argument("--ser-shape", choices=["probe", "tuples"], default="probe",
+    ap.add_argument("--ser-shape", choices=["probe", "tuples", "tuples_aos"], default="probe",
                     help="--workload ser: udp_ping probe batch (a destination per frame) or full tuples")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -470,7 +484,7 @@ def main():
                                "capture record header (nexg_pcap_read_raw layout: offsets + lengths + "
                                "monotone hint, headers read through, not counted); " + OUT_NOTE[args.out]}
     else:
-        p = eng.gen_udp4_params(F, first_index=first)
+        p = ser_params(eng, F, first, args.ser_shape)
         out = torch.empty(F * 42, dtype=torch.uint8, device=device)
         alg_bytes = F * 42
         batch = None
@@ -586,10 +600,10 @@ def main():
         res["roofline"]["basis"] = (f"bytes written (SURVEY.md 8(d) SER); parameter reads "
                                     f"({SER_READ[args.ser_shape]} B/frame) not counted")
         # the build has no output kind; tools/pmc.sh records it as ser.desc / ser_probe.desc
-        res["roofline"]["traffic"] = load_traffic("ser" if args.ser_shape == "tuples" else "ser_probe", "desc")
+        res["roofline"]["traffic"] = load_traffic(SER_TRAFFIC_KEY[args.ser_shape], "desc")
         if world == 1 and not args.no_cpu_baseline:
             try:
-                hp = ser_probe_params(p) if args.ser_shape == "probe" else p
+                hp = ser_probe_params(p) if args.ser_shape == "probe" else p[:5]
                 res["cpu_baseline"] = cpu_baseline_ser(hp, 1 << 20, args.cpu_seconds / 2, host_threads())
                 res["cpu_baseline"]["single_thread"] = cpu_baseline_ser(hp, 1 << 20, args.cpu_seconds / 2, 1)
             except Exception as e:

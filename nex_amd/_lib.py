@@ -48,6 +48,7 @@ def load():
         "nexg_probe_stream": (I, [P, P, U64, U32, P, P]),
         "nexg_decode_options": (I, [P, ctypes.POINTER(abi.Frames), P, P, P]),
         "nexg_build_udp4_batch": (I, [P, ctypes.POINTER(abi.Udp4Build), P, U32, P]),
+        "nexg_build_udp4_tuples": (I, [P, ctypes.POINTER(abi.Udp4Build), P, P, U32, P]),
         "nexg_build_udp6_batch": (I, [P, ctypes.POINTER(abi.Udp6Build), P, U32, P]),
         "nexg_build_tcp_batch": (I, [P, ctypes.POINTER(abi.TcpBuild), P, U32, P]),
         "nexg_build_icmp_echo_batch": (I, [P, ctypes.POINTER(abi.IcmpEchoBuild), P, U32, P]),

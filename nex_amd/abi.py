@@ -254,6 +254,11 @@ class Udp4Build(ctypes.Structure):
     ]
 
 
+#: struct nexg_udp4_tuple (16 B): the AoS per-frame tuple of nexg_build_udp4_tuples
+UDP4_TUPLE_DTYPE = np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("src_port", "<u2"), ("dst_port", "<u2"),
+                             ("ip_id", "<u2"), ("reserved", "<u2")])
+
+
 class Udp6Build(ctypes.Structure):
     """struct nexg_udp6_build"""
     _fields_ = [
@@ -349,7 +354,7 @@ EXPORTED_SYMBOLS = (
     "nexg_sparse_expand", "nexg_grouped_expand", "nexg_recompute_checksums_batch",
     "nexg_rx_config_default", "nexg_rx_open", "nexg_rx_next_batch", "nexg_rx_stats", "nexg_rx_close",
     "nexg_tpacket3_walk", "nexg_tx_open", "nexg_tx_send_batch", "nexg_tx_close",
-    "nexg_build_udp4_batch", "nexg_build_udp6_batch", "nexg_build_tcp_batch",
+    "nexg_build_udp4_batch", "nexg_build_udp4_tuples", "nexg_build_udp6_batch", "nexg_build_tcp_batch",
     "nexg_build_icmp_echo_batch", "nexg_build_arp_batch", "nexg_build_ndp_ns_batch", "nexg_pcap_open", "nexg_pcap_linktype", "nexg_pcap_last_error",
     "nexg_pcap_read_batch", "nexg_pcap_read_raw", "nexg_pcap_map", "nexg_pcap_walk_mapped", "nexg_pcap_set_read_threads", "nexg_pcap_close", "nexg_gen_lengths", "nexg_gen_frames", "nexg_gen_udp4_params",
 )

@@ -280,6 +280,25 @@ int nexg_build_udp4_batch(nexg_ctx* ctx, const nexg_udp4_build* p, uint8_t* out,
                       NEXG_ELAUNCH);
 }
 
+int nexg_build_udp4_tuples(nexg_ctx* ctx, const nexg_udp4_build* p, const nexg_udp4_tuple* tuples, uint8_t* out,
+                           uint32_t out_stride, void* stream) {
+    if (!ctx || !p) return NEXG_EINVAL;
+    if (28ull + p->payload_len > 65535ull)
+        return fail(ctx, NEXG_ERANGE, "UDP/IPv4 length overflow%s", nullptr);
+    if (p->src_ip || p->dst_ip || p->src_port || p->dst_port || p->ip_id || p->src_mac || p->dst_mac)
+        return fail(ctx, NEXG_EINVAL, "per-frame arrays come from the tuples: pass NULL%s", nullptr);
+    if (p->count && (!tuples || !out))
+        return fail(ctx, NEXG_EINVAL, "NULL tuples or output%s", nullptr);
+    if ((reinterpret_cast<uint64_t>(tuples) & 15u) != 0)
+        return fail(ctx, NEXG_EINVAL, "tuples must be 16-B aligned%s", nullptr);
+    if (p->payload_len && !p->payload) return fail(ctx, NEXG_EINVAL, "NULL payload%s", nullptr);
+    if (out_stride < 42u + p->payload_len)
+        return fail(ctx, NEXG_EINVAL, "out_stride shorter than a frame%s", nullptr);
+    DeviceGuard g(ctx);
+    return hip_status(ctx, nexg::launch_build_udp4_tuples(*p, tuples, out, out_stride, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
 int nexg_build_udp6_batch(nexg_ctx* ctx, const nexg_udp6_build* p, uint8_t* out,
                           uint32_t out_stride, void* stream) {
     if (!ctx || !p) return NEXG_EINVAL;

@@ -48,6 +48,7 @@ struct BuildArgs {
     nexg_udp4_build p;
     uint8_t* out;
     uint32_t out_stride;
+    const nexg_udp4_tuple* tuples;  // AOS builds: one 16-B tuple per frame
 };
 
 // Frame header given as NH (odd) little-endian halfwords of its bytes, written
@@ -102,7 +103,9 @@ __device__ __forceinline__ uint32_t shared_payload_sum(const uint8_t* pl, uint32
 // first wait (the general form waits once per optional array).
 // PROBE: the udp_ping probe batch (udp_ping.rs:30-31, 68-109 per target): only
 // dst_ip is per frame; source address, ports, id and MACs are the batch's.
-template <uint32_t MAXS, bool FULL = false, bool PROBE = false>
+// AOS: the per-frame tuple as one 16-B record (nexg_udp4_tuple), read with one
+// non-temporal dwordx4 load per lane instead of five SoA loads.
+template <uint32_t MAXS, bool FULL = false, bool PROBE = false, bool AOS = false>
 __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     constexpr bool STAGED = MAXS != 0;
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
@@ -116,11 +119,12 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     __shared__ uint32_t s_pay;
     const uint64_t pw = shared_payload_sum(p.payload, p.payload_len, &s_pay);
     if (tid < nf) {
-        const uint32_t dst = p.dst_ip[i];
-        const uint32_t src = FULL ? p.src_ip[i] : PROBE ? p.def_src_ip : (p.src_ip ? p.src_ip[i] : p.def_src_ip);
-        const uint32_t sp = FULL ? p.src_port[i] : PROBE ? p.def_src_port : (p.src_port ? p.src_port[i] : p.def_src_port);
-        const uint32_t dp = FULL ? p.dst_port[i] : PROBE ? p.def_dst_port : (p.dst_port ? p.dst_port[i] : p.def_dst_port);
-        const uint32_t id = FULL ? p.ip_id[i] : PROBE ? p.def_ip_id : (p.ip_id ? p.ip_id[i] : p.def_ip_id);
+        const u32x4 tv = AOS ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.tuples) + i) : u32x4{0, 0, 0, 0};
+        const uint32_t dst = AOS ? tv.y : p.dst_ip[i];
+        const uint32_t src = AOS ? tv.x : FULL ? p.src_ip[i] : PROBE ? p.def_src_ip : (p.src_ip ? p.src_ip[i] : p.def_src_ip);
+        const uint32_t sp = AOS ? tv.z & 0xFFFFu : FULL ? p.src_port[i] : PROBE ? p.def_src_port : (p.src_port ? p.src_port[i] : p.def_src_port);
+        const uint32_t dp = AOS ? tv.z >> 16 : FULL ? p.dst_port[i] : PROBE ? p.def_dst_port : (p.dst_port ? p.dst_port[i] : p.def_dst_port);
+        const uint32_t id = AOS ? tv.w & 0xFFFFu : FULL ? p.ip_id[i] : PROBE ? p.def_ip_id : (p.ip_id ? p.ip_id[i] : p.def_ip_id);
         const uint32_t ulen = 8u + p.payload_len, total = 20u + ulen;
         const uint64_t addr = (uint64_t)(src >> 16) + (src & 0xFFFFu) + (dst >> 16) + (dst & 0xFFFFu);
         // udp.rs:443-477 on to_bytes(): pseudo + sport + dport + length (+ payload)
@@ -131,8 +135,8 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
         const uint32_t ics = fold_complement(addr + w0 + total + id + w3 + w4);
         uint8_t h[42];
         for (int k = 0; k < 6; k++) {
-            h[k] = !FULL && !PROBE && p.dst_mac ? p.dst_mac[i * 6 + k] : p.def_dst_mac[k];
-            h[6 + k] = !FULL && !PROBE && p.src_mac ? p.src_mac[i * 6 + k] : p.def_src_mac[k];
+            h[k] = !FULL && !PROBE && !AOS && p.dst_mac ? p.dst_mac[i * 6 + k] : p.def_dst_mac[k];
+            h[6 + k] = !FULL && !PROBE && !AOS && p.src_mac ? p.src_mac[i * 6 + k] : p.def_src_mac[k];
         }
         h[12] = 0x08; h[13] = 0x00;
         h[14] = (uint8_t)(w0 >> 8); h[15] = (uint8_t)w0;
@@ -771,10 +775,26 @@ __global__ void k_gen_udp4_params(uint64_t seed, uint64_t first, uint64_t count,
 
 // --------------------------------------------------------------- launchers
 
+hipError_t launch_build_udp4_tuples(const nexg_udp4_build& p, const nexg_udp4_tuple* tuples, uint8_t* out,
+                                    uint32_t out_stride, hipStream_t s) {
+    if (p.count == 0) return hipSuccess;
+    BuildArgs a{p, out, out_stride, tuples};
+    const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
+    const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
+    if (staged && out_stride <= 64u)
+        hipLaunchKernelGGL((k_build_udp4<64, false, false, true>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    else if (staged)
+        hipLaunchKernelGGL((k_build_udp4<kBuildMaxStride, false, false, true>), dim3((uint32_t)blocks), dim3(kBuildTile),
+                           0, s, a);
+    else
+        hipLaunchKernelGGL((k_build_udp4<0, false, false, true>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_build_udp4(const nexg_udp4_build& p, uint8_t* out, uint32_t out_stride,
                              hipStream_t s) {
     if (p.count == 0) return hipSuccess;
-    BuildArgs a{p, out, out_stride};
+    BuildArgs a{p, out, out_stride, nullptr};
     const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
     const bool full = p.src_ip && p.src_port && p.dst_port && p.ip_id && !p.src_mac && !p.dst_mac;

@@ -56,6 +56,8 @@ hipError_t launch_decode_options(const ParseArgs& a, const nexg_record* recs, ne
 
 hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, uint32_t mode, void* out, hipStream_t s);
 
+hipError_t launch_build_udp4_tuples(const nexg_udp4_build& p, const nexg_udp4_tuple* tuples, uint8_t* out,
+                                    uint32_t out_stride, hipStream_t s);
 hipError_t launch_build_udp4(const nexg_udp4_build& p, uint8_t* out, uint32_t out_stride,
                              hipStream_t s);
 

@@ -315,6 +315,35 @@ class Engine:
                                                    self._stream(stream)))
         return out
 
+    @staticmethod
+    def pack_udp4_tuples(src_ip, dst_ip, src_port, dst_port, ip_id):
+        """The five per-frame tuple arrays of build_udp4 (int32 / int16 device
+        tensors) as one (count, 4) int32 tensor of 16-B nexg_udp4_tuple records."""
+        torch = _torch()
+        lo16 = lambda t: t.to(torch.int32) & 0xFFFF
+        return torch.stack([src_ip.to(torch.int32), dst_ip.to(torch.int32),
+                            lo16(src_port) | (lo16(dst_port) << 16), lo16(ip_id)], dim=1).contiguous()
+
+    def build_udp4_tuples(self, tuples, src_mac=b"\0" * 6, dst_mac=b"\0" * 6, ttl=64, ip_flags=0, dscp_ecn=0,
+                          payload=None, out_stride=None, out=None, stream=None):
+        """build_udp4 with each frame's tuple as one 16-B record
+        (nexg_build_udp4_tuples; `tuples` from pack_udp4_tuples)."""
+        torch = _torch()
+        count = tuples.shape[0]
+        plen = 0 if payload is None else payload.numel()
+        stride = out_stride or (42 + plen)
+        if out is None:
+            out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
+        p = abi.Udp4Build()
+        p.payload = None if payload is None else payload.data_ptr()
+        p.payload_len = plen
+        p.def_src_mac[:] = list(src_mac)
+        p.def_dst_mac[:] = list(dst_mac)
+        p.ttl, p.ip_flags, p.dscp_ecn, p.count = ttl, ip_flags, dscp_ecn, count
+        self._check(self.lib.nexg_build_udp4_tuples(self.ctx, ctypes.byref(p), _ptr(tuples), _ptr(out), stride,
+                                                    self._stream(stream)))
+        return out
+
     def build_udp6(self, src_ip, dst_ip, src_port=None, dst_port=None, def_src_port=0,
                    def_dst_port=0, src_mac=b"\0" * 6, dst_mac=b"\0" * 6, hop_limit=64,
                    traffic_class=0, flow_label=0, payload=None, out_stride=None, out=None,

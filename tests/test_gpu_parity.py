@@ -510,3 +510,34 @@ def test_large_mutation_sweep_slices_and_options(engine, oracle, flags, ip_offse
     sel = rng.choice(len(frames), 40_000, replace=False)  # the oracle's option walk is per frame
     want_o = np.array([oracle.decode_options(frames[i], flags, ip_offset) for i in sel], abi.OPTIONS_DTYPE)
     helpers.records_equal(got_o[sel], want_o, [frames[i] for i in sel], f"options sweep flags={flags}")
+
+
+def test_build_udp4_tuples_aos(engine, oracle):
+    """nexg_build_udp4_tuples (one 16-B tuple record per frame): the bytes of
+    every frame equal the oracle's udp_ping build (builder/udp.rs:67-95,
+    builder/ipv4.rs:94-166) of the same tuple, and equal the SoA build of the
+    same arrays, at a full 16M batch (the bench's ser.tuples workload) and at
+    ragged counts; per-frame arrays next to the tuples are refused."""
+    import ctypes
+
+    import torch
+    smac, dmac = bytes([2, 0, 0, 0, 0, 1]), bytes([2, 0, 0, 0, 0, 2])
+    for n in (1, 255, 257, 5000, 16 << 20):
+        p = engine.gen_udp4_params(n, first_index=3)
+        tup = engine.pack_udp4_tuples(*p)
+        aos = engine.build_udp4_tuples(tup, src_mac=smac, dst_mac=dmac, ip_flags=2)
+        soa = engine.build_udp4(*p, src_mac=smac, dst_mac=dmac, ip_flags=2)
+        torch.cuda.synchronize()
+        assert torch.equal(aos[: n * 42], soa[: n * 42]), n
+        m = min(n, 1 << 16)
+        host = [t[:m].cpu().numpy().view(np.uint32 if t.element_size() == 4 else np.uint16) for t in p]
+        want = oracle.build_udp4_batch(smac, dmac, *host, 64, 2)
+        assert (aos[: m * 42].cpu().numpy().reshape(m, 42) == want).all(), n
+    rec = tup[:1].cpu().numpy().view(abi.UDP4_TUPLE_DTYPE)[0]
+    assert rec["src_ip"] == int(p[0][0].item()) & 0xFFFFFFFF and rec["dst_port"] == int(p[3][0].item()) & 0xFFFF
+    bad = abi.Udp4Build()
+    bad.count, bad.dst_ip = 4, p[1].data_ptr()
+    out = torch.empty(4 * 42, dtype=torch.uint8, device="cuda")
+    rc = engine.lib.nexg_build_udp4_tuples(engine.ctx, ctypes.byref(bad), ctypes.c_void_p(tup.data_ptr()),
+                                           ctypes.c_void_p(out.data_ptr()), 42, None)
+    assert rc == abi.EINVAL

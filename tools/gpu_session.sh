@@ -22,11 +22,12 @@ for s in ${STEPS:-tests}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench_udp64 500 python bench.py --steps 50 --cpu-seconds 5 ;;
     driverbench) step bench_driver 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
-    newtests4) step pytest_new4 600 python -u -m pytest tests/test_gpu_tcp_options.py tests/test_gpu_build_probe.py -q -x --timeout 300 --timeout-method thread ;;
+    newtests4) step pytest_new4 600 python -u -m pytest tests/test_gpu_tcp_options.py tests/test_gpu_build_probe.py "tests/test_gpu_parity.py::test_build_udp4_tuples_aos" -q -x --timeout 300 --timeout-method thread ;;
     malformed) step bench_malformed 500 python tools/bench_malformed.py ;;
     benchpcap) step bench_pcap 400 python bench.py --workload imix_pcap --steps 20 --cpu-seconds 5 ;;
     ser) step bench_ser 300 python bench.py --workload ser --steps 50 --no-cpu-baseline
-         step bench_ser_tuples 300 python bench.py --workload ser --ser-shape tuples --steps 50 --no-cpu-baseline ;;
+         step bench_ser_tuples 300 python bench.py --workload ser --ser-shape tuples --steps 50 --no-cpu-baseline
+         step bench_ser_aos 300 python bench.py --workload ser --ser-shape tuples_aos --steps 50 --no-cpu-baseline ;;
     e2e) step bench_e2e 400 python bench.py --e2e --steps 5 --warmup 2 --no-cpu-baseline
          step bench_e2e_imix 400 python bench.py --e2e --workload imix --steps 3 --warmup 1 --no-cpu-baseline ;;
     # bench.py --gpus N starts its own N ranks (nex_amd/launch.py); gloo folds them onto the one GPU
@@ -41,7 +42,8 @@ for s in ${STEPS:-tests}; do
           step prof_real 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_real -o run -- python3 bench.py --workload real_traffic --steps 60 --warmup 25 --no-cpu-baseline
           step prof_large 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_large -o run -- python3 bench.py --frames 54525952 --steps 60 --warmup 25 --no-cpu-baseline
           step prof_ser 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser -o run -- python3 bench.py --workload ser --steps 60 --warmup 25 --no-cpu-baseline
-          step prof_ser_tuples 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser_tuples -o run -- python3 bench.py --workload ser --ser-shape tuples --steps 60 --warmup 25 --no-cpu-baseline ;;
+          step prof_ser_tuples 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser_tuples -o run -- python3 bench.py --workload ser --ser-shape tuples --steps 60 --warmup 25 --no-cpu-baseline
+          step prof_ser_aos 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser_aos -o run -- python3 bench.py --workload ser --ser-shape tuples_aos --steps 60 --warmup 25 --no-cpu-baseline ;;
   esac
 done
 echo done
