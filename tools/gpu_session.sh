@@ -35,6 +35,9 @@ for s in ${STEPS:-tests}; do
     rehearse8) step rehearse8 900 env NEXG_DIST_BACKEND=gloo python bench.py --gpus 8 --steps 10 --warmup 3 --cpu-seconds 2 --no-large ;;
     benchimix) step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5 ;;
     pmc) step pmc 900 bash tools/pmc.sh ;;
+    # in-process A/B of library variants under abvar/ (LIBS=a,b,...): IMIX with an output check, then the mixes
+    abspan) step ab_imix 600 python -u tools/bench_parse_ab.py --libs ${LIBS} --workloads imix,udp64 --out grouped --check --rounds 4
+            step ab_mixes 600 python -u tools/bench_malformed.py --libs ${LIBS} --kinds clean,all,tcp_ts --out grouped ;;
     prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed --no-real --no-large --no-ser
           step prof_pcap 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pcap -o run -- python3 bench.py --workload imix_pcap --steps 60 --warmup 25 --no-cpu-baseline
           step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 60 --warmup 25 --no-cpu-baseline
