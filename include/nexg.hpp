@@ -981,38 +981,28 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         const uint32_t L = 42u + (uint32_t)shape.payload.size();
         std::vector<std::vector<uint8_t>> frames;
         if (n == 0) return frames;
-        std::vector<uint32_t> src(n), dst(n);
-        std::vector<uint16_t> sp(n), dp(n), id(n);
+        // one 16-B record per tuple: a single H2D copy and one load per frame
+        // on the device (nexg_build_udp4_tuples)
+        std::vector<nexg_udp4_tuple> tup(n);
         for (uint64_t i = 0; i < n; i++) {
             const auto& a = t[i].source.octets;
             const auto& b = t[i].destination.octets;
-            src[i] = (uint32_t)a[0] << 24 | (uint32_t)a[1] << 16 | (uint32_t)a[2] << 8 | a[3];
-            dst[i] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
-            sp[i] = t[i].src_port;
-            dp[i] = t[i].dst_port;
-            id[i] = t[i].ip_id;
+            tup[i].src_ip = (uint32_t)a[0] << 24 | (uint32_t)a[1] << 16 | (uint32_t)a[2] << 8 | a[3];
+            tup[i].dst_ip = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+            tup[i].src_port = t[i].src_port;
+            tup[i].dst_port = t[i].dst_port;
+            tup[i].ip_id = t[i].ip_id;
+            tup[i].reserved = 0;
         }
-        void* d_src = scratch(5, n * 4);
-        void* d_dst = scratch(6, n * 4);
-        void* d_sp = scratch(7, n * 2);
-        void* d_dp = scratch(8, n * 2);
-        void* d_id = scratch(9, n * 2);
+        void* d_tup = scratch(5, n * sizeof(nexg_udp4_tuple));
         void* d_pl = scratch(10, shape.payload.size());
         void* d_out = scratch(11, (uint64_t)n * L);
-        check_hip(hipMemcpyAsync(d_src, src.data(), n * 4, hipMemcpyHostToDevice, stream_), "H2D");
-        check_hip(hipMemcpyAsync(d_dst, dst.data(), n * 4, hipMemcpyHostToDevice, stream_), "H2D");
-        check_hip(hipMemcpyAsync(d_sp, sp.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
-        check_hip(hipMemcpyAsync(d_dp, dp.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
-        check_hip(hipMemcpyAsync(d_id, id.data(), n * 2, hipMemcpyHostToDevice, stream_), "H2D");
+        check_hip(hipMemcpyAsync(d_tup, tup.data(), n * sizeof(nexg_udp4_tuple), hipMemcpyHostToDevice, stream_),
+                  "H2D");
         if (!shape.payload.empty())
             check_hip(hipMemcpyAsync(d_pl, shape.payload.data(), shape.payload.size(), hipMemcpyHostToDevice,
                                      stream_), "H2D");
         nexg_udp4_build p{};
-        p.src_ip = static_cast<const uint32_t*>(d_src);
-        p.dst_ip = static_cast<const uint32_t*>(d_dst);
-        p.src_port = static_cast<const uint16_t*>(d_sp);
-        p.dst_port = static_cast<const uint16_t*>(d_dp);
-        p.ip_id = static_cast<const uint16_t*>(d_id);
         p.payload = shape.payload.empty() ? nullptr : static_cast<const uint8_t*>(d_pl);
         p.payload_len = (uint32_t)shape.payload.size();
         memcpy(p.def_src_mac, shape.src_mac.data(), 6);
@@ -1020,7 +1010,8 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         p.ttl = shape.ttl;
         p.ip_flags = shape.ip_flags;
         p.count = n;
-        check(nexg_build_udp4_batch(ctx_, &p, static_cast<uint8_t*>(d_out), L, stream_), "nexg_build_udp4_batch");
+        check(nexg_build_udp4_tuples(ctx_, &p, static_cast<const nexg_udp4_tuple*>(d_tup),
+                                     static_cast<uint8_t*>(d_out), L, stream_), "nexg_build_udp4_tuples");
         std::vector<uint8_t> host((uint64_t)n * L);
         check_hip(hipMemcpyAsync(host.data(), d_out, host.size(), hipMemcpyDeviceToHost, stream_), "D2H");
         check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
