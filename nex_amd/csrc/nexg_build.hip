@@ -119,7 +119,11 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     __shared__ uint32_t s_pay;
     const uint64_t pw = shared_payload_sum(p.payload, p.payload_len, &s_pay);
     if (tid < nf) {
+#if NEXG_AOS_NT
         const u32x4 tv = AOS ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.tuples) + i) : u32x4{0, 0, 0, 0};
+#else
+        const u32x4 tv = AOS ? reinterpret_cast<const u32x4*>(a.tuples)[i] : u32x4{0, 0, 0, 0};
+#endif
         const uint32_t dst = AOS ? tv.y : p.dst_ip[i];
         const uint32_t src = AOS ? tv.x : FULL ? p.src_ip[i] : PROBE ? p.def_src_ip : (p.src_ip ? p.src_ip[i] : p.def_src_ip);
         const uint32_t sp = AOS ? tv.z & 0xFFFFu : FULL ? p.src_port[i] : PROBE ? p.def_src_port : (p.src_port ? p.src_port[i] : p.def_src_port);

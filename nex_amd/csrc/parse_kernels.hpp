@@ -553,28 +553,6 @@ NEXG_HD uint32_t span_bucket(uint32_t w3, uint32_t w5, uint32_t opt_flags) {
     return 8u;
 }
 
-// ten ds_read_b64 at an 8-B aligned LDS address into u[o..o+19] (the
-// compiler does not track asm LDS reads: the lgkmcnt wait names every result)
-__device__ __forceinline__ void lds_read_b64x10(const uint8_t* p, uint32_t (&u)[21], int o) {
-    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-    const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
-    v2u r0, r1, r2, r3, r4, r5, r6, r7, r8, r9;
-    asm volatile(
-        "ds_read_b64 %0, %10\n\tds_read_b64 %1, %10 offset:8\n\tds_read_b64 %2, %10 offset:16\n\t"
-        "ds_read_b64 %3, %10 offset:24\n\tds_read_b64 %4, %10 offset:32\n\tds_read_b64 %5, %10 offset:40\n\t"
-        "ds_read_b64 %6, %10 offset:48\n\tds_read_b64 %7, %10 offset:56\n\tds_read_b64 %8, %10 offset:64\n\t"
-        "ds_read_b64 %9, %10 offset:72\n\ts_waitcnt lgkmcnt(0)"
-        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7), "=&v"(r8), "=&v"(r9)
-        : "v"(la)
-        : "memory");
-    const v2u r[10] = {r0, r1, r2, r3, r4, r5, r6, r7, r8, r9};
-#pragma unroll
-    for (int m = 0; m < 10; m++) {
-        u[o + 2 * m] = r[m].x;
-        u[o + 2 * m + 1] = r[m].y;
-    }
-}
-
 // inclusive wave64 scan on DPP (row_shr 1/2/4/8, row_bcast 15/31): no LDS traffic
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
@@ -613,23 +591,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const bool have = t < nf;
     if (OUT == NEXG_OUT_GROUPED && lane == 0 && have) reinterpret_cast<uint8_t*>(a.out)[idx >> 6] = 0;  // every group mixed
     const bool ok = have && frame_extent(a, idx, off, len);
-#if NEXG_SPAN_SCALAR_START
-    // the group's span from uniform loads (the first frame's offset, the last
-    // frame's extent): the first sub-tile goes in flight without waiting for
-    // the per-lane extents and a barrier
-    uint64_t lo, hi;
-    {
-        uint32_t ll = 0;
-        lo = a.offsets ? a.offsets[f0] : f0 * (uint64_t)a.stride;
-        frame_extent(a, f0 + nf - 1, hi, ll);
-        hi += ll;
-    }
-#else
     if (t == 0) s_span[0] = off;
     if (t == nf - 1) s_span[1] = off + len;
     __syncthreads();
     const uint64_t lo = s_span[0], hi = s_span[1];
-#endif
     const uint64_t A0 = (base + lo) & ~15ull;
     const uint32_t span = (uint32_t)(((base + hi + 15u) & ~15ull) - A0);
     // the first sub-tile goes in flight before the group's packed check (one
@@ -728,25 +693,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // or in the last one (bytes past the span end are masked by len)
         const int dh = (int)((hr & ~3u) - S);
         if (have && dh >= -(int)kLaneWin && (dh <= (int)(SUB - kLaneWin - 4u) || (last && dh < (int)SUB))) {
-#if NEXG_SPAN_GATHER64
-            // 8-B LDS reads (ds_read_b64: 64 banks, 2 cycles; ds_read2_b32 banks
-            // mod 32 put lanes of 64-B frames two apart on one bank): dword 0
-            // alone when the window starts at 4 mod 8, else dword 20 alone. In
-            // asm: the compiler merges the two shapes into one ds_read2_b32 run
-            // on a selected base, and a dword select after 8-B aligned reads
-            // costs a VGPR that spills in the sub-tile loop
-            const uint8_t* wp = sb + dh;
-            if (dh & 4) {
-                u[0] = *reinterpret_cast<const uint32_t*>(wp);
-                lds_read_b64x10(wp + 4, u, 1);
-            } else {
-                lds_read_b64x10(wp, u, 0);
-                u[20] = *reinterpret_cast<const uint32_t*>(wp + 80);
-            }
-#else
 #pragma unroll
             for (int j = 0; j < 21; j++) u[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4 * j);
-#endif
             // A padded frame's L4 range ends at the IP end, not the frame end:
             // take the second prefix value there instead (at or past the window
             // end, so in this sub-tile or a later one), so SpanFrame sums that

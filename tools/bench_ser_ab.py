@@ -3,7 +3,7 @@
 frames) across library builds: the same parameter batch and output buffer,
 each library timed with HIP events, interleaved A B A B; the first library
 also gives the reference bytes every other build must reproduce exactly.
-usage: python tools/bench_ser_ab.py --libs A.so,B.so [--steps K]"""
+usage: python tools/bench_ser_ab.py --libs A.so,B.so [--steps K] [--shape tuples|aos]"""
 import argparse
 import json
 import os
@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--frames", type=int, default=16 << 20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--shape", choices=["tuples", "aos"], default="tuples",
+                    help="five tuple arrays (nexg_build_udp4_batch) or 16-B records (nexg_build_udp4_tuples)")
     args = ap.parse_args()
     import torch
     from nex_amd import _lib
@@ -36,8 +38,14 @@ def main():
     macs = (b"\x02\0\0\0\0\1", b"\x02\0\0\0\0\2")
     s = torch.cuda.current_stream()
 
+    tup = engines[0].pack_udp4_tuples(*p) if args.shape == "aos" else None
+
     def step(e):
-        e.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=macs[0], dst_mac=macs[1], ip_flags=2, out=out, stream=s)
+        if tup is not None:
+            e.build_udp4_tuples(tup, src_mac=macs[0], dst_mac=macs[1], ip_flags=2, out=out, stream=s)
+        else:
+            e.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=macs[0], dst_mac=macs[1], ip_flags=2, out=out,
+                         stream=s)
     for k, e in enumerate(engines):
         out.zero_()
         step(e)
@@ -46,8 +54,9 @@ def main():
             ref = out.clone()
         assert torch.equal(out, ref), f"{libs[k]} builds different bytes"
     times = {l: [] for l in libs}
-    for _ in range(args.rounds):
-        for l, e in zip(libs, engines):
+    for rnd in range(args.rounds):
+        pairs = list(zip(libs, engines))
+        for l, e in (pairs[::-1] if rnd % 2 else pairs):  # alternate the order (first-measured bias)
             for _ in range(args.warmup):
                 step(e)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
