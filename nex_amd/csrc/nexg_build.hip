@@ -119,6 +119,9 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     __shared__ uint32_t s_pay;
     const uint64_t pw = shared_payload_sum(p.payload, p.payload_len, &s_pay);
     if (tid < nf) {
+#ifndef NEXG_AOS_NT
+#define NEXG_AOS_NT 0
+#endif
 #if NEXG_AOS_NT
         const u32x4 tv = AOS ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.tuples) + i) : u32x4{0, 0, 0, 0};
 #else
