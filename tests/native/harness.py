@@ -28,6 +28,8 @@ def lib():
         L.harness_slice.argtypes = [P, U64, P, P, U32, U64, U32, U32, U32, P]
         L.harness_span_groups.restype = ctypes.c_int
         L.harness_span_groups.argtypes = [P, U64, P, U64, U32, U32, P]
+        L.harness_span_declined.restype = None
+        L.harness_span_declined.argtypes = [P]
         _lib = L
     return _lib
 
@@ -91,14 +93,23 @@ def sparse_decode(codes, lens, flags=0, ip_offset=0):
     return dd[:n], hd[:n]
 
 
-def span_groups(data, offsets, flags=0, ip_offset=0):
-    """k_parse_span's fast path + generic section (slots, free-slot extension
-    windows, bucketed items) emulated group by group over a packed batch."""
+def span_groups(data, offsets, flags=0, ip_offset=0, declined=None):
+    """k_parse_span's fast path (with the lanes' slots for IPv4 options) +
+    generic section (slots, bucketed items) emulated group by group over a
+    packed batch. `declined` (uint8[count], optional) receives 1 for every
+    frame the fast path declined to the generic core."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     offs = np.ascontiguousarray(offsets, dtype=np.uint64)
     count = len(offs) - 1
     recs = np.zeros(count, dtype=abi.RECORD_DTYPE)
-    rc = lib().harness_span_groups(data.ctypes.data, data.nbytes, offs.ctypes.data, count, flags, ip_offset,
-                                   recs.ctypes.data)
+    if declined is not None:
+        assert declined.dtype == np.uint8 and declined.flags.c_contiguous and len(declined) >= count
+        declined[:count] = 0
+    lib().harness_span_declined(ctypes.c_void_p(declined.ctypes.data if declined is not None else None))
+    try:
+        rc = lib().harness_span_groups(data.ctypes.data, data.nbytes, offs.ctypes.data, count, flags, ip_offset,
+                                       recs.ctypes.data)
+    finally:
+        lib().harness_span_declined(ctypes.c_void_p(None))
     assert rc == 0, f"harness_span_groups: {rc}"
     return recs

@@ -232,9 +232,38 @@ def test_fastpath_edge_shapes_match_oracle(oracle):
         helpers.records_equal(got, want, frames, f"edge shapes flags={flags}")
     for shift in (1, 2, 3):
         buf, offs, lens = pack(frames, 1, shift)
-        got = harness.parse_packed(buf, offs, lens, use_fast=5)
-        helpers.records_equal(got, oracle.parse_packed(buf, offs, lens), frames, f"edge span shift={shift}")
+        for flags in (0, abi.PARSE_STRICT):
+            got = harness.parse_packed(buf, offs, lens, use_fast=5, flags=flags)
+            helpers.records_equal(got, oracle.parse_packed(buf, offs, lens, flags=flags), frames,
+                                  f"edge span shift={shift} flags={flags}")
     po = np.zeros(len(frames) + 1, np.int64)
     np.cumsum([len(x) for x in frames], out=po[1:])
     data = np.frombuffer(b"".join(frames) + bytes(16), np.uint8)
     helpers.records_equal(harness.span_groups(data, po), oracle.parse_frames(frames), frames, "edge span groups")
+
+
+def test_ipv4_options_fast_path(oracle):
+    """IPv4 options on the span kernel's register fast path (round 4: the
+    walk of ipv4.rs:442-508, the re-serialised header checksum of
+    ipv4.rs:231-286 / 932-938 with Q16 / Q17, and the L4 shift, all through
+    the lane's LDS slot): every option frame of helpers.ipv4_option_frames,
+    lenient and strict, at four byte alignments, through the span-group
+    emulation equals the oracle, and the fast path takes the lenient frames
+    whose L4 bytes lie in the 80-B window instead of declining them."""
+    frames = helpers.ipv4_option_frames(np.random.default_rng(7))
+    assert len(frames) > 15000
+    for shift in (0, 1, 2, 3):
+        po = np.zeros(len(frames) + 1, np.int64)
+        np.cumsum([len(x) for x in frames], out=po[1:])
+        data = np.frombuffer(bytes(shift) + b"".join(frames) + bytes(16), np.uint8)
+        for flags in (0, abi.PARSE_STRICT):
+            dec = np.zeros(len(frames), np.uint8)
+            got = harness.span_groups(data, po + shift, flags=flags, declined=dec)
+            want = oracle.parse_frames(frames, flags=flags)
+            helpers.records_equal(got, want, frames, f"ipv4 options span groups shift={shift} flags={flags}")
+            v4opt = ((want["flags"] & abi.L_IPV4) != 0) & ((want["ip_ver_ihl"] & 15) > 5)
+            taken = v4opt & (dec == 0)
+            if flags == 0:
+                assert taken.sum() > 0.6 * v4opt.sum(), (int(taken.sum()), int(v4opt.sum()))
+            # the Q17 frames (re-serialised header longer than the packet) too
+            assert (taken & ((want["flags"] & abi.C_IP_PANIC) != 0)).sum() > 0 or flags
