@@ -841,7 +841,7 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     // past the data offset ends the walk of tcp.rs:767-818 with an error
     // (InvalidLength / Truncated): no TcpPacket (Q13), like a short header
     const bool walkfail = doff > 5u && b20 >= 2u && (b21 < 2u || b21 > olen);
-    const bool tfail = tcp && (n < 20u || doff < 5u || 4u * doff > n || walkfail);  // no TcpPacket
+    bool tfail = tcp && (n < 20u || doff < 5u || 4u * doff > n || walkfail);  // no TcpPacket
     const bool q14 = udp && (n < 8u || ulen < 8u || ulen > n);                       // no UdpPacket
     // TCP option lists of one TLV, alone (MSS of a SYN-ACK: 02 04 ..) or
     // behind NOP, NOP (timestamps, RFC 7323's layout for most data segments;
@@ -853,7 +853,66 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     const bool one = b20 >= 2u && b21 >= 2u && b21 == olen;
     const bool nnx = b20 == 1u && b21 == 1u && b22 >= 2u && b23 >= 2u && 2u + b23 == olen;
     const bool tsopt = tcp && !tfail && doff > 5u && (one || nnx);
-    if ((tcp && !tfail && doff != 5u && !tsopt) || (udp && !q14 && ulen != n)) return false;
+    // any other option list that lies in the window: the walk of
+    // tcp.rs:767-818 over the window's bytes in the slot (frame coordinates,
+    // as stored before the IPv4 options shift). A list that does not walk
+    // has no TcpPacket (Q13, as tfail); one that does re-serialises to the
+    // options up to the first EOL, zero padded to hl_ser (tcp.rs:521-575):
+    // the checksum drops the bytes [stop, 4 * doff) and sums the re-serialised
+    // data offset and length
+    // gv: nopt | 1 << 8 for a walked list; tcorr: what re-serialisation changes
+    // in the TCP checksum sum (mod 0xFFFF, as an addend: the dropped bytes
+    // [stop, 4 * doff), the data offset and length words), so only two values
+    // leave the branch
+    uint32_t gv = 0, tcorr = 0;
+    if (tcp && !tfail && doff > 5u && !tsopt) {
+        if (!oslot || l4 + 4u * doff > 80u) return false;
+        if (!sd) {
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+                reinterpret_cast<uint4*>(oslot)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        }
+        const uint32_t hlt = 4u * doff;
+        uint32_t stop = hlt, nopt = 0;
+        bool ok = true;
+#pragma unroll 1
+        for (uint32_t off = 20u; off < hlt;) {
+            const uint32_t kind = oslot[l4 + off];
+            off++;
+            if (kind == 0u) {  // EOL: taken, the walk stops
+                nopt++;
+                stop = off;
+                break;
+            }
+            if (kind == 1u) {  // NOP
+                nopt++;
+                continue;
+            }
+            if (off >= hlt) {  // Malformed
+                ok = false;
+                break;
+            }
+            const uint32_t l = oslot[l4 + off];
+            off++;
+            if (l < 2u || off + (l - 2u) > hlt) {  // InvalidLength / Truncated
+                ok = false;
+                break;
+            }
+            nopt++;
+            off += l - 2u;
+        }
+        if (!ok) {
+            tfail = true;
+        } else {
+            const uint32_t hl_ser = 20u + ((stop - 20u + 3u) & ~3u);
+            const uint32_t skipped = stop < hlt ? oslot_le_range(oslot, l4 + stop, l4 + hlt) : 0u;
+            // (data offset nibble: x16 in the LE half, x256 as BE; length: BE)
+            const uint32_t drop = (256u * (16u * (doff - (hl_ser >> 2)) + skipped) + (hlt - hl_ser)) % 0xFFFFu;
+            tcorr = drop ? 0xFFFFu - drop : 0u;
+            gv = nopt | 1u << 8;
+        }
+    }
+    if (udp && !q14 && ulen != n) return false;
     const bool tonly = tfail || q14;                                  // transport layer, no packet
     const bool none = !(tcp || udp || icmp) || (icmp && n < 8u);      // no transport layer
     const bool l4ok = !(tonly || none);
@@ -890,6 +949,7 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     else hdr = LE(0);
     uint64_t t4 = 256ull * ((icmp && !v6 ? 0u : pseudo) + hdr + restsum);
     t4 += (icmp && !v6) ? 0u : (pv + n);  // pseudo proto + length (BE constants)
+    t4 += tcorr;  // a walked TCP list: its re-serialisation (0 otherwise)
     if (udp) t4 += n;                     // UDP length word as serialised
     const uint32_t l4_calc = fold_complement(t4);
     const uint32_t l4_cs = tcp ? L(16) : (udp ? L(6) : L(2));
@@ -947,13 +1007,13 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
         r.tcp_seq = (L(4) << 16) | L(6);
         r.tcp_ack = (L(8) << 16) | L(10);
         r.l4_length = (uint16_t)(4u * doff);
-        r.l4_nopt = tsopt ? (nnx ? 3u : 1u) : 0u;
+        r.l4_nopt = tsopt ? (nnx ? 3u : 1u) : gv & 0xFFu;
         r.l4_type = (uint8_t)L(12);
         r.l4_code = (uint8_t)(L(12) >> 8);
         r.tcp_window = (uint16_t)L(14);
         r.tcp_urg = (uint16_t)L(18);
     }
-    const uint32_t hp = tsopt ? 4u * doff : h;  // header bytes before the payload
+    const uint32_t hp = tsopt || gv ? 4u * doff : h;  // header bytes before the payload
     r.payload_off = (uint16_t)(n > hp ? l4 + hp : 0u);
     r.payload_len = (uint16_t)(n - hp);
     return true;

@@ -541,6 +541,42 @@ def fastpath_edge_frames(rng):
                     seg = _tcp(pay, opts, doff=doff)
                     f.append(_eth(_ipv4(seg, 6)) if fam == 4 else _eth(_ipv6(seg, 6), 0x86DD))
     f += ipv4_option_frames(rng)
+    f += tcp_walk_frames(rng)
+    return f
+
+
+def tcp_walk_frames(rng):
+    """TCP option lists the general walk (round 4: tcp.rs:767-818 through the
+    span kernel's lane slot) takes or refuses: the SYN lists of common stacks
+    (MSS, SACK permitted, timestamps, NOP, window scale; with and without EOL
+    padding), lists that stop at an EOL with non-zero bytes after it (dropped
+    from the re-serialised header and its checksum), NOP runs, TLVs that cut
+    the list later than the first option (Q13), behind IPv4 headers with and
+    without options and IPv6, payloads 0..600 B."""
+    ts = bytes([8, 10]) + bytes(rng.integers(0, 256, 8, dtype=np.uint8))
+    lists = [bytes([2, 4, 5, 0xb4, 4, 2]) + ts + bytes([1, 3, 3, 7]),               # Linux SYN (doff 10)
+             bytes([2, 4, 5, 0xb4, 1, 3, 3, 8, 1, 1, 4, 2]),                        # Windows SYN (doff 8)
+             bytes([2, 4, 5, 0xb4, 1, 3, 3, 6, 1, 1]) + ts + bytes([4, 2, 0, 0]),   # macOS SYN (doff 11, EOL)
+             bytes([2, 4, 5, 0xb4, 0, 9, 9, 9]),                                    # EOL, junk after it
+             bytes([1, 1, 0, 0xFF, 0xEE, 0xDD, 0xCC, 0xBB]),                        # NOP NOP EOL junk
+             bytes([0]) + bytes([0x5A] * 7),                                        # EOL first
+             bytes([1] * 12),                                                       # NOP run
+             bytes([3, 3, 7, 1, 2, 4, 5]) + bytes([0]),                             # WS, NOP, MSS, EOL
+             bytes([2, 4, 5, 0xb4, 3, 3, 7, 8, 9, 9, 9, 9]),                        # 2nd TLV past the list
+             bytes([2, 4, 5, 0xb4, 3, 1, 1, 1]),                                    # 2nd TLV length 1
+             bytes([2, 4, 5, 0xb4, 3, 5, 7, 7]),                                    # 2nd TLV one byte past the list
+             bytes([2, 4, 5, 0xb4, 3, 4, 7, 7]),                                    # 2nd TLV ends the list exactly
+             bytes([2, 4, 5, 0xb4, 1, 1, 1, 3]),                                    # TLV kind at the last byte
+             bytes([4, 2, 8, 10]) + bytes(8) + bytes([1, 3, 3, 7, 2, 4, 5, 0xb4, 0, 0, 0, 0])]  # doff 10 / EOL run
+    f = []
+    for opts in lists:
+        for plen in (0, 1, 6, 40, 600):
+            body = bytes(rng.integers(0, 256, plen, dtype=np.uint8))
+            seg = _tcp(body, opts)
+            f.append(_eth(_ipv4(seg, 6)))
+            f.append(_eth(_ipv4(seg, 6, ihl=6, opts=bytes([1, 1, 1, 0]))))
+            f.append(_eth(_ipv6(seg, 6), 0x86DD))
+            f.append(_eth(_ipv4(seg, 6)) + bytes(5))  # Ethernet padding
     return f
 
 

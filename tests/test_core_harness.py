@@ -267,3 +267,26 @@ def test_ipv4_options_fast_path(oracle):
                 assert taken.sum() > 0.6 * v4opt.sum(), (int(taken.sum()), int(v4opt.sum()))
             # the Q17 frames (re-serialised header longer than the packet) too
             assert (taken & ((want["flags"] & abi.C_IP_PANIC) != 0)).sum() > 0 or flags
+
+
+def test_tcp_option_walk_fast_path(oracle):
+    """The general TCP option walk on the span kernel's fast path (round 4):
+    helpers.tcp_walk_frames (SYN lists of common stacks, EOL with junk after
+    it, Q13 cuts after the first option) at four byte alignments, lenient and
+    strict, through the span-group emulation equal the oracle, and the IPv4
+    frames whose list ends by byte 80 are taken, not declined."""
+    frames = helpers.tcp_walk_frames(np.random.default_rng(9))
+    for shift in (0, 1, 2, 3):
+        po = np.zeros(len(frames) + 1, np.int64)
+        np.cumsum([len(x) for x in frames], out=po[1:])
+        data = np.frombuffer(bytes(shift) + b"".join(frames) + bytes(16), np.uint8)
+        for flags in (0, abi.PARSE_STRICT):
+            dec = np.zeros(len(frames), np.uint8)
+            got = harness.span_groups(data, po + shift, flags=flags, declined=dec)
+            want = oracle.parse_frames(frames, flags=flags)
+            helpers.records_equal(got, want, frames, f"tcp walk span groups shift={shift} flags={flags}")
+            walked = (want["flags"] & abi.L_TCP) != 0
+            inwin = walked & ((want["l4_off"].astype(np.int64) + want["l4_length"]) <= 80)
+            assert inwin.sum() > 100 and (dec[inwin] == 0).all(), int(dec[inwin].sum())
+            q13 = ((want["flags"] & abi.L_TRANSPORT) != 0) & ~walked
+            assert q13.sum() > 20
