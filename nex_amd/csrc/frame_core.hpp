@@ -721,7 +721,13 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
         }
         return true;
     }
-    if (v4 && hl != 5u && !oslot) return false;  // options, no slot to walk them in
+#ifndef NEXG_FAST_V4OPT
+#define NEXG_FAST_V4OPT 1
+#endif
+#ifndef NEXG_FAST_TCPWALK
+#define NEXG_FAST_TCPWALK 1
+#endif
+    if (v4 && hl != 5u && (!oslot || !NEXG_FAST_V4OPT)) return false;  // options, no slot to walk them in
     const uint32_t hb = v6 ? 40u : 4u * hl;        // IP header bytes (v4: options included)
     const uint32_t l4 = 14u + hb;
     const uint32_t decl = v6 ? 40u + wbe16(w0, 18) : (decl16 ? decl16 : avail);
@@ -866,7 +872,7 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     // leave the branch
     uint32_t gv = 0, tcorr = 0;
     if (tcp && !tfail && doff > 5u && !tsopt) {
-        if (!oslot || l4 + 4u * doff > 80u) return false;
+        if (!oslot || !NEXG_FAST_TCPWALK || l4 + 4u * doff > 80u) return false;
         if (!sd) {
 #pragma unroll
             for (int k = 0; k < 5; k++)
