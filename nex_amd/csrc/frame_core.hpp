@@ -671,22 +671,8 @@ NEXG_HD uint32_t wbyte(const uint32_t (&w)[20], uint32_t i) { return (w[i >> 2] 
 NEXG_HD uint32_t wbe16(const uint32_t (&w)[20], uint32_t i) { return (wbyte(w, i) << 8) | wbyte(w, i + 1); }
 NEXG_HD uint32_t wle16(const uint32_t (&w)[20], uint32_t i) { return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFFFu; }
 
-// The window's own 80-B scratch slot (k_parse_span: the lane's LDS slot,
-// free after the sub-tile loop) for IPv4 options: the window is stored there
-// and the options walk, its sums and the shift of the L4 bytes read it back
-// with run-time addresses, where in registers they would need run-time
-// indexing (which puts the window in scratch) or a select network on every
-// frame. nullptr: IPv4 options are declined.
-NEXG_HD uint32_t oslot_le_range(const uint8_t* o, uint32_t a, uint32_t b) {  // LE halfword sum of [a, b), a even
-    uint32_t s = 0;
-#pragma unroll 1
-    for (uint32_t j = a & ~3u; j < b; j += 4)
-        s += halves(*reinterpret_cast<const uint32_t*>(o + j) & range_mask(j, a, b));
-    return s;
-}
-
 NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t opt_flags,
-                              uint64_t tail_sum, uint32_t tail_end, nexg_record& r, uint8_t* oslot = nullptr) {
+                              uint64_t tail_sum, uint32_t tail_end, nexg_record& r) {
     if (opt_flags & NEXG_PARSE_FROM_IP) return false;
     if (len < 14u) {  // Q2 (ethernet.rs:310-316), exactly as parse_frame reports it
         r = nexg_record{};
@@ -721,15 +707,8 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
         }
         return true;
     }
-#ifndef NEXG_FAST_V4OPT
-#define NEXG_FAST_V4OPT 1
-#endif
-#ifndef NEXG_FAST_TCPWALK
-#define NEXG_FAST_TCPWALK 1
-#endif
-    if (v4 && hl != 5u && (!oslot || !NEXG_FAST_V4OPT)) return false;  // options, no slot to walk them in
-    const uint32_t hb = v6 ? 40u : 4u * hl;        // IP header bytes (v4: options included)
-    const uint32_t l4 = 14u + hb;
+    if (v4 && hl != 5u) return false;  // options
+    const uint32_t l4 = v6 ? 54u : 34u;
     const uint32_t decl = v6 ? 40u + wbe16(w0, 18) : (decl16 ? decl16 : avail);
     if (strict && decl > avail) return false;
     const uint32_t ipl = decl < avail ? decl : avail;  // IP bytes parsed (v4: total_length)
@@ -764,81 +743,14 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     const bool inwin = e <= 80u;  // checksummed bytes all in the window
     if (e != len && e != tail_end && !inwin) return false;
     const uint32_t n = e - l4;
-    const bool tcp = pv == 6u, udp = pv == 17u, icmp = pv == (v6 ? 58u : 1u);
-    // IPv4 options move the L4 header to 14 + 4 * IHL: its bytes (TCP: with
-    // the four option-layout bytes) must lie in the window, or the IP bytes
-    // end inside it
-    const uint32_t sd = v6 ? 0u : hl - 5u;  // window shift in dwords (below)
-    if (sd && e > 80u && l4 + (tcp ? 24u : udp ? 8u : icmp ? 4u : 0u) > 80u) return false;
     uint32_t w[20];
 #pragma unroll
     for (int k = 0; k < 20; k++) w[k] = 4u * k >= e ? 0u : (w0[k] & range_mask(4u * k, 0, e));
     if (inwin) tail_sum = 0;
-    // IPv4 options (IHL 6..15): one branch a wave without them skips. The
-    // walk of ipv4.rs:442-508 over the window's bytes in the slot: stop = the
-    // end of the re-serialisable prefix, nopt = the options taken; a list that
-    // does not walk (a TLV cut by the header end, a length below 2 or past
-    // it) ends there, lenient only (strict declines). Then ipv4::checksum
-    // (ipv4.rs:932-938) over to_bytes()[..4 * IHL]: the header re-serialised
-    // to hl_ser bytes (options up to stop, zero padded), total length hl_ser +
-    // payload, and, when hl_ser < 4 * IHL, the first payload bytes [l4, l4 +
-    // 4 * IHL - hl_ser) in the header's place (Q16; Q17 -- to_bytes shorter
-    // than the header, a panic in the reference -- is NEXG_C_IP_PANIC; past
-    // the window: declined). Last, window dwords 9..19 are re-read from the
-    // slot IHL - 5 dwords further on, so the rest of this function reads an
-    // IHL-5 frame: the L4 header at 34, the bytes shifted in from past 80
-    // zero, the frame's bytes from 80 on in tail_sum either way.
-    uint32_t optv = 0;  // IP checksum | nopt << 16 | Q17 (no checksum) << 24
-    if (sd) {
-#pragma unroll
-        for (int k = 0; k < 5; k++)
-            reinterpret_cast<uint4*>(oslot)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-        uint32_t stop = hb, nopt = 0;
-        bool werr = false;
-#pragma unroll 1
-        for (uint32_t i = 20u; i < hb;) {
-            const uint32_t num = oslot[14u + i] & 0x1Fu;
-            if (num == 0u) {  // EOL
-                nopt++;
-                stop = i + 1u;
-                break;
-            }
-            if (num == 1u) {  // NOP
-                nopt++;
-                i++;
-                continue;
-            }
-            const uint32_t l = i + 1u < hb ? oslot[15u + i] : 0u;
-            if (i + 2u > hb || l < 2u || i + l > hb) {
-                werr = true;
-                stop = i;
-                break;
-            }
-            nopt++;
-            i += l;
-        }
-        if (werr && strict) return false;
-        const uint32_t hl_ser = 20u + ((stop - 20u + 3u) & ~3u);
-        const bool panic = hl_ser + n < hb;
-        if (!panic && l4 + (hb - hl_ser) > 80u) return false;
-        const uint32_t tot_ser = hl_ser + n < 65535u ? hl_ser + n : 65535u;
-        const uint32_t p4o = wle16(w, 26) + wle16(w, 28) + wle16(w, 30) + wle16(w, 32);
-        // (Q17: no checksum, and the payload range may run past the slot)
-        const uint32_t opt =
-            panic ? 0u : oslot_le_range(oslot, 34u, 14u + stop) + oslot_le_range(oslot, l4, l4 + (hb - hl_ser));
-        const uint64_t tip = 256ull * (((0x40u | (hl_ser >> 2)) | (wbyte(w, 15) << 8)) + wle16(w, 18) +
-                                       wle16(w, 20) + (wbyte(w, 22) | pv << 8) + p4o + opt) + tot_ser;
-        optv = (panic ? 1u << 24 : fold_complement(tip)) | nopt << 16;
-        // the shift: dword 8 keeps the destination address's low half (bytes
-        // 32..33), bytes 34.. come from 34 + 4 * sd on
-        const uint32_t* o32 = reinterpret_cast<const uint32_t*>(oslot);
-        w[8] = (w[8] & 0xFFFFu) | (o32[8u + sd] & 0xFFFF0000u);
-#pragma unroll
-        for (uint32_t k = 9; k < 20; k++) w[k] = k + sd < 20u ? o32[k + sd] : 0u;
-    }
     // L4 header words at l4 + k (compile-time extraction for both offsets + select)
     auto L = [&](uint32_t k) { return v6 ? wbe16(w, 54u + k) : wbe16(w, 34u + k); };
     auto LE = [&](uint32_t k) { return v6 ? wle16(w, 54u + k) : wle16(w, 34u + k); };
+    const bool tcp = pv == 6u, udp = pv == 17u, icmp = pv == (v6 ? 58u : 1u);
     const uint32_t doff = L(12) >> 12, ulen = L(4);
     const uint32_t o0 = v6 ? w[18] : w[13], o1 = v6 ? w[19] : w[14];
     const uint32_t b20 = (o0 >> 16) & 0xFFu, b21 = o0 >> 24, b22 = o1 & 0xFFu, b23 = (o1 >> 8) & 0xFFu;
@@ -847,7 +759,7 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     // past the data offset ends the walk of tcp.rs:767-818 with an error
     // (InvalidLength / Truncated): no TcpPacket (Q13), like a short header
     const bool walkfail = doff > 5u && b20 >= 2u && (b21 < 2u || b21 > olen);
-    bool tfail = tcp && (n < 20u || doff < 5u || 4u * doff > n || walkfail);  // no TcpPacket
+    const bool tfail = tcp && (n < 20u || doff < 5u || 4u * doff > n || walkfail);  // no TcpPacket
     const bool q14 = udp && (n < 8u || ulen < 8u || ulen > n);                       // no UdpPacket
     // TCP option lists of one TLV, alone (MSS of a SYN-ACK: 02 04 ..) or
     // behind NOP, NOP (timestamps, RFC 7323's layout for most data segments;
@@ -859,66 +771,7 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     const bool one = b20 >= 2u && b21 >= 2u && b21 == olen;
     const bool nnx = b20 == 1u && b21 == 1u && b22 >= 2u && b23 >= 2u && 2u + b23 == olen;
     const bool tsopt = tcp && !tfail && doff > 5u && (one || nnx);
-    // any other option list that lies in the window: the walk of
-    // tcp.rs:767-818 over the window's bytes in the slot (frame coordinates,
-    // as stored before the IPv4 options shift). A list that does not walk
-    // has no TcpPacket (Q13, as tfail); one that does re-serialises to the
-    // options up to the first EOL, zero padded to hl_ser (tcp.rs:521-575):
-    // the checksum drops the bytes [stop, 4 * doff) and sums the re-serialised
-    // data offset and length
-    // gv: nopt | 1 << 8 for a walked list; tcorr: what re-serialisation changes
-    // in the TCP checksum sum (mod 0xFFFF, as an addend: the dropped bytes
-    // [stop, 4 * doff), the data offset and length words), so only two values
-    // leave the branch
-    uint32_t gv = 0, tcorr = 0;
-    if (tcp && !tfail && doff > 5u && !tsopt) {
-        if (!oslot || !NEXG_FAST_TCPWALK || l4 + 4u * doff > 80u) return false;
-        if (!sd) {
-#pragma unroll
-            for (int k = 0; k < 5; k++)
-                reinterpret_cast<uint4*>(oslot)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-        }
-        const uint32_t hlt = 4u * doff;
-        uint32_t stop = hlt, nopt = 0;
-        bool ok = true;
-#pragma unroll 1
-        for (uint32_t off = 20u; off < hlt;) {
-            const uint32_t kind = oslot[l4 + off];
-            off++;
-            if (kind == 0u) {  // EOL: taken, the walk stops
-                nopt++;
-                stop = off;
-                break;
-            }
-            if (kind == 1u) {  // NOP
-                nopt++;
-                continue;
-            }
-            if (off >= hlt) {  // Malformed
-                ok = false;
-                break;
-            }
-            const uint32_t l = oslot[l4 + off];
-            off++;
-            if (l < 2u || off + (l - 2u) > hlt) {  // InvalidLength / Truncated
-                ok = false;
-                break;
-            }
-            nopt++;
-            off += l - 2u;
-        }
-        if (!ok) {
-            tfail = true;
-        } else {
-            const uint32_t hl_ser = 20u + ((stop - 20u + 3u) & ~3u);
-            const uint32_t skipped = stop < hlt ? oslot_le_range(oslot, l4 + stop, l4 + hlt) : 0u;
-            // (data offset nibble: x16 in the LE half, x256 as BE; length: BE)
-            const uint32_t drop = (256u * (16u * (doff - (hl_ser >> 2)) + skipped) + (hlt - hl_ser)) % 0xFFFFu;
-            tcorr = drop ? 0xFFFFu - drop : 0u;
-            gv = nopt | 1u << 8;
-        }
-    }
-    if (udp && !q14 && ulen != n) return false;
+    if ((tcp && !tfail && doff != 5u && !tsopt) || (udp && !q14 && ulen != n)) return false;
     const bool tonly = tfail || q14;                                  // transport layer, no packet
     const bool none = !(tcp || udp || icmp) || (icmp && n < 8u);      // no transport layer
     const bool l4ok = !(tonly || none);
@@ -931,8 +784,8 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
         return (s & 2u) ? suf[(s >> 2) + 1] + (w[s >> 2] >> 16) : suf[s >> 2];
     };
     const uint32_t h = tcp ? 20u : (udp ? 8u : 4u);
-    // s in {38,42,54,58,62,74} (window coordinates): select among compile-time evaluations
-    const uint32_t s_start = (v6 ? 54u : 34u) + h;
+    // s in {38,42,54,58,62,74}: select among compile-time evaluations
+    const uint32_t s_start = l4 + h;
     uint32_t rw;
     switch (s_start) {
         case 38: rw = rest(38); break;
@@ -955,7 +808,6 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     else hdr = LE(0);
     uint64_t t4 = 256ull * ((icmp && !v6 ? 0u : pseudo) + hdr + restsum);
     t4 += (icmp && !v6) ? 0u : (pv + n);  // pseudo proto + length (BE constants)
-    t4 += tcorr;  // a walked TCP list: its re-serialisation (0 otherwise)
     if (udp) t4 += n;                     // UDP length word as serialised
     const uint32_t l4_calc = fold_complement(t4);
     const uint32_t l4_cs = tcp ? L(16) : (udp ? L(6) : L(2));
@@ -967,11 +819,10 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     if (!v6) {  // ipv4.rs:932-938 over to_bytes(): total_length = 20 + payload, protocol value()
         const uint64_t tip =
             256ull * (wle16(w, 14) + wle16(w, 18) + wle16(w, 20) + (wbyte(w, 22) | pv << 8) + p4) + ipl;
-        const uint32_t ip_calc = sd ? optv & 0xFFFFu : fold_complement(tip);  // options: from the branch above
+        const uint32_t ip_calc = fold_complement(tip);
         const uint32_t ip_cs = wbe16(w, 24);
-        fl |= (optv >> 24) ? NEXG_C_IP_PANIC : NEXG_C_IP_CHECKED | (ip_calc == ip_cs ? NEXG_C_IP_OK : 0u);
-        r.ip_ver_ihl = (uint8_t)b14;
-        r.ip_nopt = (uint8_t)(optv >> 16);
+        fl |= NEXG_C_IP_CHECKED | (ip_calc == ip_cs ? NEXG_C_IP_OK : 0u);
+        r.ip_ver_ihl = 0x45;
         r.ip_tos = (uint8_t)wbyte(w, 15);
         r.ip_length = (uint16_t)ipl;
         r.ip_word = (wbe16(w, 18) << 16) | wbe16(w, 20);
@@ -1013,13 +864,13 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
         r.tcp_seq = (L(4) << 16) | L(6);
         r.tcp_ack = (L(8) << 16) | L(10);
         r.l4_length = (uint16_t)(4u * doff);
-        r.l4_nopt = tsopt ? (nnx ? 3u : 1u) : gv & 0xFFu;
+        r.l4_nopt = tsopt ? (nnx ? 3u : 1u) : 0u;
         r.l4_type = (uint8_t)L(12);
         r.l4_code = (uint8_t)(L(12) >> 8);
         r.tcp_window = (uint16_t)L(14);
         r.tcp_urg = (uint16_t)L(18);
     }
-    const uint32_t hp = tsopt || gv ? 4u * doff : h;  // header bytes before the payload
+    const uint32_t hp = tsopt ? 4u * doff : h;  // header bytes before the payload
     r.payload_off = (uint16_t)(n > hp ? l4 + hp : 0u);
     r.payload_len = (uint16_t)(n - hp);
     return true;
@@ -1037,7 +888,6 @@ NEXG_HD uint32_t canonical80_code(const nexg_record& r) {
     if (f >> NEXG_STATUS_SHIFT) return 10u + ((f >> NEXG_STATUS_SHIFT) & 7u);  // BufferTooShort (len < 14): 11
     if (!(f & (NEXG_L_IPV4 | NEXG_L_IPV6))) return (f & NEXG_L_IP) ? (uint32_t)NEXG_SHAPE_IP_NONE : (uint32_t)NEXG_SHAPE_ETH_ONLY;
     const bool v6 = (f & NEXG_L_IPV6) != 0, l4 = (f & NEXG_C_L4_CHECKED) != 0;
-    if (!v6 && r.ip_ver_ihl != 0x45u) return 0u;  // IPv4 options: no shape has them
     const uint32_t shape = !l4 ? (v6 ? 9u : 8u) : ((v6 ? 4u : 1u) + ((f & NEXG_L_UDP) ? 0u : (f & NEXG_L_TCP) ? 1u : 2u));
     const uint32_t end = !l4 ? (v6 ? 54u : 34u) : r.l4_off + ((f & NEXG_L_UDP) ? 8u : (f & NEXG_L_TCP) ? 20u : 4u);
     const bool coded = (l4 || !(f & NEXG_L_TRANSPORT)) && end + r.payload_len == r.packet_len;

@@ -724,8 +724,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // Q weights bytes by absolute parity; fast_canonical80 wants the
         // frame-relative LE sum: x256 (mod 0xFFFF) for a frame at an odd address
         const uint64_t tail = (sh & 1u) ? (uint64_t)tq * 256u : (uint64_t)tq;
-        // IPv4 options walk in the lane's own slot (free after the loop)
-        if (fast_canonical80(w, len, a.opt_flags, tail, qend, r, slots + SpanFrame::kSlot * t)) {
+        if (fast_canonical80(w, len, a.opt_flags, tail, qend, r)) {
             if (sparse_like(OUT)) code = canonical80_code(r);
             if (OUT == NEXG_OUT_RECORD) stage_record(slots + SpanFrame::kSlot * t, r);
         } else {  // declined: the window goes to this lane's slot for pass (B)

@@ -67,10 +67,7 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                 // the second prefix value at span_tail_end (the IP end of a padded frame)
                 const uint32_t te = nexg::span_tail_end(w80[3], w80[4], (uint32_t)len, flags);
                 const uint32_t tail = len > 80 ? Q(o + te) - Q(o + 80u) : 0u;
-                alignas(16) uint8_t oslot[80];  // the span kernel's lane slot (IPv4 options walk)
-                memset(oslot, 0xA5, sizeof(oslot));
-                if (nexg::fast_canonical80(w80, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, te, r,
-                                           oslot)) {
+                if (nexg::fast_canonical80(w80, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, te, r)) {
                     // the span kernel stores canonical80_code for these: it must be the encoder's code
                     if (nexg::canonical80_code(r) != nexg::sparse_encode(r, flags, ip_offset)) return -2;
                 } else {
@@ -202,7 +199,7 @@ extern "C" int harness_span_groups(const uint8_t* data, uint64_t data_bytes, con
             tq[t] = len[t] > W ? q : 0u;
             nexg_record r{};
             const uint64_t tail = ((base + off) & 1u) ? (uint64_t)tq[t] * 256u : (uint64_t)tq[t];
-            if (nexg::fast_canonical80(w, len[t], flags, tail, qend[t], r, lds + S * t)) {
+            if (nexg::fast_canonical80(w, len[t], flags, tail, qend[t], r)) {
                 out[f0 + t] = r;
             } else {
                 gen[t] = true;
