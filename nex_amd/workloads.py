@@ -61,8 +61,11 @@ def mutate_packed(data, offs, seed: int = abi.DEFAULT_SEED, mutate_share: float 
     buf[offs[i] + 14] = rng.integers(0, 256, len(i))
     i = sel("l4_length")  # UDP length / TCP data offset / ICMP type area of a v4 or v6 frame
     l4 = offs[i] + np.where(eth_v4[i], 34, 54)
-    buf[l4 + 4] = rng.integers(0, 256, len(i))
-    buf[l4 + 12] = rng.integers(0, 256, len(i))
+    v4b, v12 = rng.integers(0, 256, len(i)), rng.integers(0, 256, len(i))
+    end = offs[i + 1]  # a 64-B IPv6/UDP frame ends at byte 62 + 2: byte l4 + 12 is past it
+    buf[l4 + 4] = np.where(l4 + 4 < end, v4b, buf[np.minimum(l4 + 4, len(buf) - 1)])
+    k = l4 + 12 < end
+    buf[l4[k] + 12] = v12[k]
     i = sel("proto200")
     buf[offs[i] + np.where(eth_v4[i], 23, 20)] = 200
     i = sel("random")
@@ -105,7 +108,7 @@ def mutate_packed(data, offs, seed: int = abi.DEFAULT_SEED, mutate_share: float 
         sel = plain[c0:c0 + (1 << 16)]
         ramp = _ramp(new_len[sel])
         out[np.repeat(new_offs[:-1][sel], new_len[sel]) + ramp] = buf[np.repeat(offs[:-1][sel], new_len[sel]) + ramp]
-    for j in np.nonzero(~plain)[0]:
+    for j in np.nonzero((ins != 0) | (pad != 0))[0]:  # the frames the gathers above left out
         f = buf[offs[j]:offs[j + 1]]
         if pad[j]:
             f = np.concatenate([f, rng.integers(0, 256, pad[j], dtype=np.uint8)])

@@ -35,6 +35,7 @@ for s in ${STEPS:-tests}; do
     rehearse8) step rehearse8 900 env NEXG_DIST_BACKEND=gloo python bench.py --gpus 8 --steps 10 --warmup 3 --cpu-seconds 2 --no-large ;;
     benchimix) step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5 ;;
     pmc) step pmc 900 bash tools/pmc.sh ;;
+    sqkinds) step sqkinds 900 bash tools/sq_kinds.sh ;;
     abser) step ab_ser 300 python -u tools/bench_ser_ab.py --libs ${LIBS} --shape ${SHAPE:-tuples} --rounds 4 ;;
     # in-process A/B of library variants under abvar/ (LIBS=a,b,...): IMIX with an output check, then the mixes
     abspan) step ab_imix 600 python -u tools/bench_parse_ab.py --libs ${LIBS} --workloads imix,udp64 --out grouped --check --rounds 4
