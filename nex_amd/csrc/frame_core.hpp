@@ -293,7 +293,8 @@ struct SpanFrame {
             // or, for a range to the tail end, the tail minus the window's bytes
             // before it
             const bool all = gb <= ee;
-            acc += all ? ext_sum(ga, gb) : (uint64_t)(tail - ext_sum(80u, ga));
+            const uint32_t es = ext_sum(all ? ga : 80u, all ? gb : ga);  // one window loop per call site
+            acc += all ? (uint64_t)es : (uint64_t)(tail - es);
         } else if (ga < gb) {
             const uint64_t base = reinterpret_cast<uint64_t>(g);
             if (gb - ga > kDefer && d.rng == 0) {
