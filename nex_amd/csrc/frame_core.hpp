@@ -236,41 +236,17 @@ struct SpanFrame {
     uint32_t tail;      // absolute-parity sum of [80, tail_end) (when tail_end > 80)
     mutable SpanDeferred d{};
     mutable bool pend = false;
-    // extension window: frame bytes [80, ext >> 16) are also staged in LDS,
-    // byte i at slot + i + (int16_t)ext (a free slot of the workgroup holding
-    // the 16-B chunks from byte 80's chunk on); 0: none. The extension slot is
-    // never the workgroup's first (LDS address 0), so slot + (int16_t)ext + i0
-    // for any run start i0 >= 0 -- the VGPR base the compiler keeps for a byte
-    // run -- stays at or above the shared aperture's base (see u8)
-    uint32_t ext = 0;
 
-    // one generic (flat) byte load from the slot, the extension or HBM: no
-    // divergent branch.
+    // one generic (flat) byte load from the slot or HBM: no divergent branch.
     // Only object start + non-negative index here: the compiler keeps one VGPR
     // base per byte run and folds the run's index into the FLAT immediate, and
     // a FLAT access takes its aperture from that VGPR base — a negative
     // displacement of the LDS pointer (round 3's extension windows) put the
     // base below the shared aperture and faulted (profiles/r03/ext_attempt/)
     NEXG_HD uint32_t u8(uint32_t i) const {
-        const bool staged = i < (ext >> 16);
-        NEXG_SPAN_PROBE(0, i >= kSlot && !staged);  // host harness counters (no-op in the library)
-        const uint8_t* p = (i < kSlot || staged ? slot : g) +
-                           (i < kSlot ? (int32_t)i : staged ? (int32_t)i + (int32_t)(int16_t)(ext & 0xFFFFu) : (int32_t)i);
+        NEXG_SPAN_PROBE(0, i >= kSlot);  // host harness counters (no-op in the library)
+        const uint8_t* p = i < kSlot ? slot + i : g + i;
         return *p;
-    }
-    // little-endian halfword sum, absolute-address parity, of frame bytes
-    // [a, b) inside the extension window (80 <= a <= b <= ext >> 16): dword
-    // reads from the window's slot, which holds the 16-B chunks as they lie
-    // in memory. Its start slot + delta + 80 - xo is the free slot itself
-    // (xo = byte 80's offset in its chunk), never below LDS address 80
-    NEXG_HD uint32_t ext_sum(uint32_t a, uint32_t b) const {
-        const int32_t delta = (int32_t)(int16_t)(ext & 0xFFFFu);
-        const uint32_t xo = (uint32_t)(delta + (int32_t)kSlot) & 15u;
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(slot + (delta + (int32_t)kSlot - (int32_t)xo));
-        const uint32_t pa = a - kSlot + xo, pb = b - kSlot + xo;
-        uint32_t s = 0;
-        for (uint32_t j = pa & ~3u; j < pb; j += 4) s += halves(w[j >> 2] & range_mask(j, pa, pb));
-        return s;
     }
     NEXG_HD uint64_t le_sum(uint32_t a, uint32_t b) const {
         uint64_t acc = 0;
@@ -284,18 +260,7 @@ struct SpanFrame {
         const uint32_t ga = a > kSlot ? a : kSlot;
         const bool to_end = b == tail_end && tail_end > 80u && ga <= 80u;
         const uint32_t gb = to_end ? 80u : b;
-        const uint32_t ee = ext >> 16;  // extension window: frame bytes [80, ee) in LDS
-#ifndef NEXG_EXT_SUMS
-#define NEXG_EXT_SUMS 1
-#endif
-        if (NEXG_EXT_SUMS && ga < gb && ga < ee && (gb <= ee || (gb == tail_end && tail_end > 80u))) {
-            // from the window (absolute parity, like the tail): the range itself,
-            // or, for a range to the tail end, the tail minus the window's bytes
-            // before it
-            const bool all = gb <= ee;
-            const uint32_t es = ext_sum(all ? ga : 80u, all ? gb : ga);  // one window loop per call site
-            acc += all ? (uint64_t)es : (uint64_t)(tail - es);
-        } else if (ga < gb) {
+        if (ga < gb) {
             const uint64_t base = reinterpret_cast<uint64_t>(g);
             if (gb - ga > kDefer && d.rng == 0) {
                 d.rng = ga | (gb - ga) << 16;
