@@ -23,7 +23,7 @@ for s in ${STEPS:-tests}; do
     bench) step bench_udp64 500 python bench.py --steps 50 --cpu-seconds 5 ;;
     driverbench) step bench_driver 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     malformedtests) step pytest_malformed 600 python -u -m pytest tests/test_gpu_malformed.py tests/test_gpu_span.py -q -x --timeout 300 --timeout-method thread ;;
-    newtests4) step pytest_new4 600 python -u -m pytest tests/test_gpu_tcp_options.py tests/test_gpu_build_probe.py "tests/test_gpu_parity.py::test_build_udp4_tuples_aos" tests/test_cpp_api.py -q -x --timeout 300 --timeout-method thread ;;
+    newtests4) step pytest_new4 600 python -u -m pytest tests/test_gpu_launch.py tests/test_gpu_tcp_options.py tests/test_gpu_build_probe.py "tests/test_gpu_parity.py::test_build_udp4_tuples_aos" tests/test_cpp_api.py -q -x --timeout 300 --timeout-method thread ;;
     malformed) step bench_malformed 500 python tools/bench_malformed.py ;;
     benchpcap) step bench_pcap 400 python bench.py --workload imix_pcap --steps 20 --cpu-seconds 5 ;;
     ser) step bench_ser 300 python bench.py --workload ser --steps 50 --no-cpu-baseline
