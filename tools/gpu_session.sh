@@ -46,7 +46,7 @@ for s in ${STEPS:-tests}; do
           step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 60 --warmup 25 --no-cpu-baseline
           step prof_malformed 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_malformed -o run -- python3 bench.py --workload malformed --steps 60 --warmup 25 --no-cpu-baseline
           step prof_real 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_real -o run -- python3 bench.py --workload real_traffic --steps 60 --warmup 25 --no-cpu-baseline
-          step prof_large 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_large -o run -- python3 bench.py --frames 54525952 --steps 60 --warmup 25 --no-cpu-baseline
+          step prof_large 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_large -o run -- python3 bench.py --frames 54525952 --steps 60 --warmup 25 --no-cpu-baseline --no-imix
           step prof_ser 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser -o run -- python3 bench.py --workload ser --steps 60 --warmup 25 --no-cpu-baseline
           step prof_ser_tuples 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser_tuples -o run -- python3 bench.py --workload ser --ser-shape tuples --steps 60 --warmup 25 --no-cpu-baseline
           step prof_ser_aos 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ser_aos -o run -- python3 bench.py --workload ser --ser-shape tuples_aos --steps 60 --warmup 25 --no-cpu-baseline ;;
