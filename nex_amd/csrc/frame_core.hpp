@@ -243,37 +243,16 @@ struct SpanFrame {
     // a FLAT access takes its aperture from that VGPR base — a negative
     // displacement of the LDS pointer (round 3's extension windows) put the
     // base below the shared aperture and faulted (profiles/r03/ext_attempt/)
-#ifndef NEXG_SPAN_LDS_U8
-#define NEXG_SPAN_LDS_U8 0
-#endif
-#ifndef NEXG_SPAN_LDS_SUM
-#define NEXG_SPAN_LDS_SUM 0
-#endif
     NEXG_HD uint32_t u8(uint32_t i) const {
         NEXG_SPAN_PROBE(0, i >= kSlot);  // host harness counters (no-op in the library)
-#if defined(__HIP_DEVICE_COMPILE__) && NEXG_SPAN_LDS_U8
-        // LDS-typed slot reads (ds_read_u8: the LDS pipeline, not the vector
-        // memory path the streaming loads of the other workgroups queue in);
-        // bytes past the slot by a (rare) branch to HBM
-        if (i < kSlot) return reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>(
-                                  reinterpret_cast<uintptr_t>(slot) & 0xFFFFFFFFu)[i];
-        return g[i];
-#else
         const uint8_t* p = i < kSlot ? slot + i : g + i;
         return *p;
-#endif
     }
     NEXG_HD uint64_t le_sum(uint32_t a, uint32_t b) const {
         uint64_t acc = 0;
         const uint32_t lb = b < kSlot ? b : kSlot;
         if (a < lb) {  // frame-relative LE sum, x256 for an odd frame (congruent, 0 iff 0)
-#if defined(__HIP_DEVICE_COMPILE__) && NEXG_SPAN_LDS_SUM
-            const __attribute__((address_space(3))) uint32_t* w =
-                reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(reinterpret_cast<uintptr_t>(slot) &
-                                                                                    0xFFFFFFFFu);
-#else
             const uint32_t* w = reinterpret_cast<const uint32_t*>(slot);
-#endif
             uint32_t s = 0;
             for (uint32_t j = a & ~3u; j < lb; j += 4) s += halves(w[j >> 2] & range_mask(j, a, lb));
             acc = parity ? (uint64_t)s * 256u : (uint64_t)s;

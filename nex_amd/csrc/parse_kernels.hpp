@@ -742,35 +742,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // path for the few declined lanes of each wave. Items: {span position,
     // len | tail end << 16, tail sum, owner lane} in the idle prefix buffer;
     // results go back through the owner's slot.
-#ifndef NEXG_SPAN_FEW
-#define NEXG_SPAN_FEW 0  // groups with at most this many declined frames skip the bucketing
-#endif
-    const uint32_t ngen = (uint32_t)__syncthreads_count(gen);
-    if (ngen) {
-        uint4* const items = reinterpret_cast<uint4*>(&s_pfx[0][0]);
-        if (ngen <= NEXG_SPAN_FEW) {  // few: items in lane order (per-wave ballot counts, one barrier)
-            const uint64_t m = __ballot(gen);
-            if (lane == 0) s_wsum[0][wv] = (uint32_t)__builtin_popcountll(m);
-            __syncthreads();
-            const uint4 ws = *reinterpret_cast<const uint4*>(s_wsum[0]);
-            const uint32_t wo = (wv > 0 ? ws.x : 0u) + (wv > 1 ? ws.y : 0u) + (wv > 2 ? ws.z : 0u);
-            if (gen) items[wo + lanes_below(m)] = make_uint4(hr, len | qend << 16, tq, t);
-        } else {
-            if (t < kBuckets) s_hist[t] = 0;
-            __syncthreads();
-            const uint32_t rank = gen ? atomicAdd(&s_hist[key], 1u) : 0u;
-            __syncthreads();
-            if (t == 0) {
-                uint32_t acc = 0;
-                for (uint32_t k = 0; k < kBuckets; k++) {
-                    const uint32_t c = s_hist[k];
-                    s_hist[kBuckets + k] = acc;
-                    acc += c;
-                }
+    if (__syncthreads_or(gen)) {
+        if (t < kBuckets) s_hist[t] = 0;
+        __syncthreads();
+        const uint32_t rank = gen ? atomicAdd(&s_hist[key], 1u) : 0u;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t acc = 0;
+            for (uint32_t k = 0; k < kBuckets; k++) {
+                const uint32_t c = s_hist[k];
+                s_hist[kBuckets + k] = acc;
+                acc += c;
             }
-            __syncthreads();
-            if (gen) items[s_hist[kBuckets + key] + rank] = make_uint4(hr, len | qend << 16, tq, t);
+            s_hist[2 * kBuckets] = acc;
         }
+        __syncthreads();
+        uint4* const items = reinterpret_cast<uint4*>(&s_pfx[0][0]);
+        if (gen) items[s_hist[kBuckets + key] + rank] = make_uint4(hr, len | qend << 16, tq, t);
+        const uint32_t ngen = s_hist[2 * kBuckets];
         __syncthreads();
         const bool work = t < ngen;
         nexg_record rr{};
