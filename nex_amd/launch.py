@@ -16,6 +16,7 @@ Nothing in this module imports torch; `decide` is a pure function of argv,
 env and a device count so the CPU tests can check every branch.
 """
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -89,12 +90,20 @@ def relay(cmd, env, out=None) -> int:
     0 without rank 0 printing a JSON line."""
     out = out or sys.stdout
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
-    saw_json = False
-    for line in proc.stdout:
-        out.write(line)
-        out.flush()
-        saw_json |= line.lstrip().startswith("{")
-    rc = proc.wait()
+    # a SIGTERM / SIGINT to this process goes on to the launcher, which stops
+    # its ranks (no orphaned ranks holding GPUs when a driver times the run out)
+    forward = lambda sig, _frame: proc.send_signal(sig)
+    old = {sig: signal.signal(sig, forward) for sig in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        saw_json = False
+        for line in proc.stdout:
+            out.write(line)
+            out.flush()
+            saw_json |= line.lstrip().startswith("{")
+        rc = proc.wait()
+    finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
     if rc == 0 and not saw_json:
         print("bench launcher: the ranks exited 0 but rank 0 printed no result line", file=sys.stderr)
         return 1

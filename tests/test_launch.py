@@ -108,3 +108,26 @@ def test_bench_refuses_gpus_without_devices():
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 2, r.stderr
     assert "GPU(s) visible" in r.stderr and "{" not in r.stdout
+
+
+def test_relay_forwards_sigterm(tmp_path):
+    """A SIGTERM to the launcher reaches the child (torch.distributed.run
+    stops its ranks on it): the child sees it and exits with its own code."""
+    child = tmp_path / "child.py"
+    child.write_text("import signal, sys, time\n"
+                     "signal.signal(signal.SIGTERM, lambda *a: (print('got term', flush=True), sys.exit(7)))\n"
+                     "print('ready', flush=True)\n"
+                     "time.sleep(60)\n")
+    parent = tmp_path / "parent.py"
+    parent.write_text("import os, sys\n"
+                      f"sys.path.insert(0, {ROOT!r})\n"
+                      "from nex_amd import launch\n"
+                      f"sys.exit(launch.relay([sys.executable, {str(child)!r}], dict(os.environ)))\n")
+    import signal
+    import time
+    p = subprocess.Popen([sys.executable, str(parent)], stdout=subprocess.PIPE, text=True)
+    assert p.stdout.readline().strip() == "ready"
+    time.sleep(0.2)
+    p.send_signal(signal.SIGTERM)
+    rest = p.stdout.read()
+    assert p.wait(timeout=30) == 7 and "got term" in rest
