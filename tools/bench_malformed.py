@@ -64,6 +64,9 @@ def main():
         rounds = 2 if len(engines) > 1 else 1
         times, same = [], []
         ref = None
+        if len(engines) > 1:  # an untimed pass of every build first: a fresh batch's first launches run slow
+            for e in engines:
+                timed(e)
         for rnd in range(rounds):
             # A B, then B A: the build measured first in a round pays for the
             # batch's first launches, so the order alternates
