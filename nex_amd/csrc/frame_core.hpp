@@ -236,26 +236,16 @@ struct SpanFrame {
     uint32_t tail;      // absolute-parity sum of [80, tail_end) (when tail_end > 80)
     mutable SpanDeferred d{};
     mutable bool pend = false;
-    // extension window: frame bytes [80, ext >> 16) are also staged in LDS,
-    // byte i at slot + i + (int16_t)ext (a free slot of the workgroup holding
-    // the 16-B chunks from byte 80's chunk on); 0: none. The extension slot is
-    // never the workgroup's first (LDS address 0), so slot + (int16_t)ext + i0
-    // for any run start i0 >= 0 -- the VGPR base the compiler keeps for a byte
-    // run -- stays at or above the shared aperture's base (see u8)
-    uint32_t ext = 0;
 
-    // one generic (flat) byte load from the slot, the extension or HBM: no
-    // divergent branch.
+    // one generic (flat) byte load from the slot or HBM: no divergent branch.
     // Only object start + non-negative index here: the compiler keeps one VGPR
     // base per byte run and folds the run's index into the FLAT immediate, and
     // a FLAT access takes its aperture from that VGPR base — a negative
     // displacement of the LDS pointer (round 3's extension windows) put the
     // base below the shared aperture and faulted (profiles/r03/ext_attempt/)
     NEXG_HD uint32_t u8(uint32_t i) const {
-        const bool staged = i < (ext >> 16);
-        NEXG_SPAN_PROBE(0, i >= kSlot && !staged);  // host harness counters (no-op in the library)
-        const uint8_t* p = (i < kSlot || staged ? slot : g) +
-                           (i < kSlot ? (int32_t)i : staged ? (int32_t)i + (int32_t)(int16_t)(ext & 0xFFFFu) : (int32_t)i);
+        NEXG_SPAN_PROBE(0, i >= kSlot);  // host harness counters (no-op in the library)
+        const uint8_t* p = i < kSlot ? slot + i : g + i;
         return *p;
     }
     NEXG_HD uint64_t le_sum(uint32_t a, uint32_t b) const {
@@ -680,27 +670,6 @@ NEXG_HD bool fast_udp4_64(const uint32_t (&w)[16], uint32_t opt_flags, nexg_reco
 NEXG_HD uint32_t wbyte(const uint32_t (&w)[20], uint32_t i) { return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFu; }
 NEXG_HD uint32_t wbe16(const uint32_t (&w)[20], uint32_t i) { return (wbyte(w, i) << 8) | wbyte(w, i + 1); }
 NEXG_HD uint32_t wle16(const uint32_t (&w)[20], uint32_t i) { return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFFFu; }
-
-// Whether the generic core will likely read frame bytes past the 80-B slot
-// (k_parse_span fills an extension window only for those frames): an L4
-// header that starts past byte 56 (IPv4 options, an IPv6 extension header),
-// or a TCP option list behind a plain IPv4 / IPv6 header that runs past byte
-// 80. A guess that only decides where bytes are read from, never a result;
-// compile-time window indices only (a run-time index puts the window in
-// scratch).
-NEXG_HD bool span_reads_past80(const uint32_t (&w)[20], uint32_t len, uint32_t opt_flags) {
-    if (len <= 80u || (opt_flags & NEXG_PARSE_FROM_IP)) return false;
-    const uint32_t et = wbe16(w, 12);
-    if (et == 0x0800u) {
-        const uint32_t l4 = 14u + 4u * (wbyte(w, 14) & 15u);
-        return l4 > 56u || (l4 == 34u && wbyte(w, 23) == 6u && (wbyte(w, 46) >> 4) > 11u);
-    }
-    if (et == 0x86DDu) {
-        const uint32_t nh = wbyte(w, 20);
-        return nh == 0u || nh == 43u || nh == 44u || nh == 60u || (nh == 6u && (wbyte(w, 66) >> 4) > 6u);
-    }
-    return false;
-}
 
 NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t opt_flags,
                               uint64_t tail_sum, uint32_t tail_end, nexg_record& r) {

@@ -581,11 +581,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     __shared__ uint32_t s_wsum[NB][4];
     __shared__ uint64_t s_span[2];
     __shared__ uint32_t s_hist[2 * kBuckets + 1];  // generic-pass bucket counts, bases, total
-    // generic pass, non-record outputs: the lanes whose slots are free (no
-    // declined frame; never lane 0, whose slot is at LDS address 0), in lane
-    // order; the i-th declined item's extension window goes to s_free[i]
-    constexpr bool kExt = OUT != NEXG_OUT_RECORD;
-    __shared__ uint8_t s_free[kExt ? kTile : 1];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint64_t f0 = (uint64_t)blockIdx.x * kTile;  // grid order: XCD order measured slower here
     const uint64_t idx = f0 + t;
@@ -717,7 +712,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint8_t* const slots = &s_bytes[0][0];  // 80 B per lane from here on
     // (A) every lane: the canonical fast path on its head window
     uint32_t code = 0, key = 0;
-    bool gen = false, far = false;  // far: the generic core will read past the slot (extension window)
+    bool gen = false;
     const uint32_t tq = want_tail ? qb - qa : 0u;
     if (have) {
         uint32_t w[20];
@@ -735,7 +730,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         } else {  // declined: the window goes to this lane's slot for pass (B)
             gen = true;
             key = span_bucket(w[3], w[5], a.opt_flags);
-            far = kExt && span_reads_past80(w, len, a.opt_flags);
 #pragma unroll
             for (int k = 0; k < 5; k++)
                 reinterpret_cast<uint4*>(slots + SpanFrame::kSlot * t)[k] =
@@ -749,17 +743,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // len | tail end << 16, tail sum, owner lane} in the idle prefix buffer;
     // results go back through the owner's slot.
     if (__syncthreads_or(gen)) {
-        const uint64_t fm = __ballot(!gen && t != 0u);  // lanes with a free slot
         if (t < kBuckets) s_hist[t] = 0;
-        if (kExt && lane == 0) s_wsum[0][wv] = (uint32_t)__builtin_popcountll(fm);
         __syncthreads();
         const uint32_t rank = gen ? atomicAdd(&s_hist[key], 1u) : 0u;
-        const uint4 fw = *reinterpret_cast<const uint4*>(s_wsum[0]);  // free slots per wave
-        const uint32_t nfree = kExt ? fw.x + fw.y + fw.z + fw.w : 0u;
-        if (kExt && !gen && t != 0u) {
-            const uint32_t wo = (wv > 0 ? fw.x : 0u) + (wv > 1 ? fw.y : 0u) + (wv > 2 ? fw.z : 0u);
-            s_free[wo + lanes_below(fm)] = (uint8_t)t;
-        }
         __syncthreads();
         if (t == 0) {
             uint32_t acc = 0;
@@ -772,26 +758,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         __syncthreads();
         uint4* const items = reinterpret_cast<uint4*>(&s_pfx[0][0]);
+        if (gen) items[s_hist[kBuckets + key] + rank] = make_uint4(hr, len | qend << 16, tq, t);
         const uint32_t ngen = s_hist[2 * kBuckets];
-        if (gen) {
-            const uint32_t ii = s_hist[kBuckets + key] + rank;
-            items[ii] = make_uint4(hr, len | qend << 16, tq, t | (far ? 1u << 8 : 0u));
-            // extension window: the 16-B chunks from frame byte 80's chunk on,
-            // as far as the frame goes (5 at most), into the item's free slot,
-            // all loads of the workgroup in flight together: the generic core's
-            // reads past byte 80 then hit LDS instead of waiting on HBM one by one
-            if (far && ii < nfree) {
-                const uint64_t c0 = (A0 + hr + kLaneWin) & ~15ull, end = A0 + hr + len;
-                uint8_t* es = slots + SpanFrame::kSlot * s_free[ii];
-                uint4 v[5];
-#pragma unroll
-                for (int k = 0; k < 5; k++)
-                    if (c0 + 16u * k < end) v[k] = load16(reinterpret_cast<const void*>(c0 + 16u * k));
-#pragma unroll
-                for (int k = 0; k < 5; k++)
-                    if (c0 + 16u * k < end) reinterpret_cast<uint4*>(es)[k] = v[k];
-            }
-        }
         __syncthreads();
         const bool work = t < ngen;
         nexg_record rr{};
@@ -800,20 +768,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (work) {
             const uint4 it = items[t];
             ghr = it.x;
-            owner = it.w & 0xFFu;
+            owner = it.w;
             SpanFrame f{slots + SpanFrame::kSlot * owner, reinterpret_cast<const uint8_t*>(A0 + ghr), it.y >> 16,
                         ghr & 1u, it.z};
-            const uint32_t glen = it.y & 0xFFFFu;
-            if (kExt && (it.w >> 8) && t < nfree) {
-                // frame byte i in [80, ee) at slot + i + delta; s_free[t] >= 1, so
-                // slot + delta + i0 >= 0 for every run start i0 (SpanFrame::ext)
-                const uint32_t xo = (uint32_t)((A0 + ghr + kLaneWin) & 15u);
-                const uint32_t ee = 2u * kLaneWin - xo < glen ? 2u * kLaneWin - xo : glen;
-                const int32_t delta = ((int32_t)s_free[t] - (int32_t)owner) * (int32_t)SpanFrame::kSlot + (int32_t)xo -
-                                      (int32_t)kLaneWin;
-                f.ext = ((uint32_t)delta & 0xFFFFu) | ee << 16;
-            }
-            parse_frame(f, ghr & 1u, glen, a.opt_flags, a.ip_offset, rr);
+            parse_frame(f, ghr & 1u, it.y & 0xFFFFu, a.opt_flags, a.ip_offset, rr);
             dfr = f.d;
         }
         // deferred checksum ranges (SpanFrame): four at a time, one per 16-lane

@@ -160,8 +160,6 @@ extern "C" int harness_sparse_decode(const uint8_t* codes, const uint32_t* lens,
 // Records out (the record form of what the sparse kernel encodes). Frames of a
 // group that is not packed (or a batch that is not) return -1.
 static uint8_t* g_span_declined;  // optional per-frame output: 1 = the generic core parsed it
-static int g_span_ext = 1;        // emulate the extension windows of the non-record outputs
-extern "C" void harness_span_ext(int on) { g_span_ext = on; }
 extern "C" void harness_span_declined(uint8_t* out) { g_span_declined = out; }
 static uint64_t g_span_stats[6];  // declined, declined past 80 B, deferred ranges, groups with a declined
                                   // frame, HBM byte loads, inline HBM range sums (the last two: NEXG_SPAN_PROBE)
@@ -185,7 +183,7 @@ extern "C" int harness_span_groups(const uint8_t* data, uint64_t data_bytes, con
         if (hi < lo || hi > data_bytes) { free(lds); return -1; }
         const uint64_t A0 = (base + lo) & ~15ull;
         memset(lds, 0xA5, T * S);
-        bool gen[T] = {}, far[T] = {};
+        bool gen[T] = {};
         uint32_t key[T] = {}, hr[T] = {}, len[T] = {}, qend[T] = {}, tq[T] = {};
         for (uint32_t t = 0; t < nf; t++) {
             const uint64_t off = offsets[f0 + t], l = offsets[f0 + t + 1] - off;
@@ -207,7 +205,6 @@ extern "C" int harness_span_groups(const uint8_t* data, uint64_t data_bytes, con
                 gen[t] = true;
                 if (g_span_declined) g_span_declined[f0 + t] = 1;
                 key[t] = nexg::span_bucket(w[3], w[5], flags);
-                far[t] = nexg::span_reads_past80(w, len[t], flags);
                 memcpy(lds + S * t, w, S);
             }
         }
@@ -217,29 +214,10 @@ extern "C" int harness_span_groups(const uint8_t* data, uint64_t data_bytes, con
             for (uint32_t t = 0; t < nf; t++)
                 if (gen[t] && key[t] == b) items[ngen++] = t;
         g_span_stats[3] += ngen > 0;
-        // extension windows (non-record outputs): the free slots (lanes without
-        // a declined frame, lane 0 never), the 16-B chunks from byte 80's chunk
-        // on into item ii's free slot, all filled before any item is parsed
-        uint32_t nfree = 0, sfree[T];
-        for (uint32_t t = 1; t < T; t++)
-            if (!gen[t]) sfree[nfree++] = t;
-        for (uint32_t ii = 0; ii < ngen && g_span_ext; ii++) {
-            const uint32_t t = items[ii];
-            if (!far[t] || ii >= nfree) continue;
-            const uint64_t c0 = (A0 + hr[t] + W) & ~15ull, end = A0 + hr[t] + len[t];
-            for (uint32_t k = 0; k < 5; k++)
-                if (c0 + 16u * k < end) memcpy(lds + S * sfree[ii] + 16u * k, reinterpret_cast<const void*>(c0 + 16u * k), 16);
-        }
         for (uint32_t ii = 0; ii < ngen; ii++) {
             const uint32_t t = items[ii];
             nexg_record rr{};
             nexg::SpanFrame f{lds + S * t, reinterpret_cast<const uint8_t*>(A0 + hr[t]), qend[t], hr[t] & 1u, tq[t]};
-            if (g_span_ext && far[t] && ii < nfree) {
-                const uint32_t xo = (uint32_t)((A0 + hr[t] + W) & 15u);
-                const uint32_t ee = 2u * W - xo < len[t] ? 2u * W - xo : len[t];
-                const int32_t delta = ((int32_t)sfree[ii] - (int32_t)t) * (int32_t)S + (int32_t)xo - (int32_t)W;
-                f.ext = ((uint32_t)delta & 0xFFFFu) | ee << 16;
-            }
             nexg::parse_frame(f, hr[t] & 1u, len[t], flags, ip_offset, rr);
             g_span_stats[0]++;
             g_span_stats[1] += len[t] > W;

@@ -30,8 +30,6 @@ def lib():
         L.harness_span_groups.argtypes = [P, U64, P, U64, U32, U32, P]
         L.harness_span_declined.restype = None
         L.harness_span_declined.argtypes = [P]
-        L.harness_span_ext.restype = None
-        L.harness_span_ext.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
 
@@ -95,10 +93,10 @@ def sparse_decode(codes, lens, flags=0, ip_offset=0):
     return dd[:n], hd[:n]
 
 
-def span_groups(data, offsets, flags=0, ip_offset=0, declined=None, ext=True):
-    """k_parse_span's fast path + generic section (slots, bucketed items,
-    the extension windows of the non-record outputs when `ext`) emulated
-    group by group over a packed batch. `declined` (uint8[count], optional) receives 1 for every
+def span_groups(data, offsets, flags=0, ip_offset=0, declined=None):
+    """k_parse_span's fast path (with the lanes' slots for IPv4 options) +
+    generic section (slots, bucketed items) emulated group by group over a
+    packed batch. `declined` (uint8[count], optional) receives 1 for every
     frame the fast path declined to the generic core."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     offs = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -108,7 +106,6 @@ def span_groups(data, offsets, flags=0, ip_offset=0, declined=None, ext=True):
         assert declined.dtype == np.uint8 and declined.flags.c_contiguous and len(declined) >= count
         declined[:count] = 0
     lib().harness_span_declined(ctypes.c_void_p(declined.ctypes.data if declined is not None else None))
-    lib().harness_span_ext(1 if ext else 0)
     try:
         rc = lib().harness_span_groups(data.ctypes.data, data.nbytes, offs.ctypes.data, count, flags, ip_offset,
                                        recs.ctypes.data)
