@@ -388,7 +388,7 @@ def large_line(eng, args, first, out_kind, stream, device, rank, world):
     """The UDP64 headline at 52M frames (3.25 GiB, 13x the 256-MiB MALL): a
     batch no cache can hold between launches, so its rate is HBM's."""
     from nex_amd import abi
-    batch = eng.gen_batch(abi.WL_UDP64, LARGE_FRAMES, first_index=first * (LARGE_FRAMES // (16 << 20)))
+    batch = eng.gen_batch(abi.WL_UDP64, LARGE_FRAMES, first_index=rank * LARGE_FRAMES)  # this rank's index range
     return parse_object(eng, args, batch, out_kind, stream, device, rank, world,
                         f"configs[1] at {LARGE_FRAMES} x 64-B Eth/IPv4/UDP frames per GPU (3.25 GiB, 13x the "
                         "256-MiB Infinity Cache: no cross-launch cache reuse possible); " + OUT_NOTE[args.out],
