@@ -28,6 +28,7 @@ uint32_t tile_order_for(const ParseArgs& a) {
     static const int forced = [] {
         const char* e = getenv("NEXG_TILE_ORDER");
         if (!e) return -1;
+        if (strncmp(e, "xcd", 3) == 0 && e[3]) return atoi(e + 3);  // xcdK: XCD-local runs of K tiles (A/B)
         return strcmp(e, "xcd") == 0 ? 1 : (strcmp(e, "linear") == 0 ? 0 : -1);
     }();
     if (forced >= 0) return (uint32_t)forced;

@@ -146,6 +146,11 @@ __device__ __forceinline__ void stage_record(uint8_t* slot, const nexg_record& r
 __device__ __forceinline__ uint64_t tile_index(uint32_t order) {
     const uint32_t b = blockIdx.x, q = gridDim.x >> 3;
     if (!order || b >= (q << 3)) return b;
+    if (order >= 2u) {  // (A/B) XCD-local runs of K = order tiles, round-robin over the XCDs
+        const uint32_t K = order, w = b >> 3, x = b & 7u;  // x: the XCD this workgroup lands on
+        if (q % K) return b;  // a bijection only when the runs tile the grid
+        return ((uint64_t)(w / K) * 8u + x) * K + w % K;
+    }
     return (uint64_t)(b & 7u) * q + (b >> 3);
 }
 

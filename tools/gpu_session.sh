@@ -37,6 +37,7 @@ for s in ${STEPS:-tests}; do
     benchimix) step bench_imix 400 python bench.py --workload imix --steps 20 --warmup 3 --cpu-seconds 5 ;;
     pmc) step pmc 900 bash tools/pmc.sh ;;
     sqkinds) step sqkinds 900 bash tools/sq_kinds.sh ;;
+    tileorder) step tileorder 900 bash tools/tile_order_ab.sh ;;
     abser) step ab_ser 300 python -u tools/bench_ser_ab.py --libs ${LIBS} --shape ${SHAPE:-tuples} --rounds 4 ;;
     # in-process A/B of library variants under abvar/ (LIBS=a,b,...): IMIX with an output check, then the mixes
     abspan) step ab_imix 600 python -u tools/bench_parse_ab.py --libs ${LIBS} --workloads imix,udp64 --out grouped --check --rounds 4
