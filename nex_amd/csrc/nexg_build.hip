@@ -49,6 +49,7 @@ struct BuildArgs {
     uint8_t* out;
     uint32_t out_stride;
     const nexg_udp4_tuple* tuples;  // AOS builds: one 16-B tuple per frame
+    uint32_t tile_order;            // tile_index order (nexg_internal.hpp)
 };
 
 // Frame header given as NH (odd) little-endian halfwords of its bytes, written
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     constexpr bool STAGED = MAXS != 0;
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
     const nexg_udp4_build& p = a.p;
-    const uint64_t first = (uint64_t)blockIdx.x * kBuildTile;
+    const uint64_t first = tile_index(a.tile_order) * kBuildTile;
     const uint64_t left = p.count - first;
     const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
     const uint32_t tid = threadIdx.x;
@@ -785,7 +786,7 @@ __global__ void k_gen_udp4_params(uint64_t seed, uint64_t first, uint64_t count,
 hipError_t launch_build_udp4_tuples(const nexg_udp4_build& p, const nexg_udp4_tuple* tuples, uint8_t* out,
                                     uint32_t out_stride, hipStream_t s) {
     if (p.count == 0) return hipSuccess;
-    BuildArgs a{p, out, out_stride, tuples};
+    BuildArgs a{p, out, out_stride, tuples, build_tile_order()};
     const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
     if (staged && out_stride <= 64u)
@@ -801,7 +802,7 @@ hipError_t launch_build_udp4_tuples(const nexg_udp4_build& p, const nexg_udp4_tu
 hipError_t launch_build_udp4(const nexg_udp4_build& p, uint8_t* out, uint32_t out_stride,
                              hipStream_t s) {
     if (p.count == 0) return hipSuccess;
-    BuildArgs a{p, out, out_stride, nullptr};
+    BuildArgs a{p, out, out_stride, nullptr, build_tile_order()};
     const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
     const bool full = p.src_ip && p.src_port && p.dst_port && p.ip_id && !p.src_mac && !p.dst_mac;

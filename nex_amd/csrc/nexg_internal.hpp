@@ -42,7 +42,34 @@ inline bool parse_needs_tail(ParseVariant v, int out_kind) {
            (out_kind == NEXG_OUT_VERDICT || out_kind == NEXG_OUT_SPARSE || out_kind == NEXG_OUT_GROUPED);
 }
 uint32_t tile_order_for(const ParseArgs& a);
+uint32_t build_tile_order();
 ParseVariant choose_parse_variant(const ParseArgs& a);
+
+// Tile handled by this workgroup. Workgroups are dispatched to the 8 XCDs
+// round-robin (blockIdx % 8).
+//  order 0: grid order, tile = b.
+//  order 1: each XCD one contiguous eighth of the batch, tile = (b % 8) * (nb / 8) + b / 8.
+//  order K >= 2: XCD-local runs of K consecutive tiles, the runs dealt to the
+//    XCDs round-robin — XCD x's i-th workgroup takes tile (i / K * 8 + x) * K + i % K.
+//    At any moment each XCD streams its own K-tile run of the batch instead of
+//    every eighth tile (profiles/r04/tile_order/: K = 16 over 16-KiB tiles is
+//    5-7 % faster than grid order at 1 and 3.25 GiB; K = 4 is 5 % slower).
+// Workgroups past the last whole group of 8 (order 1) or 8K (order K) keep grid
+// order, so the map is a bijection on [0, nb) for every grid size.
+__host__ __device__ __forceinline__ uint64_t tile_of(uint32_t b, uint32_t nb, uint32_t order) {
+    if (!order) return b;
+    if (order == 1u) {
+        const uint32_t q = nb >> 3;
+        return b >= (q << 3) ? b : (uint64_t)(b & 7u) * q + (b >> 3);
+    }
+    const uint32_t K = order;
+    if (K > (nb >> 3)) return b;  // no whole group (and 8K cannot overflow below)
+    const uint32_t whole = nb / (8u * K) * (8u * K);
+    if (b >= whole) return b;
+    const uint32_t i = b >> 3, x = b & 7u;
+    return ((uint64_t)(i / K) * 8u + x) * K + i % K;
+}
+__device__ __forceinline__ uint64_t tile_index(uint32_t order) { return tile_of(blockIdx.x, gridDim.x, order); }
 
 hipError_t launch_checksum(const ParseArgs& a, uint32_t skipword, uint16_t* out, hipStream_t s);
 

@@ -19,21 +19,31 @@
 
 namespace nexg {
 
-// Tile order of the fixed-stride tile kernels: NEXG_TILE_ORDER=linear|xcd
-// overrides (measurement); otherwise XCD-contiguous from 3 GiB up. Measured
-// (profiles/r01_staging/tile_order.txt): grid order is 3 % faster at 1 GiB,
-// equal at 2 GiB; XCD order 6 % faster at 4 GiB and 10 % at 16 GiB. The span
-// kernel (packed batches) keeps grid order: XCD order was 3 % slower at 6 GB.
+// tile_index order named by an env variable (measurement overrides):
+// linear = 0, xcd = 1 (contiguous eighths), xcdK = XCD-local runs of K tiles;
+// -1 when unset or unrecognised.
+static int order_from_env(const char* name) {
+    const char* e = getenv(name);
+    if (!e) return -1;
+    if (strncmp(e, "xcd", 3) == 0 && e[3]) return atoi(e + 3);
+    return strcmp(e, "xcd") == 0 ? 1 : (strcmp(e, "linear") == 0 ? 0 : -1);
+}
+
+// Tile order of the parse kernels; NEXG_TILE_ORDER overrides. Fixed-stride
+// tiles (16 KiB at 64 B) take XCD-local runs of 16 tiles at every size
+// (profiles/r04/tile_order/: 0.921-0.924 of 8 TB/s at 1 and 3.25 GiB, grid
+// order 0.86-0.88, contiguous eighths 0.887-0.894, runs of 4 0.82-0.83). The
+// span kernel (packed batches, ~90 KB per IMIX tile) keeps grid order.
 uint32_t tile_order_for(const ParseArgs& a) {
-    static const int forced = [] {
-        const char* e = getenv("NEXG_TILE_ORDER");
-        if (!e) return -1;
-        if (strncmp(e, "xcd", 3) == 0 && e[3]) return atoi(e + 3);  // xcdK: XCD-local runs of K tiles (A/B)
-        return strcmp(e, "xcd") == 0 ? 1 : (strcmp(e, "linear") == 0 ? 0 : -1);
-    }();
+    static const int forced = order_from_env("NEXG_TILE_ORDER");
     if (forced >= 0) return (uint32_t)forced;
-    constexpr uint64_t kXcdOrderBytes = 3ull << 30;
-    return !a.offsets && a.count * (uint64_t)a.stride >= kXcdOrderBytes ? 1u : 0u;
+    return a.offsets ? 0u : 16u;
+}
+
+// Tile order of the udp_ping builder (k_build_udp4); NEXG_BUILD_ORDER overrides.
+uint32_t build_tile_order() {
+    static const int forced = order_from_env("NEXG_BUILD_ORDER");
+    return forced >= 0 ? (uint32_t)forced : 0u;
 }
 
 ParseVariant choose_parse_variant(const ParseArgs& a) {
@@ -241,18 +251,20 @@ hipError_t launch_decode_options(const ParseArgs& a, const nexg_record* recs, ne
 
 // calibration stream (include/nexg.h nexg_probe_stream): the parse kernels'
 // load shape with either the 8-B-per-64-B descriptor store stream or none
+// (tiles in the parse kernels' fixed-stride tile order)
 template <bool W8>
-__global__ __launch_bounds__(256) void k_probe_stream(const uint8_t* data, void* out) {
+__global__ __launch_bounds__(256) void k_probe_stream(const uint8_t* data, void* out, uint32_t order) {
     __shared__ uint32_t s_x[4];
     const uint32_t t = threadIdx.x;
-    const uint8_t* T = data + (uint64_t)blockIdx.x * 16384u;
+    const uint64_t tile = tile_index(order);
+    const uint8_t* T = data + tile * 16384u;
     uint4 v[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) v[k] = load16<true>(T + 16u * (t + 256u * k));
     uint32_t x = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
-    const uint64_t i = (uint64_t)blockIdx.x * kTile + t;
+    const uint64_t i = tile * kTile + t;
     if (W8) {
         reinterpret_cast<uint2*>(out)[i] = make_uint2(x, (uint32_t)i);
     } else {
@@ -260,27 +272,32 @@ __global__ __launch_bounds__(256) void k_probe_stream(const uint8_t* data, void*
         for (int d = 32; d >= 1; d >>= 1) x ^= __shfl_xor(x, d, 64);
         if ((t & 63u) == 0) s_x[t >> 6] = x;
         __syncthreads();
-        if (t == 0) reinterpret_cast<uint32_t*>(out)[blockIdx.x] = s_x[0] ^ s_x[1] ^ s_x[2] ^ s_x[3];
+        if (t == 0) reinterpret_cast<uint32_t*>(out)[tile] = s_x[0] ^ s_x[1] ^ s_x[2] ^ s_x[3];
     }
 }
 
 // write-only calibration stream: the builders' copy-out shape (16-B
-// non-temporal stores, 16 KiB per 256-lane workgroup); out[tile][c] = {tile, c, 0, 0}
-__global__ __launch_bounds__(256) void k_probe_write(uint8_t* out) {
+// non-temporal stores, 16 KiB per 256-lane workgroup, the builder's tile
+// order); out[tile][c] = {tile, c, 0, 0}
+__global__ __launch_bounds__(256) void k_probe_write(uint8_t* out, uint32_t order) {
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    v4u* T = reinterpret_cast<v4u*>(out + (uint64_t)blockIdx.x * 16384u);
+    const uint64_t tile = tile_index(order);
+    v4u* T = reinterpret_cast<v4u*>(out + tile * 16384u);
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
         const uint32_t c = threadIdx.x + 256u * k;
-        __builtin_nontemporal_store(v4u{blockIdx.x, c, 0u, 0u}, T + c);
+        __builtin_nontemporal_store(v4u{(uint32_t)tile, c, 0u, 0u}, T + c);
     }
 }
 
 hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, uint32_t mode, void* out, hipStream_t s) {
     if (tiles == 0) return hipSuccess;
-    if (mode == 64) hipLaunchKernelGGL(k_probe_write, dim3((uint32_t)tiles), dim3(kTile), 0, s, static_cast<uint8_t*>(out));
-    else if (mode == 8) hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out);
-    else hipLaunchKernelGGL(k_probe_stream<false>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out);
+    ParseArgs fixed{};
+    fixed.stride = 64;
+    const uint32_t ro = tile_order_for(fixed), wo = build_tile_order();
+    if (mode == 64) hipLaunchKernelGGL(k_probe_write, dim3((uint32_t)tiles), dim3(kTile), 0, s, static_cast<uint8_t*>(out), wo);
+    else if (mode == 8) hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out, ro);
+    else hipLaunchKernelGGL(k_probe_stream<false>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out, ro);
     return hipGetLastError();
 }
 

@@ -139,21 +139,6 @@ __device__ __forceinline__ void stage_record(uint8_t* slot, const nexg_record& r
     for (int k = 0; k < 4; k++) reinterpret_cast<uint4*>(slot)[k] = v[k];
 }
 
-// Tile handled by this workgroup. order 1: workgroups are dispatched to the 8
-// XCDs round-robin (blockIdx % 8), so tile = (b % 8) * (nb / 8) + b / 8 gives
-// each XCD one contiguous eighth of the batch (its own pages and L2 lines);
-// the nb % 8 tail keeps grid order. A bijection on [0, nb) either way.
-__device__ __forceinline__ uint64_t tile_index(uint32_t order) {
-    const uint32_t b = blockIdx.x, q = gridDim.x >> 3;
-    if (!order || b >= (q << 3)) return b;
-    if (order >= 2u) {  // (A/B) XCD-local runs of K = order tiles, round-robin over the XCDs
-        const uint32_t K = order, w = b >> 3, x = b & 7u;  // x: the XCD this workgroup lands on
-        if (q % K) return b;  // a bijection only when the runs tile the grid
-        return ((uint64_t)(w / K) * 8u + x) * K + w % K;
-    }
-    return (uint64_t)(b & 7u) * q + (b >> 3);
-}
-
 // MODE 0: fixed stride tile staging (STRIDE = 0 -> runtime stride).
 // MODE 1: per-lane window staging.
 template <int MODE, int OUT, int STRIDE, int WIN, bool FAST = true, bool NT = false>
@@ -587,7 +572,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     __shared__ uint64_t s_span[2];
     __shared__ uint32_t s_hist[2 * kBuckets + 1];  // generic-pass bucket counts, bases, total
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    const uint64_t f0 = (uint64_t)blockIdx.x * kTile;  // grid order: XCD order measured slower here
+    const uint64_t f0 = tile_index(a.tile_order) * kTile;
     const uint64_t idx = f0 + t;
     const uint32_t nf = a.count - f0 < kTile ? (uint32_t)(a.count - f0) : kTile;
     const uint64_t base = reinterpret_cast<uint64_t>(a.data);

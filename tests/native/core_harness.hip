@@ -10,6 +10,12 @@ static unsigned long long g_span_probe[2];
 #define NEXG_SPAN_PROBE(k, c) (g_span_probe[k] += (c) ? 1u : 0u)
 #include "../../nex_amd/csrc/parse_kernels.hpp"
 
+// tile_of (nexg_internal.hpp, the kernels' workgroup -> tile map) for every
+// workgroup of an nb-workgroup grid
+extern "C" void harness_tile_map(uint32_t nb, uint32_t order, uint64_t* out) {
+    for (uint32_t b = 0; b < nb; b++) out[b] = nexg::tile_of(b, nb, order);
+}
+
 extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uint64_t* offsets,
                              const uint32_t* lengths, uint32_t stride, uint64_t count,
                              uint32_t flags, uint32_t ip_offset, uint32_t window,

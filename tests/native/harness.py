@@ -26,6 +26,8 @@ def lib():
         L.harness_sparse_decode.argtypes = [P, P, U64, U32, U32, P, P]
         L.harness_slice.restype = ctypes.c_int
         L.harness_slice.argtypes = [P, U64, P, P, U32, U64, U32, U32, U32, P]
+        L.harness_tile_map.restype = None
+        L.harness_tile_map.argtypes = [U32, U32, P]
         L.harness_span_groups.restype = ctypes.c_int
         L.harness_span_groups.argtypes = [P, U64, P, U64, U32, U32, P]
         L.harness_span_declined.restype = None
@@ -113,3 +115,10 @@ def span_groups(data, offsets, flags=0, ip_offset=0, declined=None):
         lib().harness_span_declined(ctypes.c_void_p(None))
     assert rc == 0, f"harness_span_groups: {rc}"
     return recs
+
+
+def tile_map(nb, order):
+    """tile_of(b, nb, order) for b in [0, nb): the kernels' workgroup -> tile map."""
+    out = np.zeros(nb, np.uint64)
+    lib().harness_tile_map(nb, order, out.ctypes.data)
+    return out

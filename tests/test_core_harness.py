@@ -278,3 +278,19 @@ def test_tcp_option_walk_span_groups(oracle):
             assert dec.sum() > 0  # multi-option lists go to the generic walk
             q13 = ((want["flags"] & abi.L_TRANSPORT) != 0) & ((want["flags"] & abi.L_TCP) == 0)
             assert q13.sum() > 20
+
+
+@pytest.mark.parametrize("order", [0, 1, 2, 3, 8, 16, 64, 1 << 20, 0xFFFFFFFF])
+def test_tile_map_is_a_permutation(order):
+    """tile_of (nexg_internal.hpp), the workgroup -> tile map every tile
+    kernel uses: a permutation of [0, nb) for every grid size, ragged tails
+    included; order 16 gives each XCD (workgroup % 8) runs of 16 consecutive
+    tiles."""
+    for nb in list(range(0, 300)) + [1023, 1024, 1025, 4096 + 127, 65536, 212993]:
+        m = harness.tile_map(nb, order)
+        assert np.array_equal(np.sort(m), np.arange(nb, dtype=np.uint64)), (nb, order)
+    if order == 16:
+        m = harness.tile_map(65536, 16).reshape(-1, 8)  # row i: the i-th workgroup of each XCD
+        for x in range(8):
+            run = m[:16, x]
+            assert np.array_equal(run, np.arange(x * 16, x * 16 + 16))

@@ -410,29 +410,31 @@ def test_build_udp4_default_fields(engine, oracle):
             assert bytes(data[i]) == want, ("probe", m, i)
 
 
-def test_probe_stream(engine):
-    """nexg_probe_stream (calibration): both output shapes against numpy."""
+@pytest.mark.parametrize("tiles", [3, 8 * 16 * 2 + 5])
+def test_probe_stream(engine, tiles):
+    """nexg_probe_stream (calibration): both output shapes against numpy, at
+    3 tiles (grid order) and at 261 (runs of 16 tiles per XCD + a tail)."""
     import torch
     rng = np.random.default_rng(5)
-    host = rng.integers(0, 256, 3 * 16384, dtype=np.uint8)
+    host = rng.integers(0, 256, tiles * 16384, dtype=np.uint8)
     data = torch.from_numpy(host).cuda()
-    w = host.view("<u4").reshape(3, 4, 256, 4)  # tile, k, lane, dword
+    w = host.view("<u4").reshape(tiles, 4, 256, 4)  # tile, k, lane, dword
     lane_x = np.bitwise_xor.reduce(np.bitwise_xor.reduce(w, axis=3), axis=1)  # tile, lane
     o8 = engine.probe_stream(data, True)
     torch.cuda.synchronize()
     got = o8.cpu().numpy().view("<u4").reshape(-1, 2)
-    assert (got[:, 0] == lane_x.reshape(-1)).all() and (got[:, 1] == np.arange(768)).all()
+    assert (got[:, 0] == lane_x.reshape(-1)).all() and (got[:, 1] == np.arange(tiles * 256)).all()
     o0 = engine.probe_stream(data, False)
     torch.cuda.synchronize()
-    assert (o0.cpu().numpy().view("<u4")[:3] == np.bitwise_xor.reduce(lane_x, axis=1)).all()
-    ow = torch.full((3 * 16384 + 16,), 0xAB, dtype=torch.uint8, device="cuda")
+    assert (o0.cpu().numpy().view("<u4")[:tiles] == np.bitwise_xor.reduce(lane_x, axis=1)).all()
+    ow = torch.full((tiles * 16384 + 16,), 0xAB, dtype=torch.uint8, device="cuda")
     engine.probe_write(ow)
     torch.cuda.synchronize()
     got = ow.cpu().numpy()
-    want = np.zeros((3, 1024, 4), np.uint32)
-    want[:, :, 0] = np.arange(3)[:, None]
+    want = np.zeros((tiles, 1024, 4), np.uint32)
+    want[:, :, 0] = np.arange(tiles)[:, None]
     want[:, :, 1] = np.arange(1024)[None, :]
-    assert (got[: 3 * 16384].view("<u4") == want.reshape(-1)).all() and (got[3 * 16384:] == 0xAB).all()
+    assert (got[: tiles * 16384].view("<u4") == want.reshape(-1)).all() and (got[tiles * 16384:] == 0xAB).all()
 
 
 @pytest.mark.parametrize("workload", [abi.WL_UDP64, abi.WL_IMIX])

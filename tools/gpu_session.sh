@@ -38,6 +38,9 @@ for s in ${STEPS:-tests}; do
     pmc) step pmc 900 bash tools/pmc.sh ;;
     sqkinds) step sqkinds 900 bash tools/sq_kinds.sh ;;
     tileorder) step tileorder 900 bash tools/tile_order_ab.sh ;;
+    tileorder2) step tileorder2 1000 bash tools/tile_order_ab2.sh ;;
+    tileorder3) step tileorder3 900 bash tools/tile_order_ab3.sh ;;
+    ordertests) step ordertests 600 python -u -m pytest tests/test_gpu_tile_order.py -x -v --timeout 300 --timeout-method thread ;;
     abser) step ab_ser 300 python -u tools/bench_ser_ab.py --libs ${LIBS} --shape ${SHAPE:-tuples} --rounds 4 ;;
     # in-process A/B of library variants under abvar/ (LIBS=a,b,...): IMIX with an output check, then the mixes
     abspan) step ab_imix 600 python -u tools/bench_parse_ab.py --libs ${LIBS} --workloads imix,udp64 --out grouped --check --rounds 4

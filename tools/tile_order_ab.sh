@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/tileorder
 for rnd in 1 2; do
-  if [ $rnd = 1 ]; then L="linear xcd xcd4 xcd16 xcd64"; else L="xcd64 xcd16 xcd4 xcd linear"; fi
+  if [ $rnd = 1 ]; then L="${ORDERS:-linear xcd8 xcd16 xcd32}"; else L=$(echo ${ORDERS:-linear xcd8 xcd16 xcd32} | tr " " "\n" | tac | tr "\n" " "); fi
   for o in $L; do
     for f in 16777216 54525952; do
       NEXG_TILE_ORDER=$o timeout -k 10 120 python bench.py --frames $f --steps 50 --warmup 25 --no-cpu-baseline --no-imix > gpurun_out/tileorder/${o}_${f}_$rnd.json 2>/dev/null
