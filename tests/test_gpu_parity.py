@@ -103,7 +103,7 @@ def test_generators_match_oracle(engine, oracle):
                                             (abi.WL_UDP64, 52 << 20)])
 def test_full_size_sampled(engine, oracle, workload, count):
     """BASELINE.json full sizes: sample 65536 frames bit-exact + properties.
-    52M x 64 B (3.25 GiB) takes the XCD-contiguous tile order."""
+    52M x 64 B is 3.25 GiB."""
     import torch
     b = engine.gen_batch(workload, count)
     desc = engine.parse(b, out_kind=abi.OUT_DESC)
