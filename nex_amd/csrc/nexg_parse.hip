@@ -75,12 +75,9 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
     const uint64_t blocks = (a.count + kTile - 1) / kTile;
     dim3 grid((uint32_t)blocks), block(kTile);
     switch (v) {
-        case ParseVariant::TileStride64: {
-            // (A/B) NEXG_TILE_LDS_PAD bytes of dynamic LDS cap the workgroups per CU
-            static const uint32_t pad = [] { const char* e = getenv("NEXG_TILE_LDS_PAD"); return e ? (uint32_t)atoi(e) : 0u; }();
-            hipLaunchKernelGGL((k_parse<0, OUT, 64, 64, true, true>), grid, block, pad, s, a);
+        case ParseVariant::TileStride64:
+            hipLaunchKernelGGL((k_parse<0, OUT, 64, 64, true, true>), grid, block, 0, s, a);
             break;
-        }
         case ParseVariant::TileStride:
             hipLaunchKernelGGL((k_parse<0, OUT, 0, 128>), grid, block, 0, s, a);
             break;
