@@ -171,7 +171,10 @@ def write_ceiling(eng, out, args, stream, device):
     nbytes = out.numel() // 16384 * 16384
     _, ks = timed(lambda: eng.probe_write(out, stream=stream), args.steps, args.warmup, stream, device)
     return {"write_only_gbs": round(nbytes / ks / 1e9, 1),
-            "source": "nexg_probe_stream(out_per_64=64) over the build output buffer, same steps/warmup"}
+            "source": "nexg_probe_stream(out_per_64=64) over the build output buffer, same steps/warmup: "
+                      "16 KiB of 16-B non-temporal stores per workgroup at the builder's tile order and 5 "
+                      "workgroups per CU; a reference stream, not a bound (the builder's 10.75-KiB tiles "
+                      "run faster, DESIGN.md §6 round 4)"}
 
 
 def ser_line(eng, args, F, first, stream, device, rank, world):
@@ -264,7 +267,11 @@ def stream_ceilings(eng, batch, args, stream, device):
         _, ks = timed(lambda: eng.probe_stream(batch.data, w8, out=out, stream=stream),
                       args.steps, args.warmup, stream, device)
         r[key] = round(nbytes / ks / 1e9, 1)
-    r["source"] = "nexg_probe_stream on this batch, same steps/warmup, HIP events on the launch stream"
+    r["source"] = ("nexg_probe_stream on this batch, same steps/warmup, HIP events on the launch stream: "
+                   "a bare 16-B non-temporal read stream in the parse kernel's tile order at 8 workgroups per "
+                   "CU; a reference stream, not a bound (the parse kernel at 6 per CU runs faster; the best "
+                   "bare read stream found, 3 per CU, is 0.89 / 0.93 of 8 TB/s at 1 / 3.25 GiB: "
+                   "profiles/r04/occupancy/)")
     if args.out in ("sparse", "desc", "grouped"):  # the same parse with the other output kinds
         from nex_amd import abi
         for key, kind in (("desc_output", abi.OUT_DESC), ("flags_output", abi.OUT_FLAGS),

@@ -12,6 +12,8 @@
 // k_gen_*: SURVEY.md Appendix C workloads. splitmix64 is counter based
 // (draw m of frame i is mix(seed ^ i*phi + (m+1)*phi)), so a wave fills one
 // frame cooperatively: lane l produces 8-byte words l, l+64, ...
+#include <stdlib.h>
+
 #include "frame_core.hpp"
 #include "nexg_internal.hpp"
 
@@ -51,6 +53,22 @@ struct BuildArgs {
     const nexg_udp4_tuple* tuples;  // AOS builds: one 16-B tuple per frame
     uint32_t tile_order;            // tile_index order (nexg_internal.hpp)
 };
+
+// Dynamic LDS beside k_build_udp4<64>'s 16-KiB static tile so that 5
+// workgroups fit a CU's 160 KiB instead of 8 (at most 32 KiB each): fewer
+// concurrent write streams per CU. 16M udp_ping frames in contiguous eighths
+// (profiles/r04/occupancy/builder_occupancy_ab.log): probe batch 0.887-0.891
+// of 8 TB/s written against 0.743 at 8 per CU, full tuples 0.717-0.719 against
+// 0.681; 4 per CU the same, 6 and 7 in between. NEXG_BUILD_LDS_PAD overrides
+// (measurement).
+constexpr uint32_t kBuildCapPad = 160u * 1024u / 5u - (kBuildTile * 64u + 16u) - 256u;
+uint32_t build_lds_pad() {
+    static const uint32_t pad = [] {
+        const char* e = getenv("NEXG_BUILD_LDS_PAD");
+        return e ? (uint32_t)atoi(e) : kBuildCapPad;
+    }();
+    return pad;
+}
 
 // Frame header given as NH (odd) little-endian halfwords of its bytes, written
 // to LDS at an even offset d0: (NH-1)/2 dword writes + 1 halfword write, the
@@ -789,8 +807,9 @@ hipError_t launch_build_udp4_tuples(const nexg_udp4_build& p, const nexg_udp4_tu
     BuildArgs a{p, out, out_stride, tuples, build_tile_order()};
     const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
+    const uint32_t pad = build_lds_pad();
     if (staged && out_stride <= 64u)
-        hipLaunchKernelGGL((k_build_udp4<64, false, false, true>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+        hipLaunchKernelGGL((k_build_udp4<64, false, false, true>), dim3((uint32_t)blocks), dim3(kBuildTile), pad, s, a);
     else if (staged)
         hipLaunchKernelGGL((k_build_udp4<kBuildMaxStride, false, false, true>), dim3((uint32_t)blocks), dim3(kBuildTile),
                            0, s, a);
@@ -807,11 +826,12 @@ hipError_t launch_build_udp4(const nexg_udp4_build& p, uint8_t* out, uint32_t ou
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
     const bool full = p.src_ip && p.src_port && p.dst_port && p.ip_id && !p.src_mac && !p.dst_mac;
     const bool probe = !p.src_ip && !p.src_port && !p.dst_port && !p.ip_id && !p.src_mac && !p.dst_mac;
-    // a 16-KiB tile for the udp_ping shapes keeps ~10 workgroups per CU
+    // the udp_ping shapes: a 16-KiB tile + build_lds_pad() -> 5 workgroups per CU
+    const uint32_t pad = build_lds_pad();
     if (staged && out_stride <= 64u && full)
-        hipLaunchKernelGGL((k_build_udp4<64, true>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+        hipLaunchKernelGGL((k_build_udp4<64, true>), dim3((uint32_t)blocks), dim3(kBuildTile), pad, s, a);
     else if (staged && out_stride <= 64u && probe)
-        hipLaunchKernelGGL((k_build_udp4<64, false, true>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+        hipLaunchKernelGGL((k_build_udp4<64, false, true>), dim3((uint32_t)blocks), dim3(kBuildTile), pad, s, a);
     else if (staged && out_stride <= 64u)
         hipLaunchKernelGGL(k_build_udp4<64>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     else if (staged)

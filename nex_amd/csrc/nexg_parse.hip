@@ -282,10 +282,12 @@ __global__ __launch_bounds__(256) void k_probe_stream(const uint8_t* data, void*
 
 // write-only calibration stream: the builders' copy-out shape (16-B
 // non-temporal stores, 16 KiB per 256-lane workgroup, the builder's tile
-// order); out[tile][c] = {tile, c, 0, 0}
+// order and workgroups per CU); out[tile][c] = {tile, c, 0, 0}
 __global__ __launch_bounds__(256) void k_probe_write(uint8_t* out, uint32_t order) {
+    extern __shared__ uint32_t s_cap[];  // dynamic LDS: caps workgroups per CU only
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     const uint64_t tile = tile_index(order);
+    if (order == 0xFFFFFFFFu) s_cap[threadIdx.x] = 0u;
     v4u* T = reinterpret_cast<v4u*>(out + tile * 16384u);
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
@@ -299,7 +301,9 @@ hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, uint32_t mod
     ParseArgs fixed{};
     fixed.stride = 64;
     const uint32_t ro = tile_order_for(fixed), wo = build_tile_order();
-    if (mode == 64) hipLaunchKernelGGL(k_probe_write, dim3((uint32_t)tiles), dim3(kTile), 0, s, static_cast<uint8_t*>(out), wo);
+    if (mode == 64)  // the builder's LDS footprint: its 16-KiB tile + build_lds_pad()
+        hipLaunchKernelGGL(k_probe_write, dim3((uint32_t)tiles), dim3(kTile), 16400u + build_lds_pad(), s,
+                           static_cast<uint8_t*>(out), wo);
     else if (mode == 8) hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out, ro);
     else hipLaunchKernelGGL(k_probe_stream<false>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out, ro);
     return hipGetLastError();

@@ -41,6 +41,7 @@ for s in ${STEPS:-tests}; do
     tileorder2) step tileorder2 1000 bash tools/tile_order_ab2.sh ;;
     orderbench) step orderbench 300 ./tools/orderbench
                 step orderbench52 300 ./tools/orderbench 54525952 ;;
+    buildocc) step buildocc 900 bash tools/build_occ_ab.sh ;;
     sizesweep) step sizesweep 900 bash tools/size_sweep.sh ;;
     tileorder3) step tileorder3 900 bash tools/tile_order_ab3.sh ;;
     ordertests) step ordertests 600 python -u -m pytest tests/test_gpu_tile_order.py -x -v --timeout 300 --timeout-method thread ;;
