@@ -132,19 +132,36 @@ NEXG_HD uint4 load16a4(const void* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Device loads of HBM bytes go through address-space-1 pointers: a
+// global_load is counted on vmcnt alone, while a flat load (what a generic
+// pointer becomes when the compiler cannot prove it global, e.g. one built
+// from an integer address) also counts on lgkmcnt, so the next s_waitcnt
+// lgkmcnt(0) for an LDS access, a shuffle or a barrier waits for it too.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define NEXG_GLOBAL(T, p) reinterpret_cast<const __attribute__((address_space(1))) T*>(reinterpret_cast<uintptr_t>(p))
+#else
+#define NEXG_GLOBAL(T, p) reinterpret_cast<const T*>(p)
+#endif
+
 // 16-B global load; NT = non-temporal (streamed once, do not keep in cache)
 template <bool NT = false>
 NEXG_HD uint4 load16(const void* p) {
-    u32x4 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p))
-                 : *reinterpret_cast<const u32x4*>(p);
+    u32x4 v = NT ? __builtin_nontemporal_load(NEXG_GLOBAL(u32x4, p)) : *NEXG_GLOBAL(u32x4, p);
     return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// 16-B global load from an absolute address (k_parse_span's sub-tile
+// stream: as a flat load its prefetch was waited for at the next barrier)
+template <bool NT = false>
+NEXG_HD uint4 load16g(uint64_t addr) {
+    return load16<NT>(reinterpret_cast<const void*>(addr));
 }
 
 // little-endian halfword sum of global bytes [A, B) (absolute addresses)
 NEXG_HD uint64_t global_le_sum(uint64_t A, uint64_t B) {
     uint64_t acc = 0;
     for (uint64_t d = A & ~15ull; d < B; d += 16) {
-        const uint4 v = *reinterpret_cast<const uint4*>(d);
+        const uint4 v = load16(reinterpret_cast<const void*>(d));
         uint32_t s = 0;
         if (d >= A && d + 16 <= B) {
             s = halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);

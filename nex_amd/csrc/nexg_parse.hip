@@ -343,3 +343,13 @@ hipError_t launch_checksum(const ParseArgs& a, uint32_t skipword, uint16_t* out,
 }
 
 }  // namespace nexg
+
+#ifdef NEXG_SPAN_TIMING
+// (measurement builds only) copies k_parse_span's per-workgroup timestamps
+// [entry, after the span check, after the sub-tile loop, after the fast path,
+// after the generic section, exit, CU id, -] to the host (s_memtime counts per XCD: compare stamps of one workgroup only)
+extern "C" int nexg_debug_span_times(void* host, uint64_t workgroups) {
+    if (workgroups > nexg::kSpanTimingMax) workgroups = nexg::kSpanTimingMax;
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(nexg::g_span_times), workgroups * 64u, 0, hipMemcpyDeviceToHost);
+}
+#endif

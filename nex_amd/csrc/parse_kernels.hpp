@@ -554,6 +554,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     return v;
 }
 
+// (measurement builds only) per-workgroup phase timestamps of k_parse_span:
+// -DNEXG_SPAN_TIMING, read back by nexg_debug_span_times (nexg_parse.hip),
+// summarised by tools/span_timing.py
+#ifdef NEXG_SPAN_TIMING
+constexpr uint32_t kSpanTimingMax = 1u << 17;
+__device__ uint64_t g_span_times[kSpanTimingMax * 8];
+#define NEXG_SPAN_STAMP(k) \
+    do { if (t == 0 && blockIdx.x < kSpanTimingMax) g_span_times[blockIdx.x * 8u + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define NEXG_SPAN_STAMP(k)
+#endif
+
 // NB = 2: sub-tile k stages into buffer k&1, so the barrier that publishes
 // sub-tile k also retires every lookup into sub-tile k-2's buffer (3 barriers
 // per sub-tile, ~42 KB LDS); NB = 1 (the library's): one buffer and a 4th
@@ -572,6 +584,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     __shared__ uint64_t s_span[2];
     __shared__ uint32_t s_hist[2 * kBuckets + 1];  // generic-pass bucket counts, bases, total
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    NEXG_SPAN_STAMP(0);
+#ifdef NEXG_SPAN_TIMING
+    if (t == 0 && blockIdx.x < kSpanTimingMax) g_span_times[blockIdx.x * 8u + 6] = __smid();
+#endif
     const uint64_t f0 = tile_index(a.tile_order) * kTile;
     const uint64_t idx = f0 + t;
     const uint32_t nf = a.count - f0 < kTile ? (uint32_t)(a.count - f0) : kTile;
@@ -596,7 +612,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int i = 0; i < CPT; i++) {
             const uint32_t c = S + 16u * (t + 256u * i);
-            v[i] = c < span ? load16<true>(reinterpret_cast<const void*>(A0 + c)) : make_uint4(0, 0, 0, 0);
+            v[i] = c < span ? load16g<true>(A0 + c) : make_uint4(0, 0, 0, 0);
         }
     };
     const bool plausible = hi >= lo && hi <= a.data_bytes && hi - lo <= (1ull << 30);
@@ -605,6 +621,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // span is small enough for 32-bit span-relative arithmetic
     const bool inside = !have || (ok && off >= lo && off + len <= hi);
     const bool span_ok = __syncthreads_and(inside) && plausible;
+    NEXG_SPAN_STAMP(1);
     nexg_record r{};
     if (!span_ok) {  // not packed here: every lane parses its own frame from HBM
         if (have) {
@@ -699,6 +716,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (NB == 1) __syncthreads();
     }
     if (NB == 2) __syncthreads();  // the stage buffers become per-lane slots below
+    NEXG_SPAN_STAMP(2);
     uint8_t* const slots = &s_bytes[0][0];  // 80 B per lane from here on
     // (A) every lane: the canonical fast path on its head window
     uint32_t code = 0, key = 0;
@@ -732,6 +750,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // path for the few declined lanes of each wave. Items: {span position,
     // len | tail end << 16, tail sum, owner lane} in the idle prefix buffer;
     // results go back through the owner's slot.
+    NEXG_SPAN_STAMP(3);
     if (__syncthreads_or(gen)) {
         if (t < kBuckets) s_hist[t] = 0;
         __syncthreads();
@@ -825,6 +844,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // group as a mixed one — head 0, stored at the start — which keeps the
     // uniformity test and the head store out of the generic section's register
     // budget: with them the App. C mix ran 10 % slower, profiles/r03/grouped)
+    NEXG_SPAN_STAMP(4);
     if (sparse_like(OUT)) store_sparse_coded<OUT, false>(a, idx, have, r, code);
     else if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
     if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the slots (pitch 80 B)
@@ -832,6 +852,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         __syncthreads();
         copy_out_records<SpanFrame::kSlot>(slots, a.out, f0, nf);
     }
+    NEXG_SPAN_STAMP(5);
 }
 
 }  // namespace nexg

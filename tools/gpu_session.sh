@@ -42,6 +42,7 @@ for s in ${STEPS:-tests}; do
     orderbench) step orderbench 300 ./tools/orderbench
                 step orderbench52 300 ./tools/orderbench 54525952 ;;
     buildocc) step buildocc 900 bash tools/build_occ_ab.sh ;;
+    spantiming) step spantiming 300 python -u tools/span_timing.py abvar/libnexg_timing.so ;;
     sizesweep) step sizesweep 900 bash tools/size_sweep.sh ;;
     tileorder3) step tileorder3 900 bash tools/tile_order_ab3.sh ;;
     ordertests) step ordertests 600 python -u -m pytest tests/test_gpu_tile_order.py -x -v --timeout 300 --timeout-method thread ;;
