@@ -449,8 +449,12 @@ static void launch_l4_fam(const L4Args& a, uint32_t flen, hipStream_t s) {
     const uint64_t blocks = (a.count + kBuildTile - 1) / kBuildTile;
     const bool staged = a.out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(a.out) & 15u) == 0;
     (void)flen;
+    // IPv6: 16-KiB tile + build_lds_pad() -> 5 workgroups per CU (icmp6 echo
+    // 0.29 -> 0.26 ms at 16M frames); IPv4 shapes run faster at 8 per CU (tcp
+    // SYN 0.21 vs 0.24-0.26 ms, icmp echo 0.132 vs 0.140; profiles/r04/builders/)
+    const uint32_t pad = FAM == 6 ? build_lds_pad() : 0u;
     if (staged && a.out_stride <= 64u)
-        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 64>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 64>), dim3((uint32_t)blocks), dim3(kBuildTile), pad, s, a);
     else if (staged)
         hipLaunchKernelGGL((k_build_l4<FAM, KIND, kBuildMaxStride>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     else
@@ -849,7 +853,7 @@ hipError_t launch_build_udp6(const nexg_udp6_build& p, uint8_t* out, uint32_t ou
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
     // a 16-KiB tile for the udp_ping shapes keeps ~10 workgroups per CU
     if (staged && out_stride <= 64u)
-        hipLaunchKernelGGL(k_build_udp6<64>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+        hipLaunchKernelGGL(k_build_udp6<64>, dim3((uint32_t)blocks), dim3(kBuildTile), build_lds_pad(), s, a);  // 0.279 -> 0.253 ms
     else if (staged)
         hipLaunchKernelGGL(k_build_udp6<kBuildMaxStride>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     else

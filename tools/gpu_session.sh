@@ -43,6 +43,8 @@ for s in ${STEPS:-tests}; do
                 step orderbench52 300 ./tools/orderbench 54525952 ;;
     buildocc) step buildocc 900 bash tools/build_occ_ab.sh ;;
     spantiming) step spantiming 300 python -u tools/span_timing.py abvar/libnexg_timing.so ;;
+    builders) step builders_tests 600 python -u -m pytest tests/test_gpu_build_l4.py tests/test_gpu_build_probe.py tests/test_gpu_parity.py -k "build or udp_ping or probe" -q -x --timeout 300 --timeout-method thread
+              step builders_ab 600 bash -c 'for r in 1 2; do NEXG_BUILD_LDS_PAD=0 python tools/bench_builders.py || exit 1; python tools/bench_builders.py || exit 1; done' ;;
     sizesweep) step sizesweep 900 bash tools/size_sweep.sh ;;
     tileorder3) step tileorder3 900 bash tools/tile_order_ab3.sh ;;
     ordertests) step ordertests 600 python -u -m pytest tests/test_gpu_tile_order.py -x -v --timeout 300 --timeout-method thread ;;
