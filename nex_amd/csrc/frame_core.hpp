@@ -669,7 +669,9 @@ NEXG_HD bool fast_udp4_64(const uint32_t (&w)[16], uint32_t opt_flags, nexg_reco
 // TCP header that does not parse (transport layer only, Q14), and IP lengths
 // that end the layer before the frame end (Ethernet padding) or past it
 // (clamped unless strict). w0[k] holds bytes 4k..4k+3 of the frame
-// (little-endian), already zero past `len`; tail_sum is the frame-relative
+// (little-endian); bytes past `len` may hold anything (every sum and field
+// below reads only bytes the checks before it placed inside the frame, and
+// the window is masked to the IP end, which is at most `len`); tail_sum is the frame-relative
 // little-endian halfword sum of bytes [80, tail_end) (even frame offsets weigh
 // 1, odd 256; 0 when tail_end <= 80) or any value congruent to it mod 0xFFFF
 // that is 0 only when it is (callers holding an absolute-parity sum of a frame
@@ -796,7 +798,7 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     uint32_t suf[21];
     suf[20] = 0;
 #pragma unroll
-    for (int k = 19; k >= 0; k--) suf[k] = suf[k + 1] + halves(w[k]);
+    for (int k = 19; k >= 0; k--) suf[k] = halves_acc(w[k], suf[k + 1]);
     auto rest = [&](uint32_t s) {  // LE sum of window bytes [s, 80), s even
         return (s & 2u) ? suf[(s >> 2) + 1] + (w[s >> 2] >> 16) : suf[s >> 2];
     };
@@ -814,10 +816,11 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     }
     const uint64_t restsum = (uint64_t)rw + tail_sum;
     // pseudo-header address words (LE halves), util.rs:91-93 / 122-123
-    uint32_t p6 = 0;
+    // (bytes 22..53 and 26..33 as dword halves: one v_sad_u16 per dword)
+    uint32_t p6 = (w[5] >> 16) + (w[13] & 0xFFFFu);
 #pragma unroll
-    for (uint32_t k = 0; k < 32; k += 2) p6 += wle16(w, 22 + k);
-    const uint32_t p4 = wle16(w, 26) + wle16(w, 28) + wle16(w, 30) + wle16(w, 32);
+    for (int k = 6; k <= 12; k++) p6 = halves_acc(w[k], p6);
+    const uint32_t p4 = halves_acc(w[7], (w[6] >> 16) + (w[8] & 0xFFFFu));
     const uint32_t pseudo = v6 ? p6 : p4;
     uint32_t hdr;  // L4 header words other than the checksum (LE halves)
     if (tcp) hdr = LE(0) + LE(2) + LE(4) + LE(6) + LE(8) + LE(10) + LE(12) + LE(14) + LE(18);

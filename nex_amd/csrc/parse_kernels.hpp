@@ -464,12 +464,9 @@ __global__ __launch_bounds__(256) void k_parse_lane80(ParseArgs a) {
         uint32_t d[21];
 #pragma unroll
         for (int j = 0; j < 21; j++) d[j] = q == 0 ? u[j] : q == 1 ? u[j + 1] : q == 2 ? u[j + 2] : u[j + 3];
-        uint32_t w[20];
+        uint32_t w[20];  // bytes past len left in place: fast_canonical80 never reads them
 #pragma unroll
-        for (int k = 0; k < 20; k++) {
-            const uint32_t v = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-            w[k] = 4u * k < len ? (v & range_mask(4u * k, 0, len)) : 0u;
-        }
+        for (int k = 0; k < 20; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
         // k_tail_sums weights by absolute parity (see k_parse_span)
         done = fast_canonical80(w, len, a.opt_flags, (uint64_t)tail << (8u * (sh & 1u)), len, r);
     }
@@ -723,20 +720,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     bool gen = false;
     const uint32_t tq = want_tail ? qb - qa : 0u;
     if (have) {
+        // the realigned window; bytes past len (the next frame's) are left in
+        // place: fast_canonical80 never reads them, the slot copy masks them
         uint32_t w[20];
 #pragma unroll
-        for (int k = 0; k < 20; k++) {
-            const uint32_t v = __builtin_amdgcn_alignbyte(u[k + 1], u[k], sh);
-            w[k] = 4u * k < len ? (v & range_mask(4u * k, 0, len)) : 0u;
-        }
+        for (int k = 0; k < 20; k++) w[k] = __builtin_amdgcn_alignbyte(u[k + 1], u[k], sh);
         // Q weights bytes by absolute parity; fast_canonical80 wants the
         // frame-relative LE sum: x256 (mod 0xFFFF) for a frame at an odd address
         const uint64_t tail = (sh & 1u) ? (uint64_t)tq * 256u : (uint64_t)tq;
         if (fast_canonical80(w, len, a.opt_flags, tail, qend, r)) {
             if (sparse_like(OUT)) code = canonical80_code(r);
             if (OUT == NEXG_OUT_RECORD) stage_record(slots + SpanFrame::kSlot * t, r);
-        } else {  // declined: the window goes to this lane's slot for pass (B)
+        } else {  // declined: the window goes to this lane's slot for pass (B), zero past len
             gen = true;
+#pragma unroll
+            for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
             key = span_bucket(w[3], w[5], a.opt_flags);
 #pragma unroll
             for (int k = 0; k < 5; k++)

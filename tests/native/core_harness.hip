@@ -73,7 +73,12 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                 // the second prefix value at span_tail_end (the IP end of a padded frame)
                 const uint32_t te = nexg::span_tail_end(w80[3], w80[4], (uint32_t)len, flags);
                 const uint32_t tail = len > 80 ? Q(o + te) - Q(o + 80u) : 0u;
-                if (nexg::fast_canonical80(w80, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, te, r)) {
+                // the span kernel hands fast_canonical80 its window unmasked: the
+                // next frame's bytes past len (here a poison pattern) must not matter
+                uint32_t wf[20];
+                memset(wf, 0xA5, sizeof(wf));
+                memcpy(wf, g, len < 80 ? len : 80);
+                if (nexg::fast_canonical80(wf, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, te, r)) {
                     // the span kernel stores canonical80_code for these: it must be the encoder's code
                     if (nexg::canonical80_code(r) != nexg::sparse_encode(r, flags, ip_offset)) return -2;
                 } else {
@@ -199,13 +204,16 @@ extern "C" int harness_span_groups(const uint8_t* data, uint64_t data_bytes, con
             const uint8_t* g = data + off;
             uint32_t w[20] = {0};
             memcpy(w, g, l < W ? l : W);
+            uint32_t wf[20];  // as the kernel: the window unmasked past len (the batch's next bytes)
+            memset(wf, 0x5A, sizeof(wf));
+            memcpy(wf, g, (uint64_t)W <= (uint64_t)(data + data_bytes - g) ? W : (size_t)(data + data_bytes - g));
             qend[t] = nexg::span_tail_end(w[3], w[4], len[t], flags);
             uint32_t q = 0;  // absolute-parity LE sum of [80, qend): Q(end) - Q(start + 80)
             for (uint32_t k = W; k < qend[t]; k++) q += (uint32_t)g[k] << (((base + off + k) & 1u) ? 8u : 0u);
             tq[t] = len[t] > W ? q : 0u;
             nexg_record r{};
             const uint64_t tail = ((base + off) & 1u) ? (uint64_t)tq[t] * 256u : (uint64_t)tq[t];
-            if (nexg::fast_canonical80(w, len[t], flags, tail, qend[t], r)) {
+            if (nexg::fast_canonical80(wf, len[t], flags, tail, qend[t], r)) {
                 out[f0 + t] = r;
             } else {
                 gen[t] = true;
