@@ -762,13 +762,19 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     const bool inwin = e <= 80u;  // checksummed bytes all in the window
     if (e != len && e != tail_end && !inwin) return false;
     const uint32_t n = e - l4;
-    uint32_t w[20];
-#pragma unroll
-    for (int k = 0; k < 20; k++) w[k] = 4u * k >= e ? 0u : (w0[k] & range_mask(4u * k, 0, e));
+    // the window as given: bytes past e are only ever summed by the payload
+    // sums below, which take the bytes [e, 80) back out when e <= 80; every
+    // header field read here lies before e whenever it is used
+    const uint32_t (&w)[20] = w0;
     if (inwin) tail_sum = 0;
-    // L4 header words at l4 + k (compile-time extraction for both offsets + select)
-    auto L = [&](uint32_t k) { return v6 ? wbe16(w, 54u + k) : wbe16(w, 34u + k); };
-    auto LE = [&](uint32_t k) { return v6 ? wle16(w, 54u + k) : wle16(w, 34u + k); };
+    // the L4 header's dwords, selected once: l4 = 34 / 54 = 2 mod 4, so bytes
+    // l4 - 2 .. l4 + 21 are dwords 8..13 / 13..18 and byte l4 + k sits at
+    // offset k + 2 of hd (k even: a whole little-endian half of one dword)
+    uint32_t hd[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) hd[j] = v6 ? w[13 + j] : w[8 + j];
+    auto LE = [&](uint32_t k) { return ((k + 2u) & 2u) ? hd[(k + 2u) >> 2] >> 16 : hd[(k + 2u) >> 2] & 0xFFFFu; };
+    auto L = [&](uint32_t k) { const uint32_t x = LE(k); return ((x & 0xFFu) << 8) | (x >> 8); };
     const bool tcp = pv == 6u, udp = pv == 17u, icmp = pv == (v6 ? 58u : 1u);
     const uint32_t doff = L(12) >> 12, ulen = L(4);
     const uint32_t o0 = v6 ? w[18] : w[13], o1 = v6 ? w[19] : w[14];
@@ -814,6 +820,17 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
         case 62: rw = rest(62); break;
         default: rw = rest(74); break;
     }
+    if (inwin) {  // minus the window bytes [e, 80): dword e / 4 from byte e % 4 on, and the dwords after it
+        const uint32_t q = e >> 2;
+        uint32_t wq = 0, sq = 0;
+#pragma unroll
+        for (int k = 8; k < 20; k++) {
+            const bool m = q == (uint32_t)k;
+            wq = m ? w[k] : wq;
+            sq = m ? suf[k + 1] : sq;
+        }
+        rw -= q >= 20u ? 0u : halves_acc(wq & (0xFFFFFFFFu << (8u * (e & 3u))), sq);
+    }
     const uint64_t restsum = (uint64_t)rw + tail_sum;
     // pseudo-header address words (LE halves), util.rs:91-93 / 122-123
     // (bytes 22..53 and 26..33 as dword halves: one v_sad_u16 per dword)
@@ -823,9 +840,9 @@ NEXG_HD bool fast_canonical80(const uint32_t (&w0)[20], uint32_t len, uint32_t o
     const uint32_t p4 = halves_acc(w[7], (w[6] >> 16) + (w[8] & 0xFFFFu));
     const uint32_t pseudo = v6 ? p6 : p4;
     uint32_t hdr;  // L4 header words other than the checksum (LE halves)
-    if (tcp) hdr = LE(0) + LE(2) + LE(4) + LE(6) + LE(8) + LE(10) + LE(12) + LE(14) + LE(18);
-    else if (udp) hdr = LE(0) + LE(2);
-    else hdr = LE(0);
+    if (tcp) hdr = halves_acc(hd[3], halves_acc(hd[2], halves_acc(hd[1], (hd[0] >> 16) + (hd[4] & 0xFFFFu) + (hd[5] & 0xFFFFu))));
+    else if (udp) hdr = halves_acc(hd[1] & 0xFFFFu, hd[0] >> 16);
+    else hdr = hd[0] >> 16;
     uint64_t t4 = 256ull * ((icmp && !v6 ? 0u : pseudo) + hdr + restsum);
     t4 += (icmp && !v6) ? 0u : (pv + n);  // pseudo proto + length (BE constants)
     if (udp) t4 += n;                     // UDP length word as serialised
