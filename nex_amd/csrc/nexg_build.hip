@@ -340,6 +340,7 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
     constexpr int NIP = FAM == 4 ? 10 : 20;             // IP header halfwords
     constexpr int NL4 = KIND == kL4Tcp ? 10 : 4;        // fixed L4 header halfwords
     constexpr int NH = 7 + NIP + NL4;
+    static_assert(NH % 2 == 1, "lds_put_halfwords takes an odd halfword count");
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
     __shared__ uint32_t s_pay;
     const uint32_t tid = threadIdx.x;
@@ -427,8 +428,12 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
         uint8_t* base = STAGED ? smem : a.out + first * a.out_stride;
         const uint32_t d0 = tid * a.out_stride;
         const bool odd = (a.out_stride & 1u) != 0;
+        if (STAGED && !odd) {
+            lds_put_halfwords<NH>(base, d0, hw);  // dword writes (NH odd): half the LDS stores
+        } else {
 #pragma unroll
-        for (int k = 0; k < NH; k++) put_hw(base, d0 + 2u * k, hw[k], odd);
+            for (int k = 0; k < NH; k++) put_hw(base, d0 + 2u * k, hw[k], odd);
+        }
         uint32_t p = d0 + 2u * NH;
         if (KIND == kL4Tcp) {
             for (uint32_t k = 0; k < a.opt_padded; k += 2) put_hw(base, p + k, a.options[k] | ((uint32_t)a.options[k + 1] << 8), odd);
@@ -455,6 +460,9 @@ static void launch_l4_fam(const L4Args& a, uint32_t flen, hipStream_t s) {
     const uint32_t pad = FAM == 6 ? build_lds_pad() : 0u;
     if (staged && a.out_stride <= 64u)
         hipLaunchKernelGGL((k_build_l4<FAM, KIND, 64>), dim3((uint32_t)blocks), dim3(kBuildTile), pad, s, a);
+    else if (staged && a.out_stride <= 80u)  // tcp_ping's 66 B: a 20-KiB tile (7 per CU) instead of 32 KiB (4)
+        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 80>), dim3((uint32_t)blocks), dim3(kBuildTile),
+                           FAM == 6 && pad ? pad - 4096u : 0u, s, a);
     else if (staged)
         hipLaunchKernelGGL((k_build_l4<FAM, KIND, kBuildMaxStride>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     else
