@@ -211,6 +211,7 @@ struct Build6Args {
     nexg_udp6_build p;
     uint8_t* out;
     uint32_t out_stride;
+    uint32_t tile_order;  // tile_index order (nexg_internal.hpp), as k_build_udp4
 };
 
 template <uint32_t MAXS>
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
     constexpr bool STAGED = MAXS != 0;
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
     const nexg_udp6_build& p = a.p;
-    const uint64_t first = (uint64_t)blockIdx.x * kBuildTile;
+    const uint64_t first = tile_index(a.tile_order) * kBuildTile;
     const uint64_t left = p.count - first;
     const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
     const uint32_t tid = threadIdx.x;
@@ -322,6 +323,7 @@ struct L4Args {
     uint64_t count;
     uint8_t* out;
     uint32_t out_stride;
+    uint32_t tile_order;  // tile_index order (nexg_internal.hpp), as k_build_udp4
 };
 
 // halfword v (memory order: low byte first) at LDS/global byte offset p
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
     __shared__ uint32_t s_pay;
     const uint32_t tid = threadIdx.x;
-    const uint64_t first = (uint64_t)blockIdx.x * kBuildTile;
+    const uint64_t first = tile_index(a.tile_order) * kBuildTile;
     const uint64_t left = a.count - first;
     const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
     const uint64_t i = first + tid;
@@ -469,8 +471,9 @@ static void launch_l4_fam(const L4Args& a, uint32_t flen, hipStream_t s) {
         hipLaunchKernelGGL((k_build_l4<FAM, KIND, 0>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
 }
 
-static hipError_t launch_l4(const L4Args& a, int kind, uint32_t flen, hipStream_t s) {
+static hipError_t launch_l4(L4Args& a, int kind, uint32_t flen, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
+    a.tile_order = l4_build_tile_order();
     if (kind == kL4Tcp) {
         if (a.ip.family == 4) launch_l4_fam<4, kL4Tcp>(a, flen, s);
         else launch_l4_fam<6, kL4Tcp>(a, flen, s);
@@ -856,7 +859,7 @@ hipError_t launch_build_udp4(const nexg_udp4_build& p, uint8_t* out, uint32_t ou
 hipError_t launch_build_udp6(const nexg_udp6_build& p, uint8_t* out, uint32_t out_stride,
                              hipStream_t s) {
     if (p.count == 0) return hipSuccess;
-    Build6Args a{p, out, out_stride};
+    Build6Args a{p, out, out_stride, l4_build_tile_order()};
     const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
     // a 16-KiB tile for the udp_ping shapes keeps ~10 workgroups per CU

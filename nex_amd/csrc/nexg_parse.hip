@@ -50,6 +50,15 @@ uint32_t build_tile_order() {
     return forced >= 0 ? (uint32_t)forced : 1u;
 }
 
+// Tile order of the builders with several per-frame parameter arrays
+// (k_build_udp6, k_build_l4); NEXG_L4_ORDER overrides. Grid order: contiguous
+// eighths made tcp SYN 0.199 -> 0.230-0.240 ms and tcp_ping 0.247 -> 0.30 at
+// 16M frames, icmp4 echo 0.133 -> 0.129 (profiles/r04/builders/order_ab.log).
+uint32_t l4_build_tile_order() {
+    static const int forced = order_from_env("NEXG_L4_ORDER");
+    return forced >= 0 ? (uint32_t)forced : 0u;
+}
+
 ParseVariant choose_parse_variant(const ParseArgs& a) {
     const bool aligned = (reinterpret_cast<uint64_t>(a.data) & 15u) == 0;
     if (!a.offsets && aligned && a.stride % 16u == 0 && a.stride > 0 && a.stride <= 128u &&

@@ -8,7 +8,8 @@ the tiles; a wrong one skips some frames and parses others twice.
 - every order the env overrides select (grid, contiguous eighths, runs of
   3 / 8 / 16 / 64) in a child process per order: the parse outputs of fixed
   64-B and 96-B strides and of a packed IMIX batch (span kernel), and the
-  udp_ping builds, hashed and compared with the grid-order run."""
+  udp_ping / udp6 / tcp_ping / icmp_ping builds, hashed and compared with
+  the grid-order run."""
 import json
 import os
 import subprocess
@@ -54,12 +55,24 @@ p = e.gen_udp4_params(nf, first_index=3)
 put("build.full", e.build_udp4(*p))
 put("build.probe", e.build_udp4(None, p[1], def_src_ip=0x0A000001, def_src_port=40000, def_dst_port=33435))
 put("build.tuples", e.build_udp4_tuples(e.pack_udp4_tuples(*p)))
+g = torch.Generator(device="cuda").manual_seed(9)
+rb = lambda *s: torch.randint(0, 256, s, dtype=torch.uint8, device="cuda", generator=g)
+r16 = lambda: torch.randint(-32768, 32767, (nf,), dtype=torch.int16, device="cuda", generator=g)
+a4s, a4d, a6s, a6d, sp, dp = rb(nf, 4), rb(nf, 4), rb(nf, 16), rb(nf, 16), r16(), r16()
+seq = torch.randint(-2**31, 2**31 - 1, (nf,), dtype=torch.int32, device="cuda", generator=g)
+opts = bytes.fromhex("020405b4040201010303 07".replace(" ", ""))
+put("build.udp6", e.build_udp6(a6s, a6d, sp, dp))
+put("build.tcp4", e.build_tcp(4, a4s, a4d, sp, dp, seq, None, flags=0x02, window=64240))
+put("build.tcp4_opts", e.build_tcp(4, a4s, a4d, sp, dp, seq, None, flags=0x02, window=64240, options=opts))
+put("build.tcp6", e.build_tcp(6, a6s, a6d, sp, dp, seq, None, flags=0x12, window=1024))
+put("build.icmp4", e.build_icmp_echo(4, a4s, a4d, sp, dp))
+put("build.icmp6", e.build_icmp_echo(6, a6s, a6d, sp, dp))
 print(json.dumps(h))
 '''
 
 
 def run_child(order):
-    env = dict(os.environ, NEXG_TILE_ORDER=order, NEXG_BUILD_ORDER=order)
+    env = dict(os.environ, NEXG_TILE_ORDER=order, NEXG_BUILD_ORDER=order, NEXG_L4_ORDER=order)
     r = subprocess.run([sys.executable, "-c", CHILD, str(N_FIXED), str(N_IMIX)], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -6,7 +6,7 @@ and with its option list (54 / 66 B), icmp_ping echo (IPv4 42 B, IPv6 62 B),
 HIP events around the launches. Prints one JSON object: per shape kernel ms
 and the fraction of 8 TB/s written. Run once per NEXG_BUILD_LDS_PAD setting
 to compare occupancies (the pad is read once per process).
-usage: [NEXG_BUILD_LDS_PAD=0] python tools/bench_builders.py [--frames N]"""
+usage: [NEXG_BUILD_LDS_PAD=0] [NEXG_L4_ORDER=linear|xcd|xcdK] python tools/bench_builders.py [--frames N]"""
 import argparse
 import json
 import os
@@ -42,7 +42,8 @@ def main():
         "icmp4_echo_42B": (42, lambda out: eng.build_icmp_echo(4, a4s, a4d, sp, dp, ip_id=ipid, out=out)),
         "icmp6_echo_62B": (62, lambda out: eng.build_icmp_echo(6, a6s, a6d, sp, dp, out=out)),
     }
-    res = {"frames": n, "lds_pad": os.environ.get("NEXG_BUILD_LDS_PAD", "default")}
+    res = {"frames": n, "lds_pad": os.environ.get("NEXG_BUILD_LDS_PAD", "default"),
+           "order": os.environ.get("NEXG_L4_ORDER", "default")}
     for name, (flen, fn) in shapes.items():
         out = torch.empty(n * flen, dtype=torch.uint8, device="cuda")
         for _ in range(10):
