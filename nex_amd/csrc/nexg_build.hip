@@ -88,6 +88,15 @@ __device__ __forceinline__ void lds_put_halfwords(uint8_t* smem, uint32_t d0, co
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }
 
+// Per-frame parameter or the batch default. The array is read as a global
+// (address-space 1) pointer: written as `per ? per[i] : def` with def in the
+// kernel arguments, the compiler selected between the two addresses and issued
+// flat loads (counted on both vmcnt and lgkmcnt) for every parameter.
+template <class T>
+__device__ __forceinline__ uint32_t per_or_def(const T* per, uint64_t i, uint32_t def) {
+    return per ? (uint32_t)NEXG_GLOBAL(T, per)[i] : def;
+}
+
 // tile copy-out shared by the builders: nf frames of `stride` bytes staged
 // contiguously in LDS leave as 16-B non-temporal stores (+ byte tail of a
 // partial tile). Non-temporal: the udp_ping build of 16M frames takes 0.132
@@ -233,8 +242,8 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
         uint32_t sw[4], dw[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) { sw[k] = s4[k]; dw[k] = d4[k]; }
-        const uint32_t sp = p.src_port ? p.src_port[i] : p.def_src_port;
-        const uint32_t dp = p.dst_port ? p.dst_port[i] : p.def_dst_port;
+        const uint32_t sp = per_or_def(p.src_port, i, p.def_src_port);
+        const uint32_t dp = per_or_def(p.dst_port, i, p.def_dst_port);
         const uint32_t ulen = 8u + p.payload_len;
         // util.rs:111-133 pseudo-header: address segments (as LE halves x 256),
         // next header 17, length; then sport, dport, length, payload (skipword 3)
@@ -246,10 +255,10 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
         uint32_t hw[31];
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-            const uint32_t b0 = p.dst_mac ? p.dst_mac[i * 6 + 2 * k] : p.def_dst_mac[2 * k];
-            const uint32_t b1 = p.dst_mac ? p.dst_mac[i * 6 + 2 * k + 1] : p.def_dst_mac[2 * k + 1];
-            const uint32_t c0 = p.src_mac ? p.src_mac[i * 6 + 2 * k] : p.def_src_mac[2 * k];
-            const uint32_t c1 = p.src_mac ? p.src_mac[i * 6 + 2 * k + 1] : p.def_src_mac[2 * k + 1];
+            const uint32_t b0 = per_or_def(p.dst_mac, i * 6 + 2 * k, p.def_dst_mac[2 * k]);
+            const uint32_t b1 = per_or_def(p.dst_mac, i * 6 + 2 * k + 1, p.def_dst_mac[2 * k + 1]);
+            const uint32_t c0 = per_or_def(p.src_mac, i * 6 + 2 * k, p.def_src_mac[2 * k]);
+            const uint32_t c1 = per_or_def(p.src_mac, i * 6 + 2 * k + 1, p.def_src_mac[2 * k + 1]);
             hw[k] = b0 | (b1 << 8);
             hw[3 + k] = c0 | (c1 << 8);
         }
@@ -368,10 +377,10 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
         uint32_t hw[NH];
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-            const uint32_t b0 = ip.dst_mac ? ip.dst_mac[i * 6 + 2 * k] : ip.def_dst_mac[2 * k];
-            const uint32_t b1 = ip.dst_mac ? ip.dst_mac[i * 6 + 2 * k + 1] : ip.def_dst_mac[2 * k + 1];
-            const uint32_t c0 = ip.src_mac ? ip.src_mac[i * 6 + 2 * k] : ip.def_src_mac[2 * k];
-            const uint32_t c1 = ip.src_mac ? ip.src_mac[i * 6 + 2 * k + 1] : ip.def_src_mac[2 * k + 1];
+            const uint32_t b0 = per_or_def(ip.dst_mac, i * 6 + 2 * k, ip.def_dst_mac[2 * k]);
+            const uint32_t b1 = per_or_def(ip.dst_mac, i * 6 + 2 * k + 1, ip.def_dst_mac[2 * k + 1]);
+            const uint32_t c0 = per_or_def(ip.src_mac, i * 6 + 2 * k, ip.def_src_mac[2 * k]);
+            const uint32_t c1 = per_or_def(ip.src_mac, i * 6 + 2 * k + 1, ip.def_src_mac[2 * k + 1]);
             hw[k] = b0 | (b1 << 8);
             hw[3 + k] = c0 | (c1 << 8);
         }
@@ -380,10 +389,10 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
         uint64_t t;
         constexpr int L = 7 + NIP;  // first L4 halfword
         if (KIND == kL4Tcp) {
-            const uint32_t sp = a.sport ? a.sport[i] : a.def_sport;
-            const uint32_t dp = a.dport ? a.dport[i] : a.def_dport;
-            const uint32_t sq = a.seq ? a.seq[i] : a.def_seq;
-            const uint32_t ak = a.ack ? a.ack[i] : a.def_ack;
+            const uint32_t sp = per_or_def(a.sport, i, a.def_sport);
+            const uint32_t dp = per_or_def(a.dport, i, a.def_dport);
+            const uint32_t sq = per_or_def(a.seq, i, a.def_seq);
+            const uint32_t ak = per_or_def(a.ack, i, a.def_ack);
             const uint32_t w6 = ((l4_hdr / 4u) << 12) | (a.flags & 0xFFu);
             t = sp + dp + (sq >> 16) + (sq & 0xFFFFu) + (ak >> 16) + (ak & 0xFFFFu) + w6 + a.window + a.urg +
                 a.opt_sum + pay_sum;
@@ -393,8 +402,8 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
             hw[L + 6] = bswap16(w6); hw[L + 7] = bswap16(a.window);
             hw[L + 9] = bswap16(a.urg);
         } else {
-            const uint32_t id = a.ident ? a.ident[i] : a.def_ident;
-            const uint32_t sq = a.seqno ? a.seqno[i] : a.def_seqno;
+            const uint32_t id = per_or_def(a.ident, i, a.def_ident);
+            const uint32_t sq = per_or_def(a.seqno, i, a.def_seqno);
             const uint32_t w0 = (a.icmp_type << 8) | a.icmp_code;
             t = w0 + id + sq + pay_sum;
             hw[L + 0] = bswap16(w0);
@@ -405,7 +414,7 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
         hw[KIND == kL4Tcp ? L + 8 : L + 1] = bswap16(cs);
         // ---- IP header ----
         if (FAM == 4) {
-            const uint32_t total = 20u + l4_len, id = ip.ip_id ? ip.ip_id[i] : ip.def_ip_id;
+            const uint32_t total = 20u + l4_len, id = per_or_def(ip.ip_id, i, ip.def_ip_id);
             const uint32_t w0 = (0x45u << 8) | ip.tos, w3 = ((uint32_t)(ip.ip_flags & 7u)) << 13;
             const uint32_t w4 = ((uint32_t)ip.ttl << 8) | proto;
             const uint32_t ics = fold_complement(256ull * addr_le + w0 + total + id + w3 + w4);
@@ -438,7 +447,12 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
         }
         uint32_t p = d0 + 2u * NH;
         if (KIND == kL4Tcp) {
-            for (uint32_t k = 0; k < a.opt_padded; k += 2) put_hw(base, p + k, a.options[k] | ((uint32_t)a.options[k + 1] << 8), odd);
+            // unrolled over the 40-B maximum with a uniform guard: constant
+            // kernarg offsets become scalar loads, where a run-time index made
+            // one vector load + vmcnt(0) wait per option halfword pair
+#pragma unroll
+            for (uint32_t k = 0; k < 40u; k += 2)
+                if (k < a.opt_padded) put_hw(base, p + k, a.options[k] | ((uint32_t)a.options[k + 1] << 8), odd);
             p += a.opt_padded;
         }
         for (uint32_t k = 0; k < a.payload_len; k++) base[p + k] = a.payload[k];
