@@ -156,10 +156,10 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
         const u32x4 tv = AOS ? reinterpret_cast<const u32x4*>(a.tuples)[i] : u32x4{0, 0, 0, 0};
 #endif
         const uint32_t dst = AOS ? tv.y : p.dst_ip[i];
-        const uint32_t src = AOS ? tv.x : FULL ? p.src_ip[i] : PROBE ? p.def_src_ip : per_or_def(p.src_ip, i, p.def_src_ip);
-        const uint32_t sp = AOS ? tv.z & 0xFFFFu : FULL ? p.src_port[i] : PROBE ? p.def_src_port : per_or_def(p.src_port, i, p.def_src_port);
-        const uint32_t dp = AOS ? tv.z >> 16 : FULL ? p.dst_port[i] : PROBE ? p.def_dst_port : per_or_def(p.dst_port, i, p.def_dst_port);
-        const uint32_t id = AOS ? tv.w & 0xFFFFu : FULL ? p.ip_id[i] : PROBE ? p.def_ip_id : per_or_def(p.ip_id, i, p.def_ip_id);
+        const uint32_t src = AOS ? tv.x : FULL ? p.src_ip[i] : PROBE ? p.def_src_ip : (p.src_ip ? p.src_ip[i] : p.def_src_ip);
+        const uint32_t sp = AOS ? tv.z & 0xFFFFu : FULL ? p.src_port[i] : PROBE ? p.def_src_port : (p.src_port ? p.src_port[i] : p.def_src_port);
+        const uint32_t dp = AOS ? tv.z >> 16 : FULL ? p.dst_port[i] : PROBE ? p.def_dst_port : (p.dst_port ? p.dst_port[i] : p.def_dst_port);
+        const uint32_t id = AOS ? tv.w & 0xFFFFu : FULL ? p.ip_id[i] : PROBE ? p.def_ip_id : (p.ip_id ? p.ip_id[i] : p.def_ip_id);
         const uint32_t ulen = 8u + p.payload_len, total = 20u + ulen;
         const uint64_t addr = (uint64_t)(src >> 16) + (src & 0xFFFFu) + (dst >> 16) + (dst & 0xFFFFu);
         // udp.rs:443-477 on to_bytes(): pseudo + sport + dport + length (+ payload)
@@ -170,8 +170,8 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
         const uint32_t ics = fold_complement(addr + w0 + total + id + w3 + w4);
         uint8_t h[42];
         for (int k = 0; k < 6; k++) {
-            h[k] = !FULL && !PROBE && !AOS ? (uint8_t)per_or_def(p.dst_mac, i * 6 + k, p.def_dst_mac[k]) : p.def_dst_mac[k];
-            h[6 + k] = !FULL && !PROBE && !AOS ? (uint8_t)per_or_def(p.src_mac, i * 6 + k, p.def_src_mac[k]) : p.def_src_mac[k];
+            h[k] = !FULL && !PROBE && !AOS && p.dst_mac ? p.dst_mac[i * 6 + k] : p.def_dst_mac[k];
+            h[6 + k] = !FULL && !PROBE && !AOS && p.src_mac ? p.src_mac[i * 6 + k] : p.def_src_mac[k];
         }
         h[12] = 0x08; h[13] = 0x00;
         h[14] = (uint8_t)(w0 >> 8); h[15] = (uint8_t)w0;

@@ -47,7 +47,6 @@ for s in ${STEPS:-tests}; do
               step builders_ab 600 bash -c 'for r in 1 2; do NEXG_BUILD_LDS_PAD=0 python tools/bench_builders.py || exit 1; python tools/bench_builders.py || exit 1; done' ;;
     buildorder) step builders_tests 600 python -u -m pytest tests/test_gpu_build_l4.py tests/test_gpu_tile_order.py tests/test_gpu_parity.py -k "build or udp_ping or probe or order" -q -x --timeout 300 --timeout-method thread
                 step builders_order_ab 600 bash -c 'for r in 1 2 3; do python tools/bench_builders.py || exit 1; done' ;;
-    buildbench) step builders_bench 300 bash -c 'for r in 1 2; do python tools/bench_builders.py || exit 1; done' ;;
     sizesweep) step sizesweep 900 bash tools/size_sweep.sh ;;
     tileorder3) step tileorder3 900 bash tools/tile_order_ab3.sh ;;
     ordertests) step ordertests 600 python -u -m pytest tests/test_gpu_tile_order.py -x -v --timeout 300 --timeout-method thread ;;
