@@ -17,9 +17,13 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+
+from nex_amd import clocks  # noqa: E402  (imports no torch)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 IMIX_WARMUP = 40  # untimed launches before the 6-GB packed batches are timed (see imix_line)
@@ -185,13 +189,15 @@ def ser_line(eng, args, F, first, stream, device, rank, world):
     the host."""
     import torch
     from nex_amd import dist
-    p = ser_params(eng, F, first, "tuples_aos")
+    p = ser_params(eng, F, first, "tuples")
     out = torch.empty(F * 42, dtype=torch.uint8, device=device)
     torch.cuda.synchronize(device)
     alg = F * 42
     ceil = write_ceiling(eng, out, args, stream, device)
     res = {}
-    for shape in ("probe", "tuples", "tuples_aos"):
+    # ser.tuples_aos (nexg_build_udp4_tuples) is an entry-point check, slower than
+    # the five arrays (DESIGN.md §6 round 4): --workload ser --ser-shape tuples_aos
+    for shape in ("probe", "tuples"):
         elapsed, kernel_s = timed(ser_step(eng, p, out, stream, shape), args.steps, args.warmup, stream, device)
         tp = dist.throughput(F, alg, args.steps, elapsed, device)
         if rank != 0:
@@ -208,16 +214,88 @@ def ser_line(eng, args, F, first, stream, device, rank, world):
                           "basis": f"bytes written (SURVEY.md 8(d) SER); parameter reads ({SER_READ[shape]} "
                                    "B/frame) not counted",
                           "stream_ceilings": dict(ceil, frac_of_write_only=round(ach / ceil["write_only_gbs"], 4))}}
-        if world == 1 and not args.no_cpu_baseline and shape != "tuples_aos":  # same tuples as "tuples"
+        if world == 1 and not args.no_cpu_baseline:
             try:
                 hp = ser_probe_params(p) if shape == "probe" else p[:5]
                 r["cpu_baseline"] = cpu_baseline_ser(hp, 1 << 20, args.cpu_seconds / 4, host_threads())
             except Exception as e:
                 r["cpu_baseline"] = {"value": None, "error": repr(e)}
         res[shape] = r
+    del out, p
+    for shape in PROBE_SHAPES:
+        r = probe_object(eng, args, F, first, shape, stream, device, rank, world)
+        if r is not None:
+            res[shape] = r
     if rank != 0:
         return None
-    return dict(res["probe"], tuples=res["tuples"], tuples_aos=res["tuples_aos"])
+    return dict(res["probe"], tuples=res["tuples"], **{k: res[k] for k in PROBE_SHAPES})
+
+
+#: the other ping callers' probe batches in the serialize line
+PROBE_SHAPES = ("tcp_ping", "icmp_ping", "udp6")
+
+
+def cpu_baseline_probe(shape, dst_host, seconds, nthreads):
+    """Oracle builds of a probe batch (oracle/nex_oracle.c nexo_build_probe_batch:
+    the single-frame restatements of the example's builder chain, one per
+    destination) over a bounded sample of the same destinations."""
+    from nex_amd import probes
+    from oracle import oracle
+    from tests import helpers
+    n = dst_host.shape[0]
+    out = np.empty((n, probes.frame_len(shape)), np.uint8)
+    reps, t = 0, 0.0
+    while t < seconds and reps < 1000:
+        t0 = time.perf_counter()
+        helpers.probe_oracle_build(oracle, shape, dst_host, nthreads=nthreads, out=out)
+        t += time.perf_counter() - t0
+        reps += 1
+    L = probes.frame_len(shape)
+    return {"value": round(n * reps / t / 1e6, 3), "unit": "Mpkt/s", "cores": nthreads, "kind": "port",
+            "gib_s": round(L * n * reps / t / 2**30, 3),
+            "sample": f"{nthreads} thread(s), first {n} destinations of the same batch, {reps} passes ({t:.1f} s), "
+                      "oracle/nex_oracle.c nexo_build_probe_batch (literal restatement of the example's builder "
+                      "chain per frame; Rust reference not buildable here)"}
+
+
+def probe_object(eng, args, F, first, shape, stream, device, rank, world):
+    """One probe batch of nex_amd/probes.py (tcp_ping / icmp_ping / udp_ping's
+    IPv6 branch): F frames per GPU, a destination per frame (4 / 16 B read),
+    roofline on the bytes written, the oracle builder on the host."""
+    import torch
+    from nex_amd import dist, probes
+    L = probes.frame_len(shape)
+    g = torch.Generator(device=device).manual_seed(0x6E6578 + first)
+    dst = torch.randint(0, 256, (F, probes.dst_bytes(shape)), dtype=torch.uint8, device=device, generator=g)
+    src = probes.source(shape, device)
+    pay = torch.tensor(list(probes.ICMP_PAYLOAD), dtype=torch.uint8, device=device)
+    out = torch.empty(F * L, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize(device)
+    alg = F * L
+    step = lambda: probes.build(eng, shape, dst, src=src, out=out, stream=stream, payload_t=pay)
+    elapsed, kernel_s = timed(step, args.steps, args.warmup, stream, device)
+    tp = dist.throughput(F, alg, args.steps, elapsed, device)
+    if rank != 0:
+        return None
+    ach = alg / kernel_s / 1e9
+    rd = probes.dst_bytes(shape)
+    r = {"workload": f"SURVEY 8(f)3 probe batch: build+checksum {F} frames per GPU, " + probes.NOTE[shape]
+                     + f"; one source, a destination per frame ({rd} B read), the rest the example's constants",
+         "value": tp["value"], "unit": "Mpkt/s", "steps": args.steps, "ms_per_step": tp["ms_per_step"],
+         "gib_s": tp["gib_s"], "bytes_per_gpu": alg,
+         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic(f"ser_{shape}", "desc"),
+                      "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": alg,
+                      "frac_counting_reads": round((alg + F * rd) / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+                      "basis": f"bytes written ({L} B/frame); the destination reads ({rd} B/frame) not counted"}}
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            n = min(F, 1 << 20)
+            r["cpu_baseline"] = cpu_baseline_probe(shape, dst[:n].cpu().numpy(), args.cpu_seconds / 4,
+                                                   host_threads())
+        except Exception as e:
+            r["cpu_baseline"] = {"value": None, "error": repr(e)}
+    return r
 
 
 def load_traffic(workload, out_kind):
@@ -281,14 +359,43 @@ def stream_ceilings(eng, batch, args, stream, device):
                 continue
             _, ks = timed(lambda: eng.parse(batch, out_kind=kind, out=out, stream=stream),
                           args.steps, args.warmup, stream, device)
-            ach = batch.total_bytes / ks / 1e9
-            r[key] = {"kernel_ms": round(ks * 1e3, 4), "achieved": round(ach, 1),
-                      "frac": round(ach / HBM_PEAK_GBS, 4)}
+            r[key] = output_rate(batch, kind, ks)
+    return r
+
+
+OUT_WIDTH = {1: 8, 4: 4, 5: 2}  # nexg_desc / flags / verdict bytes per frame
+
+
+def output_rate(batch, kind, ks):
+    """An output kind's kernel time on a batch: fraction of 8 TB/s on the read
+    bytes (the roofline's basis) and counting the bytes it writes per frame."""
+    ach = batch.total_bytes / ks / 1e9
+    r = {"kernel_ms": round(ks * 1e3, 4), "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4)}
+    if kind in OUT_WIDTH:
+        moved = batch.total_bytes + OUT_WIDTH[kind] * batch.count
+        r["frac_counting_writes"] = round(moved / ks / 1e9 / HBM_PEAK_GBS, 4)
+    return r
+
+
+def object_clocks(eng, batch, sampler, stream, device):
+    """The clocks a timed object ran at: the sysfs DPM levels / power sampled
+    during its warmup + timed launches, and for the span kernel's batches one
+    stamped launch right after them (nexg_probe_span_clock: the shader clock
+    the workgroups held and their cycles per phase)."""
+    import torch
+    r = {"sysfs": sampler.summary()}
+    if batch.offsets is not None:  # packed / monotone batches: the span kernel
+        try:
+            _, st = eng.probe_span_clock(batch, stream=stream)
+            torch.cuda.synchronize(device)
+            r["span"] = clocks.span_summary(st.cpu().numpy())
+        except Exception as e:  # reported, never fatal to the measurement
+            r["span"] = {"error": repr(e)}
     return r
 
 
 def parse_object(eng, args, batch, out_kind, stream, device, rank, world, workload, traffic_key,
-                 warmup, steps, cpu_label=None, extra=None):
+                 warmup, steps, cpu_label=None, extra=None, also=()):
     """One parse workload beside the default run, same output kind and timing
     discipline: W untimed launches (+ the warmup floor), K timed, max over
     ranks. Returns the object rank 0 adds to the JSON line (None elsewhere)."""
@@ -300,10 +407,19 @@ def parse_object(eng, args, batch, out_kind, stream, device, rank, world, worklo
     torch.cuda.synchronize(device)
     alg = batch.total_bytes
     wstats = {}
-    elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
-                              steps, warmup, stream, device, stats=wstats)
+    with clocks.Sampler(device.index) as smp:
+        elapsed, kernel_s = timed(lambda: eng.parse(batch, out_kind=out_kind, out=out, stream=stream),
+                                  steps, warmup, stream, device, stats=wstats)
     tp = dist.throughput(n, alg, steps, elapsed, device)
     per_rank = dist.all_ranks(round(kernel_s * 1e3, 4), device)
+    clk = object_clocks(eng, batch, smp, stream, device)
+    per_rank_clock = dist.all_ranks(clk.get("span", {}).get("shader_clock_ghz", {}).get("median", 0.0), device)
+    other = {}
+    for key, kind in also:  # the same batch with other output kinds (same timing discipline)
+        o2 = torch.empty(Engine.out_bytes(kind, n), dtype=torch.uint8, device=device)
+        _, ks = timed(lambda: eng.parse(batch, out_kind=kind, out=o2, stream=stream), steps, warmup, stream, device)
+        other[key] = output_rate(batch, kind, ks)
+        del o2
     share = None
     if extra is not None and extra.pop("shape_share", False):  # share of frames with a shape code
         from nex_amd import abi
@@ -325,8 +441,13 @@ def parse_object(eng, args, batch, out_kind, stream, device, rank, world, worklo
         r["sparse_shape_share"] = share
     if extra:
         r.update(extra)
+    r["clocks"] = clk
+    if other:
+        r["other_outputs"] = other
     if world > 1:
         r["per_rank_kernel_ms"] = per_rank
+        if "span" in clk:
+            r["per_rank_shader_clock_ghz"] = per_rank_clock
     if cpu_label and world == 1 and not args.no_cpu_baseline:
         try:
             r["cpu_baseline"] = cpu_baseline(batch, cpu_label, 1 << 20, args.cpu_seconds / 2, host_threads())
@@ -364,7 +485,8 @@ def malformed_line(eng, args, F, first, out_kind, stream, device, rank, world):
     return parse_object(eng, args, batch, out_kind, stream, device, rank, world,
                         f"SURVEY App. C malformed mix: {batch.count} frames per GPU ({distinct} distinct, tiled), "
                         f"IMIX with half the frames mutated {counts}; " + OUT_NOTE[args.out], "malformed",
-                        max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2), extra={"shape_share": True})
+                        max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2), cpu_label="malformed",
+                        extra={"shape_share": True})
 
 
 def real_traffic_batch(eng, F, first):
@@ -383,9 +505,13 @@ def real_traffic_line(eng, args, F, first, out_kind, stream, device, rank, world
     """IMIX with the TCP option lists real segments carry (VERDICT r03
     missing 3), same output kind and timing as the IMIX object."""
     batch, desc = real_traffic_batch(eng, F, first)
+    from nex_amd import abi
+    # the per-frame descriptors a parse_frame / dump caller reads (examples/dump.rs:96-224)
+    # on the shape where the grouped output degenerates to per-frame codes
     return parse_object(eng, args, batch, out_kind, stream, device, rank, world, desc + OUT_NOTE[args.out],
                         "real_traffic", max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2),
-                        cpu_label="real_traffic", extra={"shape_share": True})
+                        cpu_label="real_traffic", extra={"shape_share": True},
+                        also=(("desc_output", abi.OUT_DESC),) if out_kind != abi.OUT_DESC else ())
 
 
 LARGE_FRAMES = 52 << 20  # 3.25 GiB of 64-B frames: 13x the 256-MiB Infinity Cache
@@ -547,8 +673,11 @@ def main():
 
     warm = max(args.warmup, IMIX_WARMUP) if args.workload in ("imix", "imix_pcap", "malformed", "real_traffic") and not args.e2e else args.warmup  # see imix_line
     wstats = {}
-    elapsed, kernel_s, local_s = timed(step, args.steps, warm, stream, device, host_clock=args.e2e, with_local=True,
-                                       stats=wstats)
+    with clocks.Sampler(device.index) as smp:
+        elapsed, kernel_s, local_s = timed(step, args.steps, warm, stream, device, host_clock=args.e2e,
+                                           with_local=True, stats=wstats)
+    head_clocks = object_clocks(eng, batch, smp, stream, device) if batch is not None and not args.e2e \
+        else {"sysfs": smp.summary()}
     tp = dist.throughput(F, alg_bytes, args.steps, elapsed, device)
     # each rank's kernel time and its own timed-region wall time (balance across GPUs)
     per_rank = {"kernel_ms": dist.all_ranks(round(kernel_s * 1e3, 4), device),
@@ -630,6 +759,7 @@ def main():
         res["roofline"]["stream_ceilings"] = dict(
             ceilings, frac_of_read_only=round(achieved / ceilings["read_only_gbs"], 4),
             frac_of_read64_write8=round(achieved / ceilings["read64_write8_gbs"], 4))
+    res["clocks"] = head_clocks
     if world > 1:
         res["per_rank"] = per_rank
     if imix is not None:

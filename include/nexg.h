@@ -508,6 +508,21 @@ int nexg_decode_options(nexg_ctx* ctx, const nexg_frames* frames, const nexg_rec
 int nexg_probe_stream(nexg_ctx* ctx, const void* data, uint64_t bytes, uint32_t out_per_64,
                       void* out, void* stream);
 
+/* Calibration (not a reference entry point): the clock a parse of this batch
+ * runs at. Runs the span kernel that nexg_parse_batch runs for the batch
+ * (packed layouts and monotone capture records; NEXG_EINVAL for any other
+ * layout) with NEXG_OUT_GROUPED into `out` (NEXG_GROUPED_BYTES(count),
+ * 16-B aligned: the same bytes nexg_parse_batch writes), in an
+ * instance that also stores 8 u64 per 256-frame workgroup into `stamps`
+ * (device, ceil(count / 256) * 8 entries, 8-B aligned): s_memtime (shader
+ * clock ticks of the workgroup's XCD) at [0] entry, [1] after the span check,
+ * [2] after the sub-tile loop, [3] after the fast path, [4] after the generic
+ * section, [5] exit; s_memrealtime (100 MHz) at [6] entry and [7] exit. A
+ * workgroup's clock is ([5] - [0]) / ([7] - [6]) x 100 MHz. The product
+ * kernels contain no stamp. */
+int nexg_probe_span_clock(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
+                          void* out, uint64_t* stamps, void* stream);
+
 /* ---- serialize path (udp_ping.rs:68-109 shape) -------------------------- */
 typedef struct nexg_udp4_build {
     const uint32_t* src_ip;   /* per frame, IPv4 address as BE u32 value, or
@@ -572,12 +587,17 @@ typedef struct nexg_udp6_build {
     uint8_t def_src_mac[6], def_dst_mac[6];
     uint8_t hop_limit;        /* Ipv6PacketBuilder default 64 (builder/ipv6.rs:33) */
     uint8_t traffic_class;    /* builder default 0                            */
-    uint8_t reserved[2];
+    uint8_t src_shared;       /* 1: src_ip holds ONE address, the source of every
+                                 frame (udp_ping's probe batch: one interface
+                                 address, a destination per frame)            */
+    uint8_t reserved;
     uint64_t count;
 } nexg_udp6_build;
 
 /* Writes frame i (62 + payload_len bytes) at out + i*out_stride.
- * NEXG_ERANGE if 8 + payload_len > 65535 (builder/udp.rs:83, builder/ipv6.rs:137). */
+ * NEXG_ERANGE if 8 + payload_len > 65535 (builder/udp.rs:83, builder/ipv6.rs:137).
+ * With src_shared and every other per-frame array NULL (the probe batch) the
+ * kernel reads 16 B per frame (dst_ip) and nothing else. */
 int nexg_build_udp6_batch(nexg_ctx* ctx, const nexg_udp6_build* params,
                           uint8_t* out, uint32_t out_stride, void* stream);
 
@@ -598,7 +618,11 @@ typedef struct nexg_ip_build {
     uint8_t ttl;              /* IPv4 TTL / IPv6 hop limit (builders default 64) */
     uint8_t ip_flags;         /* IPv4 3-bit flags (tcp_ping/icmp_ping: DontFragment 0b010) */
     uint8_t tos;              /* IPv4 dscp<<2|ecn / IPv6 traffic class */
-    uint8_t reserved[3];
+    uint8_t src_shared;       /* 1: src_ip holds ONE address (4 or 16 B), the source of
+                                 every frame: the probe batches of tcp_ping / icmp_ping
+                                 (tcp_ping.rs:108-163, icmp_ping.rs:67-120: one interface
+                                 address, a destination per target) */
+    uint8_t reserved[2];
 } nexg_ip_build;
 
 /* TcpPacketBuilder::build (builder/tcp.rs:93-158; tcp.rs:521-575 to_bytes:
@@ -640,7 +664,11 @@ typedef struct nexg_icmp_echo_build {
 } nexg_icmp_echo_build;
 
 /* NEXG_ERANGE on BuildError::LengthOverflow (padded options > 40; segment >
- * 65515 (IPv4) / 65535 (IPv6); ICMP > 65515 / 65535). */
+ * 65515 (IPv4) / 65535 (IPv6); ICMP > 65515 / 65535). Probe batches: with
+ * ip.src_shared set and every other per-frame array NULL (ports, seq / ack,
+ * identifier / sequence, ip_id, MACs) the kernels read only dst_ip per frame
+ * (4 / 16 B), as the tcp_ping / icmp_ping probes of one host vary only the
+ * target. */
 int nexg_build_tcp_batch(nexg_ctx* ctx, const nexg_tcp_build* params, uint8_t* out,
                          uint32_t out_stride, void* stream);
 int nexg_build_icmp_echo_batch(nexg_ctx* ctx, const nexg_icmp_echo_build* params,

@@ -277,7 +277,8 @@ class Udp6Build(ctypes.Structure):
         ("def_dst_mac", ctypes.c_uint8 * 6),
         ("hop_limit", ctypes.c_uint8),
         ("traffic_class", ctypes.c_uint8),
-        ("reserved", ctypes.c_uint8 * 2),
+        ("src_shared", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8),
         ("count", ctypes.c_uint64),
     ]
 
@@ -290,7 +291,7 @@ class IpBuild(ctypes.Structure):
         ("family", ctypes.c_uint32), ("flow_label", ctypes.c_uint32), ("def_ip_id", ctypes.c_uint16),
         ("def_src_mac", ctypes.c_uint8 * 6), ("def_dst_mac", ctypes.c_uint8 * 6),
         ("ttl", ctypes.c_uint8), ("ip_flags", ctypes.c_uint8), ("tos", ctypes.c_uint8),
-        ("reserved", ctypes.c_uint8 * 3),
+        ("src_shared", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 2),
     ]
 
 
@@ -351,6 +352,7 @@ HEADER_INLINE = ("nexg_sparse_decode", "nexg_grouped_code")
 EXPORTED_SYMBOLS = (
     "nexg_abi_version", "nexg_strerror", "nexg_ctx_create", "nexg_ctx_destroy",
     "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch", "nexg_decode_options", "nexg_probe_stream",
+    "nexg_probe_span_clock",
     "nexg_sparse_expand", "nexg_grouped_expand", "nexg_recompute_checksums_batch",
     "nexg_rx_config_default", "nexg_rx_open", "nexg_rx_next_batch", "nexg_rx_stats", "nexg_rx_close",
     "nexg_tpacket3_walk", "nexg_tx_open", "nexg_tx_send_batch", "nexg_tx_close",

@@ -669,9 +669,12 @@ NEXG_HD bool fast_udp4_64(const uint32_t (&w)[16], uint32_t opt_flags, nexg_reco
 // TCP header that does not parse (transport layer only, Q14), and IP lengths
 // that end the layer before the frame end (Ethernet padding) or past it
 // (clamped unless strict). w0[k] holds bytes 4k..4k+3 of the frame
-// (little-endian); bytes past `len` may hold anything (every sum and field
-// below reads only bytes the checks before it placed inside the frame, and
-// the window is masked to the IP end, which is at most `len`); tail_sum is the frame-relative
+// (little-endian). The window is NOT masked: bytes past `len` (in the span
+// kernel the next frame's bytes) reach every read, so no header field may be
+// read without an earlier n / data-offset / IP-length check that places it
+// before the IP end e (<= len), and the payload sums subtract the window's
+// bytes [e, 80) instead of masking them (the host harness poisons the bytes
+// past `len` to keep this honest); tail_sum is the frame-relative
 // little-endian halfword sum of bytes [80, tail_end) (even frame offsets weigh
 // 1, odd 256; 0 when tail_end <= 80) or any value congruent to it mod 0xFFFF
 // that is 0 only when it is (callers holding an absolute-parity sum of a frame

@@ -265,6 +265,25 @@ int nexg_probe_stream(nexg_ctx* ctx, const void* data, uint64_t bytes, uint32_t 
                       NEXG_ELAUNCH);
 }
 
+int nexg_probe_span_clock(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option, void* out,
+                          uint64_t* stamps, void* stream) {
+    if (!ctx) return NEXG_EINVAL;
+    if (!frames_valid(frames)) return fail(ctx, NEXG_EINVAL, "invalid frame batch%s", nullptr);
+    if (frames->count && (!out || !stamps)) return fail(ctx, NEXG_EINVAL, "NULL output or stamps%s", nullptr);
+    if (((reinterpret_cast<uint64_t>(out) & 15u) | (reinterpret_cast<uint64_t>(stamps) & 7u)) != 0)
+        return fail(ctx, NEXG_EINVAL, "misaligned output or stamps%s", nullptr);
+    DeviceGuard g(ctx);
+    nexg::ParseArgs a = to_args(frames);
+    a.opt_flags = option ? option->flags : 0u;
+    a.ip_offset = option ? option->ip_offset : 0u;
+    a.out = out;
+    a.tile_order = nexg::tile_order_for(a);
+    a.stamps = stamps;
+    if (nexg::choose_parse_variant(a) != nexg::ParseVariant::SpanTile)
+        return fail(ctx, NEXG_EINVAL, "probe_span_clock: the batch does not take the span kernel%s", nullptr);
+    return hip_status(ctx, nexg::launch_span_clock(a, static_cast<hipStream_t>(stream)), NEXG_ELAUNCH);
+}
+
 int nexg_build_udp4_batch(nexg_ctx* ctx, const nexg_udp4_build* p, uint8_t* out,
                           uint32_t out_stride, void* stream) {
     if (!ctx || !p) return NEXG_EINVAL;

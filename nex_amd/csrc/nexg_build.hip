@@ -65,7 +65,9 @@ constexpr uint32_t kBuildCapPad = 160u * 1024u / 5u - (kBuildTile * 64u + 16u) -
 uint32_t build_lds_pad() {
     static const uint32_t pad = [] {
         const char* e = getenv("NEXG_BUILD_LDS_PAD");
-        return e ? (uint32_t)atoi(e) : kBuildCapPad;
+        if (!e) return kBuildCapPad;
+        const long v = atol(e);  // clamped: a negative or oversized pad fails every build launch
+        return v <= 0 ? 0u : v >= (long)kBuildCapPad ? kBuildCapPad : (uint32_t)v;
     }();
     return pad;
 }
@@ -84,6 +86,42 @@ __device__ __forceinline__ void lds_put_halfwords(uint8_t* smem, uint32_t d0, co
         *reinterpret_cast<uint32_t*>(smem + b32 + 4u * m) = v;
     }
     *reinterpret_cast<uint16_t*>(smem + (al ? d0 + 2u * (NH - 1) : d0)) = (uint16_t)(al ? hw[NH - 1] : hw[0]);
+}
+
+// N (even) halfwords at an even offset e: dword writes, the run shifted by a
+// halfword (one 2-B write at each end) when e = 2 mod 4
+template <int N>
+__device__ __forceinline__ void lds_put_even_run(uint8_t* smem, uint32_t e, const uint32_t (&hw)[N]) {
+    static_assert(N % 2 == 0, "even halfword count");
+    if ((e & 2u) == 0) {
+#pragma unroll
+        for (int m = 0; m < N / 2; m++)
+            *reinterpret_cast<uint32_t*>(smem + e + 4u * m) = hw[2 * m] | (hw[2 * m + 1] << 16);
+    } else {
+        *reinterpret_cast<uint16_t*>(smem + e) = (uint16_t)hw[0];
+#pragma unroll
+        for (int m = 0; m < N / 2 - 1; m++)
+            *reinterpret_cast<uint32_t*>(smem + e + 2u + 4u * m) = hw[2 * m + 1] | (hw[2 * m + 2] << 16);
+        *reinterpret_cast<uint16_t*>(smem + e + 2u * (N - 1)) = (uint16_t)hw[N - 1];
+    }
+}
+
+// NH (odd) halfwords of frame bytes at any LDS offset d0. Even d0:
+// lds_put_halfwords. Odd d0 (odd frame strides): the first byte alone, the
+// next 2 NH - 2 bytes re-paired into halfwords at the even offset d0 + 1
+// (dword writes), the last byte alone — instead of 2 NH byte writes.
+template <int NH>
+__device__ __forceinline__ void lds_put_frame_hw(uint8_t* smem, uint32_t d0, const uint32_t (&hw)[NH]) {
+    if ((d0 & 1u) == 0) {
+        lds_put_halfwords<NH>(smem, d0, hw);
+        return;
+    }
+    uint32_t sh[NH - 1];
+#pragma unroll
+    for (int k = 0; k < NH - 1; k++) sh[k] = (hw[k] >> 8) | ((hw[k + 1] & 0xFFu) << 8);
+    smem[d0] = (uint8_t)hw[0];
+    lds_put_even_run<NH - 1>(smem, d0 + 1u, sh);
+    smem[d0 + 2u * NH - 1u] = (uint8_t)(hw[NH - 1] >> 8);
 }
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }
@@ -132,7 +170,8 @@ __device__ __forceinline__ uint32_t shared_payload_sum(const uint8_t* pl, uint32
 // PROBE: the udp_ping probe batch (udp_ping.rs:30-31, 68-109 per target): only
 // dst_ip is per frame; source address, ports, id and MACs are the batch's.
 // AOS: the per-frame tuple as one 16-B record (nexg_udp4_tuple), read with one
-// non-temporal dwordx4 load per lane instead of five SoA loads.
+// plain dwordx4 load per lane instead of five SoA loads (NEXG_AOS_NT=1 builds
+// the non-temporal load for A/B: 0.150 vs 0.136 ms, profiles/r04/ab/).
 template <uint32_t MAXS, bool FULL = false, bool PROBE = false, bool AOS = false>
 __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     constexpr bool STAGED = MAXS != 0;
@@ -189,15 +228,10 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
         if (STAGED) {
             const uint32_t d0 = tid * a.out_stride;
             uint8_t* d = smem + d0;
-            if ((a.out_stride & 1u) == 0) {  // even stride: frame starts are 2-B aligned
-                uint32_t hw[21];
+            uint32_t hw[21];
 #pragma unroll
-                for (int k = 0; k < 21; k++) hw[k] = (uint32_t)h[2 * k] | ((uint32_t)h[2 * k + 1] << 8);
-                lds_put_halfwords<21>(smem, d0, hw);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 42; k++) d[k] = h[k];
-            }
+            for (int k = 0; k < 21; k++) hw[k] = (uint32_t)h[2 * k] | ((uint32_t)h[2 * k + 1] << 8);
+            lds_put_frame_hw<21>(smem, d0, hw);  // dword writes at either parity of d0
             for (uint32_t k = 0; k < p.payload_len; k++) d[42 + k] = p.payload[k];
             for (uint32_t k = flen; k < a.out_stride; k++) d[k] = 0;
         } else {
@@ -223,7 +257,10 @@ struct Build6Args {
     uint32_t tile_order;  // tile_index order (nexg_internal.hpp), as k_build_udp4
 };
 
-template <uint32_t MAXS>
+// PROBE: udp_ping's IPv6 probe batch: src_ip holds one address (src_shared),
+// dst_ip one per frame, ports and MACs from the batch defaults: 16 B read per
+// frame.
+template <uint32_t MAXS, bool PROBE = false>
 __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
     constexpr bool STAGED = MAXS != 0;
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
@@ -237,13 +274,15 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
     __shared__ uint32_t s_pay;
     const uint64_t pw = shared_payload_sum(p.payload, p.payload_len, &s_pay);
     if (tid < nf) {
-        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(p.src_ip + 16u * i);
-        const uint32_t* d4 = reinterpret_cast<const uint32_t*>(p.dst_ip + 16u * i);
+        const uint64_t si = PROBE || p.src_shared ? 0u : i;  // one source for the whole batch
+        // addresses are 4-B aligned (the ABI checks): dword loads
+        const auto* s4 = NEXG_GLOBAL(uint32_t, p.src_ip + 16u * si);
+        const auto* d4 = NEXG_GLOBAL(uint32_t, p.dst_ip + 16u * i);
         uint32_t sw[4], dw[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) { sw[k] = s4[k]; dw[k] = d4[k]; }
-        const uint32_t sp = per_or_def(p.src_port, i, p.def_src_port);
-        const uint32_t dp = per_or_def(p.dst_port, i, p.def_dst_port);
+        const uint32_t sp = PROBE ? p.def_src_port : per_or_def(p.src_port, i, p.def_src_port);
+        const uint32_t dp = PROBE ? p.def_dst_port : per_or_def(p.dst_port, i, p.def_dst_port);
         const uint32_t ulen = 8u + p.payload_len;
         // util.rs:111-133 pseudo-header: address segments (as LE halves x 256),
         // next header 17, length; then sport, dport, length, payload (skipword 3)
@@ -255,10 +294,12 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
         uint32_t hw[31];
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-            const uint32_t b0 = per_or_def(p.dst_mac, i * 6 + 2 * k, p.def_dst_mac[2 * k]);
-            const uint32_t b1 = per_or_def(p.dst_mac, i * 6 + 2 * k + 1, p.def_dst_mac[2 * k + 1]);
-            const uint32_t c0 = per_or_def(p.src_mac, i * 6 + 2 * k, p.def_src_mac[2 * k]);
-            const uint32_t c1 = per_or_def(p.src_mac, i * 6 + 2 * k + 1, p.def_src_mac[2 * k + 1]);
+            const uint8_t* dm = PROBE ? nullptr : p.dst_mac;
+            const uint8_t* sm = PROBE ? nullptr : p.src_mac;
+            const uint32_t b0 = per_or_def(dm, i * 6 + 2 * k, p.def_dst_mac[2 * k]);
+            const uint32_t b1 = per_or_def(dm, i * 6 + 2 * k + 1, p.def_dst_mac[2 * k + 1]);
+            const uint32_t c0 = per_or_def(sm, i * 6 + 2 * k, p.def_src_mac[2 * k]);
+            const uint32_t c1 = per_or_def(sm, i * 6 + 2 * k + 1, p.def_src_mac[2 * k + 1]);
             hw[k] = b0 | (b1 << 8);
             hw[3 + k] = c0 | (c1 << 8);
         }
@@ -279,12 +320,7 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
         if (STAGED) {
             const uint32_t d0 = tid * a.out_stride;
             uint8_t* d = smem + d0;
-            if ((a.out_stride & 1u) == 0) {
-                lds_put_halfwords<31>(smem, d0, hw);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 31; k++) { d[2 * k] = (uint8_t)hw[k]; d[2 * k + 1] = (uint8_t)(hw[k] >> 8); }
-            }
+            lds_put_frame_hw<31>(smem, d0, hw);
             for (uint32_t k = 0; k < p.payload_len; k++) d[62 + k] = p.payload[k];
             for (uint32_t k = flen; k < a.out_stride; k++) d[k] = 0;
         } else {
@@ -345,7 +381,10 @@ __device__ __forceinline__ void put_hw(uint8_t* base, uint32_t p, uint32_t v, bo
     }
 }
 
-template <int FAM, int KIND, uint32_t MAXS>
+// PROBE: a tcp_ping / icmp_ping probe batch (ip.src_shared, every other
+// per-frame array NULL): only the destination is read per frame (4 / 16 B);
+// source, ports, seq / ack, identifier / sequence, id and MACs are the batch's.
+template <int FAM, int KIND, uint32_t MAXS, bool PROBE = false>
 __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
     constexpr bool STAGED = MAXS != 0;
     constexpr int NIP = FAM == 4 ? 10 : 20;             // IP header halfwords
@@ -365,11 +404,13 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
     const uint32_t flen = 14u + 2u * NIP + l4_len;
     if (tid < nf) {
         const nexg_ip_build& ip = a.ip;
-        uint32_t sw[FAM == 4 ? 1 : 4], dw[FAM == 4 ? 1 : 4];
+        constexpr uint32_t AW = FAM == 4 ? 1u : 4u;  // address dwords
+        const uint64_t si = PROBE || ip.src_shared ? 0u : i;  // one source for the whole batch
+        uint32_t sw[AW], dw[AW];
 #pragma unroll
-        for (int k = 0; k < (FAM == 4 ? 1 : 4); k++) {
-            sw[k] = reinterpret_cast<const uint32_t*>(ip.src_ip + (FAM == 4 ? 4u : 16u) * i)[k];
-            dw[k] = reinterpret_cast<const uint32_t*>(ip.dst_ip + (FAM == 4 ? 4u : 16u) * i)[k];
+        for (uint32_t k = 0; k < AW; k++) {
+            sw[k] = NEXG_GLOBAL(uint32_t, ip.src_ip)[AW * si + k];
+            dw[k] = NEXG_GLOBAL(uint32_t, ip.dst_ip)[AW * i + k];
         }
         uint32_t addr_le = 0;  // address words as LE halves: x256 gives the BE sum (mod 0xFFFF)
 #pragma unroll
@@ -377,10 +418,12 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
         uint32_t hw[NH];
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-            const uint32_t b0 = per_or_def(ip.dst_mac, i * 6 + 2 * k, ip.def_dst_mac[2 * k]);
-            const uint32_t b1 = per_or_def(ip.dst_mac, i * 6 + 2 * k + 1, ip.def_dst_mac[2 * k + 1]);
-            const uint32_t c0 = per_or_def(ip.src_mac, i * 6 + 2 * k, ip.def_src_mac[2 * k]);
-            const uint32_t c1 = per_or_def(ip.src_mac, i * 6 + 2 * k + 1, ip.def_src_mac[2 * k + 1]);
+            const uint8_t* dm = PROBE ? nullptr : ip.dst_mac;
+            const uint8_t* sm = PROBE ? nullptr : ip.src_mac;
+            const uint32_t b0 = per_or_def(dm, i * 6 + 2 * k, ip.def_dst_mac[2 * k]);
+            const uint32_t b1 = per_or_def(dm, i * 6 + 2 * k + 1, ip.def_dst_mac[2 * k + 1]);
+            const uint32_t c0 = per_or_def(sm, i * 6 + 2 * k, ip.def_src_mac[2 * k]);
+            const uint32_t c1 = per_or_def(sm, i * 6 + 2 * k + 1, ip.def_src_mac[2 * k + 1]);
             hw[k] = b0 | (b1 << 8);
             hw[3 + k] = c0 | (c1 << 8);
         }
@@ -389,10 +432,10 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
         uint64_t t;
         constexpr int L = 7 + NIP;  // first L4 halfword
         if (KIND == kL4Tcp) {
-            const uint32_t sp = per_or_def(a.sport, i, a.def_sport);
-            const uint32_t dp = per_or_def(a.dport, i, a.def_dport);
-            const uint32_t sq = per_or_def(a.seq, i, a.def_seq);
-            const uint32_t ak = per_or_def(a.ack, i, a.def_ack);
+            const uint32_t sp = PROBE ? a.def_sport : per_or_def(a.sport, i, a.def_sport);
+            const uint32_t dp = PROBE ? a.def_dport : per_or_def(a.dport, i, a.def_dport);
+            const uint32_t sq = PROBE ? a.def_seq : per_or_def(a.seq, i, a.def_seq);
+            const uint32_t ak = PROBE ? a.def_ack : per_or_def(a.ack, i, a.def_ack);
             const uint32_t w6 = ((l4_hdr / 4u) << 12) | (a.flags & 0xFFu);
             t = sp + dp + (sq >> 16) + (sq & 0xFFFFu) + (ak >> 16) + (ak & 0xFFFFu) + w6 + a.window + a.urg +
                 a.opt_sum + pay_sum;
@@ -402,8 +445,8 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
             hw[L + 6] = bswap16(w6); hw[L + 7] = bswap16(a.window);
             hw[L + 9] = bswap16(a.urg);
         } else {
-            const uint32_t id = per_or_def(a.ident, i, a.def_ident);
-            const uint32_t sq = per_or_def(a.seqno, i, a.def_seqno);
+            const uint32_t id = PROBE ? a.def_ident : per_or_def(a.ident, i, a.def_ident);
+            const uint32_t sq = PROBE ? a.def_seqno : per_or_def(a.seqno, i, a.def_seqno);
             const uint32_t w0 = (a.icmp_type << 8) | a.icmp_code;
             t = w0 + id + sq + pay_sum;
             hw[L + 0] = bswap16(w0);
@@ -414,7 +457,7 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
         hw[KIND == kL4Tcp ? L + 8 : L + 1] = bswap16(cs);
         // ---- IP header ----
         if (FAM == 4) {
-            const uint32_t total = 20u + l4_len, id = per_or_def(ip.ip_id, i, ip.def_ip_id);
+            const uint32_t total = 20u + l4_len, id = PROBE ? ip.def_ip_id : per_or_def(ip.ip_id, i, ip.def_ip_id);
             const uint32_t w0 = (0x45u << 8) | ip.tos, w3 = ((uint32_t)(ip.ip_flags & 7u)) << 13;
             const uint32_t w4 = ((uint32_t)ip.ttl << 8) | proto;
             const uint32_t ics = fold_complement(256ull * addr_le + w0 + total + id + w3 + w4);
@@ -439,8 +482,8 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
         uint8_t* base = STAGED ? smem : a.out + first * a.out_stride;
         const uint32_t d0 = tid * a.out_stride;
         const bool odd = (a.out_stride & 1u) != 0;
-        if (STAGED && !odd) {
-            lds_put_halfwords<NH>(base, d0, hw);  // dword writes (NH odd): half the LDS stores
+        if (STAGED) {
+            lds_put_frame_hw<NH>(base, d0, hw);  // dword writes at either parity
         } else {
 #pragma unroll
             for (int k = 0; k < NH; k++) put_hw(base, d0 + 2u * k, hw[k], odd);
@@ -465,35 +508,44 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
     }
 }
 
-template <int FAM, int KIND>
-static void launch_l4_fam(const L4Args& a, uint32_t flen, hipStream_t s) {
+template <int FAM, int KIND, bool PROBE>
+static void launch_l4_form(const L4Args& a, hipStream_t s) {
     const uint64_t blocks = (a.count + kBuildTile - 1) / kBuildTile;
     const bool staged = a.out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(a.out) & 15u) == 0;
-    (void)flen;
     // IPv6: 16-KiB tile + build_lds_pad() -> 5 workgroups per CU (icmp6 echo
     // 0.29 -> 0.26 ms at 16M frames); IPv4 shapes run faster at 8 per CU (tcp
     // SYN 0.21 vs 0.24-0.26 ms, icmp echo 0.132 vs 0.140; profiles/r04/builders/)
-    const uint32_t pad = FAM == 6 ? build_lds_pad() : 0u;
+    const uint32_t pad = FAM == 6 || PROBE ? build_lds_pad() : 0u;
     if (staged && a.out_stride <= 64u)
-        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 64>), dim3((uint32_t)blocks), dim3(kBuildTile), pad, s, a);
+        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 64, PROBE>), dim3((uint32_t)blocks), dim3(kBuildTile), pad, s, a);
     else if (staged && a.out_stride <= 80u)  // tcp_ping's 66 B: a 20-KiB tile (7 per CU) instead of 32 KiB (4)
-        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 80>), dim3((uint32_t)blocks), dim3(kBuildTile),
-                           FAM == 6 && pad ? pad - 4096u : 0u, s, a);
+        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 80, PROBE>), dim3((uint32_t)blocks), dim3(kBuildTile),
+                           pad > 4096u ? pad - 4096u : 0u, s, a);
     else if (staged)
-        hipLaunchKernelGGL((k_build_l4<FAM, KIND, kBuildMaxStride>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+        hipLaunchKernelGGL((k_build_l4<FAM, KIND, kBuildMaxStride, PROBE>), dim3((uint32_t)blocks), dim3(kBuildTile),
+                           0, s, a);
     else
-        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 0>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
+        hipLaunchKernelGGL((k_build_l4<FAM, KIND, 0, PROBE>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
 }
 
-static hipError_t launch_l4(L4Args& a, int kind, uint32_t flen, hipStream_t s) {
+template <int FAM, int KIND>
+static void launch_l4_fam(const L4Args& a, hipStream_t s) {
+    // the probe batch: one source, a destination per frame, nothing else per frame
+    const bool probe = a.ip.src_shared && !a.ip.ip_id && !a.ip.src_mac && !a.ip.dst_mac &&
+                       (KIND == kL4Tcp ? !a.sport && !a.dport && !a.seq && !a.ack : !a.ident && !a.seqno);
+    if (probe) launch_l4_form<FAM, KIND, true>(a, s);
+    else launch_l4_form<FAM, KIND, false>(a, s);
+}
+
+static hipError_t launch_l4(L4Args& a, int kind, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     a.tile_order = l4_build_tile_order();
     if (kind == kL4Tcp) {
-        if (a.ip.family == 4) launch_l4_fam<4, kL4Tcp>(a, flen, s);
-        else launch_l4_fam<6, kL4Tcp>(a, flen, s);
+        if (a.ip.family == 4) launch_l4_fam<4, kL4Tcp>(a, s);
+        else launch_l4_fam<6, kL4Tcp>(a, s);
     } else {
-        if (a.ip.family == 4) launch_l4_fam<4, kL4Icmp>(a, flen, s);
-        else launch_l4_fam<6, kL4Icmp>(a, flen, s);
+        if (a.ip.family == 4) launch_l4_fam<4, kL4Icmp>(a, s);
+        else launch_l4_fam<6, kL4Icmp>(a, s);
     }
     return hipGetLastError();
 }
@@ -509,7 +561,7 @@ hipError_t launch_build_tcp(const nexg_tcp_build& p, uint8_t* out, uint32_t out_
     for (uint32_t k = 0; k < a.opt_padded; k += 2) a.opt_sum += ((uint32_t)a.options[k] << 8) | a.options[k + 1];
     a.payload = p.payload; a.payload_len = p.payload_len; a.count = p.count;
     a.out = out; a.out_stride = out_stride;
-    return launch_l4(a, kL4Tcp, 0, s);
+    return launch_l4(a, kL4Tcp, s);
 }
 
 hipError_t launch_build_icmp_echo(const nexg_icmp_echo_build& p, uint8_t* out, uint32_t out_stride,
@@ -520,7 +572,7 @@ hipError_t launch_build_icmp_echo(const nexg_icmp_echo_build& p, uint8_t* out, u
     a.icmp_type = p.icmp_type; a.icmp_code = p.icmp_code;
     a.payload = p.payload; a.payload_len = p.payload_len; a.count = p.count;
     a.out = out; a.out_stride = out_stride;
-    return launch_l4(a, kL4Icmp, 0, s);
+    return launch_l4(a, kL4Icmp, s);
 }
 
 // ---- arp / ndp probes ------------------------------------------------------
@@ -876,9 +928,12 @@ hipError_t launch_build_udp6(const nexg_udp6_build& p, uint8_t* out, uint32_t ou
     Build6Args a{p, out, out_stride, l4_build_tile_order()};
     const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
-    // a 16-KiB tile for the udp_ping shapes keeps ~10 workgroups per CU
-    if (staged && out_stride <= 64u)
-        hipLaunchKernelGGL(k_build_udp6<64>, dim3((uint32_t)blocks), dim3(kBuildTile), build_lds_pad(), s, a);  // 0.279 -> 0.253 ms
+    const bool probe = p.src_shared && !p.src_port && !p.dst_port && !p.src_mac && !p.dst_mac;
+    // a 16-KiB tile for the udp_ping shapes + build_lds_pad(): 5 workgroups per CU (0.279 -> 0.253 ms)
+    if (staged && out_stride <= 64u && probe)
+        hipLaunchKernelGGL((k_build_udp6<64, true>), dim3((uint32_t)blocks), dim3(kBuildTile), build_lds_pad(), s, a);
+    else if (staged && out_stride <= 64u)
+        hipLaunchKernelGGL(k_build_udp6<64>, dim3((uint32_t)blocks), dim3(kBuildTile), build_lds_pad(), s, a);
     else if (staged)
         hipLaunchKernelGGL(k_build_udp6<kBuildMaxStride>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
     else

@@ -23,6 +23,7 @@ struct ParseArgs {
     uint32_t hints = 0;       // NEXG_FRAMES_* (include/nexg.h)
     uint32_t* tail = nullptr; // TwoPass tail-sum hand-off (count entries) for outputs
                               // narrower than 4 B per frame; null -> the output itself
+    uint64_t* stamps = nullptr;  // k_parse_span<..., TIMING>: 8 clock stamps per workgroup
 };
 
 // Kernel variants of the parse path.
@@ -35,6 +36,8 @@ enum class ParseVariant {
 };
 
 hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStream_t s);
+// nexg_probe_span_clock: the span kernel's stamped instance (grouped output)
+hipError_t launch_span_clock(const ParseArgs& a, hipStream_t s);
 // TwoPass hands each frame's tail sum to pass 2 through its own output
 // element; outputs narrower than 4 B need a.tail (count u32) instead.
 inline bool parse_needs_tail(ParseVariant v, int out_kind) {

@@ -127,6 +127,14 @@ static hipError_t launch_slice(ParseVariant v, const ParseArgs& a, hipStream_t s
     return hipGetLastError();
 }
 
+hipError_t launch_span_clock(const ParseArgs& a, hipStream_t s) {
+    if (a.count == 0) return hipSuccess;
+    const uint64_t blocks = (a.count + kTile - 1) / kTile;
+    hipLaunchKernelGGL((k_parse_span<NEXG_OUT_GROUPED, 1, NEXG_SPAN_SUB, NEXG_SPAN_WPE, true>), dim3((uint32_t)blocks),
+                       dim3(kTile), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     if (out_kind == NEXG_OUT_SLICE) return launch_slice(v, a, s);
@@ -353,12 +361,3 @@ hipError_t launch_checksum(const ParseArgs& a, uint32_t skipword, uint16_t* out,
 
 }  // namespace nexg
 
-#ifdef NEXG_SPAN_TIMING
-// (measurement builds only) copies k_parse_span's per-workgroup timestamps
-// [entry, after the span check, after the sub-tile loop, after the fast path,
-// after the generic section, exit, CU id, -] to the host (s_memtime counts per XCD: compare stamps of one workgroup only)
-extern "C" int nexg_debug_span_times(void* host, uint64_t workgroups) {
-    if (workgroups > nexg::kSpanTimingMax) workgroups = nexg::kSpanTimingMax;
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(nexg::g_span_times), workgroups * 64u, 0, hipMemcpyDeviceToHost);
-}
-#endif

@@ -42,9 +42,10 @@ __device__ __forceinline__ void store_result(void* out, uint64_t idx, const nexg
         const uint32_t st = (r.flags >> NEXG_STATUS_SHIFT) & 7u;
         const uint16_t v = (uint16_t)(st ? (NEXG_VERDICT_ERR | (st << 3)) : (r.flags & 0xFFFFu));
         __builtin_nontemporal_store(v, reinterpret_cast<uint16_t*>(out) + idx);
-    } else if (OUT == NEXG_OUT_DESC) {
-        uint2 d = make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
-        reinterpret_cast<uint2*>(out)[idx] = d;
+    } else if (OUT == NEXG_OUT_DESC) {  // non-temporal, as the flags / verdict streams
+        typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(v2u{r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16)},
+                                    reinterpret_cast<v2u*>(out) + idx);
     } else {
         uint4 v[4];
         __builtin_memcpy(v, &r, sizeof(r));
@@ -130,6 +131,28 @@ __device__ __forceinline__ void copy_out_records(const uint8_t* stage, void* out
     uint4* dst = reinterpret_cast<uint4*>(out) + first * 4u;
     for (uint32_t c = threadIdx.x; c < nf * 4u; c += kTile)
         dst[c] = *reinterpret_cast<const uint4*>(stage + (c >> 2) * PITCH + 16u * (c & 3u));
+}
+
+// NEXG_OUT_DESC output of a tile through LDS: each thread has written its
+// 8-B descriptor at the start of its PITCH-byte slot (call after a barrier);
+// the tile's nf descriptors leave as contiguous 16-B non-temporal stores, two
+// descriptors per thread (threads 0..127), instead of 8-B stores per thread.
+template <uint32_t PITCH>
+__device__ __forceinline__ void copy_out_descs(const uint8_t* stage, void* out, uint64_t first, uint32_t nf) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    const uint32_t c = threadIdx.x, f = 2u * c;
+    if (f >= nf) return;
+    const uint2 d0 = *reinterpret_cast<const uint2*>(stage + f * PITCH);
+    if (f + 1u < nf) {
+        const uint2 d1 = *reinterpret_cast<const uint2*>(stage + (f + 1u) * PITCH);
+        __builtin_nontemporal_store(u32x4{d0.x, d0.y, d1.x, d1.y}, reinterpret_cast<u32x4*>(out) + (first + f) / 2u);
+    } else {
+        __builtin_nontemporal_store(v2u{d0.x, d0.y}, reinterpret_cast<v2u*>(out) + first + f);
+    }
+}
+
+__device__ __forceinline__ void stage_desc(uint8_t* slot, const nexg_record& r) {
+    *reinterpret_cast<uint2*>(slot) = make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
 }
 
 __device__ __forceinline__ void stage_record(uint8_t* slot, const nexg_record& r) {
@@ -219,8 +242,9 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
                 if (k < chunks) *reinterpret_cast<uint4*>(slot + 16u * k) = v[k];
         }
     }
-    // MODE 0 + RECORD: every thread stays for the coalesced copy-out
+    // MODE 0 + RECORD / DESC: every thread stays for the coalesced copy-out
     constexpr bool kStaged = MODE == 0 && OUT == NEXG_OUT_RECORD && PITCH >= 64;
+    constexpr bool kStagedDesc = MODE == 0 && OUT == NEXG_OUT_DESC;
     if constexpr (OUT == NEXG_OUT_SLICE) {  // FrameSlice boundaries from the same staging
         if (tid < nf) {
             nexg_slice sl;
@@ -258,6 +282,7 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
             }
         }
         if (kStaged) stage_record(slot, r);  // own slot: no other thread reads it
+        else if (kStagedDesc) stage_desc(slot, r);
         else if constexpr (!sparse_like(OUT)) store_result<OUT>(a.out, idx, r);
     }
     if constexpr (sparse_like(OUT)) {
@@ -271,6 +296,10 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
     if (kStaged) {
         __syncthreads();
         copy_out_records<PITCH>(smem, a.out, first, nf);
+    }
+    if (kStagedDesc) {
+        __syncthreads();
+        copy_out_descs<PITCH>(smem, a.out, first, nf);
     }
 }
 
@@ -551,23 +580,24 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     return v;
 }
 
-// (measurement builds only) per-workgroup phase timestamps of k_parse_span:
-// -DNEXG_SPAN_TIMING, read back by nexg_debug_span_times (nexg_parse.hip),
-// summarised by tools/span_timing.py
-#ifdef NEXG_SPAN_TIMING
-constexpr uint32_t kSpanTimingMax = 1u << 17;
-__device__ uint64_t g_span_times[kSpanTimingMax * 8];
+// Per-workgroup clock stamps of k_parse_span's calibration instance
+// (TIMING = true, launched only by nexg_probe_span_clock; the product
+// instances compile no stamp): stamps[8 * workgroup + k] = s_memtime (shader
+// clock ticks of the workgroup's XCD) at k = 0 entry, 1 span check, 2 end of
+// the sub-tile loop, 3 end of the fast path, 4 end of the generic section,
+// 5 exit; k = 6 / 7 = s_memrealtime (100 MHz) at entry / exit. The clock a
+// workgroup ran at is (t5 - t0) / (rt7 - rt6) x 100 MHz (MI355X_MICROARCH.md
+// 'DVFS give-back' item 6).
 #define NEXG_SPAN_STAMP(k) \
-    do { if (t == 0 && blockIdx.x < kSpanTimingMax) g_span_times[blockIdx.x * 8u + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define NEXG_SPAN_STAMP(k)
-#endif
+    do { if constexpr (TIMING) { if (t == 0) a.stamps[blockIdx.x * 8ull + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
+#define NEXG_SPAN_RTSTAMP(k) \
+    do { if constexpr (TIMING) { if (t == 0) a.stamps[blockIdx.x * 8ull + (k)] = __builtin_amdgcn_s_memrealtime(); } } while (0)
 
 // NB = 2: sub-tile k stages into buffer k&1, so the barrier that publishes
 // sub-tile k also retires every lookup into sub-tile k-2's buffer (3 barriers
 // per sub-tile, ~42 KB LDS); NB = 1 (the library's): one buffer and a 4th
 // barrier (~25 KB LDS, 6 workgroups per CU).
-template <int OUT, int NB = 1, uint32_t SUB = 16384, int WPE = 1>
+template <int OUT, int NB = 1, uint32_t SUB = 16384, int WPE = 1, bool TIMING = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_parse_span(ParseArgs a) {
     // each stage buffer: [96-B apron | SUB bytes | 96-B pad]; the apron holds
     // the previous sub-tile's last 96 bytes, so a head window that starts
@@ -581,10 +611,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     __shared__ uint64_t s_span[2];
     __shared__ uint32_t s_hist[2 * kBuckets + 1];  // generic-pass bucket counts, bases, total
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    NEXG_SPAN_RTSTAMP(6);
     NEXG_SPAN_STAMP(0);
-#ifdef NEXG_SPAN_TIMING
-    if (t == 0 && blockIdx.x < kSpanTimingMax) g_span_times[blockIdx.x * 8u + 6] = __smid();
-#endif
     const uint64_t f0 = tile_index(a.tile_order) * kTile;
     const uint64_t idx = f0 + t;
     const uint32_t nf = a.count - f0 < kTile ? (uint32_t)(a.count - f0) : kTile;
@@ -630,6 +658,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
         }
         store_out<OUT>(a, idx, have, r);
+        NEXG_SPAN_STAMP(5);
+        NEXG_SPAN_RTSTAMP(7);
         return;
     }
     // span-relative positions: head, tail start (head + 80), end
@@ -844,13 +874,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // budget: with them the App. C mix ran 10 % slower, profiles/r03/grouped)
     NEXG_SPAN_STAMP(4);
     if (sparse_like(OUT)) store_sparse_coded<OUT, false>(a, idx, have, r, code);
-    else if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
+    else if (OUT == NEXG_OUT_DESC) {  // 256 x 8 B through the slots: 16-B non-temporal stores
+        // own slot only (the generic section's reads of other lanes' slots
+        // ended at its last barrier)
+        if (have) stage_desc(slots + SpanFrame::kSlot * t, r);
+        __syncthreads();
+        copy_out_descs<SpanFrame::kSlot>(slots, a.out, f0, nf);
+    } else if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
     if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the slots (pitch 80 B)
         static_assert(kStage >= kTile * SpanFrame::kSlot, "record staging needs 20 KiB");
         __syncthreads();
         copy_out_records<SpanFrame::kSlot>(slots, a.out, f0, nf);
     }
     NEXG_SPAN_STAMP(5);
+    NEXG_SPAN_RTSTAMP(7);
 }
 
 }  // namespace nexg

@@ -271,6 +271,25 @@ class Engine:
         self._check(self.lib.nexg_probe_stream(self.ctx, None, nbytes, 64, _ptr(out), self._stream(stream)))
         return out
 
+    def probe_span_clock(self, batch: FrameBatch, option: ParseOption = ParseOption(),
+                         mode: ParseMode = ParseMode.Lenient, out=None, stream=None):
+        """One stamped launch of the span kernel over `batch`
+        (nexg_probe_span_clock; calibration, not a reference entry point):
+        returns (grouped output, stamps) device tensors, stamps int64
+        (workgroups, 8) as include/nexg.h lays them out; span_clock_summary
+        reduces them on the host."""
+        torch = _torch()
+        nbytes = self.out_bytes(abi.OUT_GROUPED, batch.count)
+        if out is None:
+            out = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=self.torch_device)
+        nwg = max(1, (batch.count + 255) // 256)
+        stamps = torch.zeros((nwg, 8), dtype=torch.int64, device=self.torch_device)
+        fr = batch.to_c()
+        opt = abi.ParseOptionC(option.flags(mode), option.offset)
+        self._check(self.lib.nexg_probe_span_clock(self.ctx, ctypes.byref(fr), ctypes.byref(opt), _ptr(out),
+                                                   _ptr(stamps), self._stream(stream)))
+        return out, stamps
+
     def checksum(self, batch: FrameBatch, skipword: int, stream=None):
         """util::checksum(buf, skipword) per buffer (util.rs:65)."""
         torch = _torch()
@@ -350,15 +369,17 @@ class Engine:
                    stream=None):
         """udp_ping's IPv6 branch (udp_ping.rs:83-89): UdpPacketBuilder ->
         Ipv6PacketBuilder -> EthernetPacketBuilder on every tuple. src_ip /
-        dst_ip are (count, 16) uint8 device tensors in network order."""
+        dst_ip are (count, 16) uint8 device tensors in network order; src_ip
+        may be one address (every frame's source: the probe batch)."""
         torch = _torch()
-        count = src_ip.shape[0] if src_ip.dim() > 1 else src_ip.numel() // 16
+        count = dst_ip.shape[0] if dst_ip.dim() > 1 else dst_ip.numel() // 16
         plen = 0 if payload is None else payload.numel()
         stride = out_stride or (62 + plen)
         if out is None:
             out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
         p = abi.Udp6Build()
         p.src_ip, p.dst_ip = src_ip.data_ptr(), dst_ip.data_ptr()
+        p.src_shared = 1 if src_ip.numel() == 16 and count != 1 else 0
         p.src_port = None if src_port is None else src_port.data_ptr()
         p.dst_port = None if dst_port is None else dst_port.data_ptr()
         p.src_mac = p.dst_mac = None
@@ -376,8 +397,12 @@ class Engine:
     @staticmethod
     def _ip_build(family, src_ip, dst_ip, ip_id, def_ip_id, src_mac, dst_mac, ttl, ip_flags, tos,
                   flow_label):
+        """src_ip: (count, 4|16) per frame, or ONE address ((4|16,) or (1, 4|16)):
+        the probe batches' single source (nexg_ip_build.src_shared)."""
         ip = abi.IpBuild()
         ip.src_ip, ip.dst_ip = src_ip.data_ptr(), dst_ip.data_ptr()
+        w = 4 if family == 4 else 16
+        ip.src_shared = 1 if src_ip.numel() == w and dst_ip.numel() != w else 0
         ip.ip_id = None if ip_id is None else ip_id.data_ptr()
         ip.src_mac = ip.dst_mac = None
         ip.family, ip.flow_label, ip.def_ip_id = family, flow_label, def_ip_id
@@ -393,9 +418,11 @@ class Engine:
                   out_stride=None, out=None, stream=None):
         """tcp_ping (examples/tcp_ping.rs:111-163): TcpPacketBuilder -> IPv4/IPv6
         builder -> EthernetPacketBuilder on every tuple. Addresses are
-        (count, 4|16) uint8 device tensors; ports/ids int16, seq/ack int32."""
+        (count, 4|16) uint8 device tensors (src_ip may be one address: every
+        frame's source); ports/ids int16, seq/ack int32. One source, a
+        destination per frame and no other array is tcp_ping's probe batch."""
         torch = _torch()
-        count = src_ip.shape[0]
+        count = dst_ip.shape[0]
         plen = 0 if payload is None else payload.numel()
         padded = (len(options) + 3) // 4 * 4
         flen = 14 + (20 if family == 4 else 40) + 20 + padded + plen
@@ -425,9 +452,10 @@ class Engine:
                         ip_id=None, def_ip_id=0, src_mac=b"\0" * 6, dst_mac=b"\0" * 6, ttl=64,
                         ip_flags=0, tos=0, flow_label=0, out_stride=None, out=None, stream=None):
         """icmp_ping (examples/icmp_ping.rs:67-102): Icmp(v6)PacketBuilder with
-        echo_fields -> IPv4/IPv6 builder -> EthernetPacketBuilder."""
+        echo_fields -> IPv4/IPv6 builder -> EthernetPacketBuilder. src_ip may
+        be one address (every frame's source: icmp_ping's probe batch)."""
         torch = _torch()
-        count = src_ip.shape[0]
+        count = dst_ip.shape[0]
         plen = 0 if payload is None else payload.numel()
         flen = 14 + (20 if family == 4 else 40) + 8 + plen
         stride = out_stride or flen

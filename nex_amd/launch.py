@@ -57,7 +57,10 @@ def decide(argv, env, gpus: int, n_devices=None, script="bench.py", python=sys.e
         return "error", f"--gpus {gpus}: need at least one rank"
     if in_rank:
         world = int(env["WORLD_SIZE"])
-        if world != gpus:
+        # `torchrun --nproc-per-node 8 bench.py` (no --gpus): the launcher's
+        # world is the rank count; only an explicit --gpus that disagrees is refused
+        explicit = any(a == "--gpus" or a.startswith("--gpus=") for a in argv)
+        if world != gpus and explicit:
             return "error", (f"WORLD_SIZE={world} but --gpus {gpus}: launch one rank per GPU "
                              f"(torch.distributed.run --nproc-per-node {gpus}) or drop the launcher "
                              "and let bench.py start the ranks itself")

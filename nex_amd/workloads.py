@@ -118,7 +118,7 @@ def mutate_packed(data, offs, seed: int = abi.DEFAULT_SEED, mutate_share: float 
             g = f.copy()
             g[l4 + 12] = ((5 + len(o) // 4) << 4) | (g[l4 + 12] & 0x0F)
             k = 16 if eth_v4[j] else 18
-            v = ((int(g[k]) << 8) | int(g[k + 1])) + len(o)
+            v = (((int(g[k]) << 8) | int(g[k + 1])) + len(o)) & 0xFFFF  # u16 field: wraps
             g[k], g[k + 1] = v >> 8, v & 0xFF
             f = np.concatenate([g[:l4 + 20], o, g[l4 + 20:]])
         elif ins[j] == 4:  # 802.1Q tag in front of the EtherType (frame[12:14])
@@ -127,7 +127,7 @@ def mutate_packed(data, offs, seed: int = abi.DEFAULT_SEED, mutate_share: float 
             nh = f[20]
             g = f.copy()
             g[20] = 0
-            pl = ((int(g[18]) << 8) | int(g[19])) + 8
+            pl = (((int(g[18]) << 8) | int(g[19])) + 8) & 0xFFFF  # u16 field: wraps
             g[18], g[19] = pl >> 8, pl & 0xFF
             f = np.concatenate([g[:54], np.array([nh, 0, 0, 0, 0, 0, 0, 0], np.uint8), g[54:]])
         out[new_offs[j]:new_offs[j] + len(f)] = f

@@ -851,6 +851,55 @@ int nexo_build_udp4_batch(const nexo_udp4_tuples* p, uint8_t* out, int nthreads)
     return 0;
 }
 
+/* one build of a probe batch (nexo_probe_batch) with destination i */
+static int probe_one(const nexo_probe_batch* p, uint64_t i, uint8_t* out) {
+    nexo_ip_spec ip = p->ip;
+    const size_t w = ip.family == 4 ? 4 : 16;
+    memcpy(ip.dst, p->dst + w * i, w);
+    if (p->kind == 0)
+        return nexo_build_tcp(&ip, p->sport, p->dport, p->seq, p->ack, p->tcp_flags, p->window, p->urg, p->opts,
+                              p->opt_len, p->payload, p->payload_len, out);
+    if (p->kind == 1)
+        return nexo_build_icmp_echo(&ip, p->icmp_type, p->icmp_code, p->ident, p->seqno, p->payload,
+                                    p->payload_len, out);
+    return nexo_build_udp6(ip.src_mac, ip.dst_mac, ip.src, ip.dst, p->sport, p->dport, ip.ttl, ip.dscp_ecn,
+                           ip.flow_label, p->payload, p->payload_len, out);
+}
+
+typedef struct {
+    const nexo_probe_batch* p;
+    uint8_t* out;
+    int flen;
+    uint64_t begin, end;
+} probe_job;
+
+static void* probe_worker(void* arg) {
+    probe_job* j = (probe_job*)arg;
+    for (uint64_t i = j->begin; i < j->end; i++) probe_one(j->p, i, j->out + (uint64_t)j->flen * i);
+    return NULL;
+}
+
+int nexo_build_probe_batch(const nexo_probe_batch* p, uint8_t* out, int nthreads) {
+    uint8_t first[70000];
+    if (p->count == 0) return 0;
+    const int flen = probe_one(p, 0, first);
+    if (flen < 0) return -1;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    probe_job jobs[256];
+    for (int t = 0; t < nthreads; t++)
+        jobs[t] = (probe_job){p, out, flen, p->count * (uint64_t)t / (uint64_t)nthreads,
+                              p->count * (uint64_t)(t + 1) / (uint64_t)nthreads};
+    if (nthreads == 1) {
+        probe_worker(&jobs[0]);
+        return flen;
+    }
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, probe_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    return flen;
+}
+
 /* ======================= FrameSlice (frame.rs:84-287) =================== */
 
 typedef struct {

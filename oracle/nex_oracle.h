@@ -125,6 +125,27 @@ int nexo_build_udp6(const uint8_t src_mac[6], const uint8_t dst_mac[6],
                     uint32_t flow_label, const uint8_t* payload, uint32_t payload_len,
                     uint8_t* out);
 
+/* A probe batch of one of the udp_ping / tcp_ping / icmp_ping compositions:
+ * every field from `ip` and the L4 fields below, except the destination, which
+ * is dst[i] (4 B for family 4, 16 B for 6); frame i (flen bytes, the return
+ * value of one single build) at out + flen i. kind: 0 tcp (nexo_build_tcp),
+ * 1 icmp echo (nexo_build_icmp_echo), 2 udp over IPv6 (nexo_build_udp6).
+ * Static index-range split over nthreads (the probe builders' CPU baseline).
+ * Returns flen, or -1 (length overflow). */
+typedef struct {
+    int kind;
+    nexo_ip_spec ip;
+    const uint8_t* dst;
+    uint64_t count;
+    uint16_t sport, dport, window, urg;   /* tcp; udp6: sport / dport */
+    uint32_t seq, ack;
+    uint8_t tcp_flags, icmp_type, icmp_code, pad0;
+    uint16_t ident, seqno;                 /* icmp echo */
+    const uint8_t* opts; uint32_t opt_len;
+    const uint8_t* payload; uint32_t payload_len;
+} nexo_probe_batch;
+int nexo_build_probe_batch(const nexo_probe_batch* p, uint8_t* out, int nthreads);
+
 /* nexg_recompute_checksums_batch's semantics for one frame, in place: the
  * mutable views' recompute_checksum chained as mutable_chaining.rs:19-63. */
 void nexo_recompute_frame(uint8_t* frame, size_t len, uint32_t flags, uint32_t ip_offset, uint32_t which,

@@ -68,6 +68,8 @@ def lib():
         L.nexo_build_udp6.restype = I
         L.nexo_build_udp6.argtypes = [P, P, P, P, U16, U16, ctypes.c_uint8, ctypes.c_uint8, U32, P,
                                       U32, P]
+        L.nexo_build_probe_batch.restype = I
+        L.nexo_build_probe_batch.argtypes = [ctypes.POINTER(ProbeBatch), P, I]
         L.nexo_recompute_frame.restype = None
         L.nexo_recompute_frame.argtypes = [P, S, U32, U32, U32, P]
         L.nexo_gen_length.restype = U32
@@ -249,6 +251,50 @@ def build_tcp(spec, sport, dport, seq=0, ack=0, flags=0, window=0xFFFF, urg=0, o
     if n < 0:
         raise ValueError("BuildError::LengthOverflow")
     return out.raw[:n]
+
+
+class ProbeBatch(ctypes.Structure):
+    """struct nexo_probe_batch (oracle/nex_oracle.h)"""
+    _fields_ = [("kind", ctypes.c_int), ("ip", IpSpec), ("dst", ctypes.c_void_p), ("count", ctypes.c_uint64),
+                ("sport", ctypes.c_uint16), ("dport", ctypes.c_uint16), ("window", ctypes.c_uint16),
+                ("urg", ctypes.c_uint16), ("seq", ctypes.c_uint32), ("ack", ctypes.c_uint32),
+                ("tcp_flags", ctypes.c_uint8), ("icmp_type", ctypes.c_uint8), ("icmp_code", ctypes.c_uint8),
+                ("pad0", ctypes.c_uint8), ("ident", ctypes.c_uint16), ("seqno", ctypes.c_uint16),
+                ("opts", ctypes.c_void_p), ("opt_len", ctypes.c_uint32),
+                ("payload", ctypes.c_void_p), ("payload_len", ctypes.c_uint32)]
+
+
+PROBE_KIND = {"tcp": 0, "icmp": 1, "udp6": 2}
+
+
+def build_probe_batch(kind, spec, dst, nthreads=1, out=None, **l4):
+    """A probe batch (nexo_build_probe_batch): every frame built from `spec`
+    and the L4 fields `l4` (tcp: sport, dport, seq, ack, flags, window, urg,
+    options, payload; icmp: icmp_type, icmp_code, ident, seqno, payload; udp6:
+    sport, dport, payload) with destination dst[i] ((count, 4|16) uint8).
+    Returns a (count, flen) uint8 array."""
+    dst = np.ascontiguousarray(dst, np.uint8)
+    n = dst.shape[0]
+    ob, on = _buf(l4.get("options", b""))
+    pb, pn = _buf(l4.get("payload", b""))
+    p = ProbeBatch(kind=PROBE_KIND[kind], ip=spec, dst=dst.ctypes.data, count=n,
+                   sport=l4.get("sport", 0), dport=l4.get("dport", 0), window=l4.get("window", 0xFFFF),
+                   urg=l4.get("urg", 0), seq=l4.get("seq", 0), ack=l4.get("ack", 0),
+                   tcp_flags=l4.get("flags", 0), icmp_type=l4.get("icmp_type", 8),
+                   icmp_code=l4.get("icmp_code", 0), ident=l4.get("ident", 0), seqno=l4.get("seqno", 0),
+                   opts=ctypes.cast(ob, ctypes.c_void_p), opt_len=on,
+                   payload=ctypes.cast(pb, ctypes.c_void_p), payload_len=pn)
+    first = ctypes.create_string_buffer(70000)
+    p.count = min(n, 1)  # one build first: the frame length (or the overflow)
+    flen = lib().nexo_build_probe_batch(ctypes.byref(p), first, 1) if n else 0
+    p.count = n
+    if flen < 0:
+        raise ValueError("BuildError::LengthOverflow")
+    if out is None:
+        out = np.empty((n, max(flen, 1)), np.uint8)
+    if n:
+        lib().nexo_build_probe_batch(ctypes.byref(p), out.ctypes.data, nthreads)
+    return out
 
 
 def build_icmp_echo(spec, icmp_type, code, ident, seqno, payload=b""):

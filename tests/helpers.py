@@ -610,3 +610,14 @@ def ipv4_option_frames(rng):
                         f.append(_eth(_ipv4(seg, proto, ihl=ihl, opts=opts, total=t)))
                     f.append(_eth(ip) + bytes(rng.integers(0, 256, int(rng.integers(1, 30)), dtype=np.uint8)))
     return f
+
+
+def probe_oracle_build(oracle, shape, dst_host, nthreads=1, out=None):
+    """The oracle's frames of a nex_amd.probes shape for numpy destinations
+    ((count, 4|16) uint8): oracle.build_probe_batch over probes.oracle_args."""
+    from nex_amd import probes
+    kind, spec, l4 = probes.oracle_args(shape)
+    spec = dict(spec)
+    fam = spec.pop("family")
+    sp = oracle.ip_spec(fam, spec.pop("src"), bytes(16 if fam == 6 else 4), **spec)
+    return oracle.build_probe_batch(kind, sp, dst_host, nthreads=nthreads, out=out, **l4)

@@ -7,6 +7,10 @@
 
 // SpanFrame's HBM touches past its LDS bytes, counted by harness_span_groups
 static unsigned long long g_span_probe[2];
+// byte pattern written past each frame's length where the kernels leave the
+// next frame's bytes (harness_set_poison; 0xA5 by default)
+static unsigned char g_poison = 0xA5;
+extern "C" void harness_set_poison(int v) { g_poison = (unsigned char)v; }
 #define NEXG_SPAN_PROBE(k, c) (g_span_probe[k] += (c) ? 1u : 0u)
 #include "../../nex_amd/csrc/parse_kernels.hpp"
 
@@ -31,7 +35,7 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
             const uint8_t* g = data + off;
             const uint32_t o = (uint32_t)(reinterpret_cast<uint64_t>(g) & 15u);
             const uint32_t wlen = len < window ? (uint32_t)len : window;
-            memset(slot, 0xA5, sizeof(slot));  // poison: bytes outside the window must not matter
+            memset(slot, g_poison, sizeof(slot));  // poison: bytes outside the window must not matter
             memcpy(slot + o, g, wlen);
             uint32_t w[16];
             if (use_fast && len == 64) memcpy(w, g, 64);
@@ -76,7 +80,7 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                 // the span kernel hands fast_canonical80 its window unmasked: the
                 // next frame's bytes past len (here a poison pattern) must not matter
                 uint32_t wf[20];
-                memset(wf, 0xA5, sizeof(wf));
+                memset(wf, g_poison, sizeof(wf));
                 memcpy(wf, g, len < 80 ? len : 80);
                 if (nexg::fast_canonical80(wf, (uint32_t)len, flags, par ? (uint64_t)tail * 256u : tail, te, r)) {
                     // the span kernel stores canonical80_code for these: it must be the encoder's code

@@ -37,7 +37,10 @@ def lib():
 
 
 def parse_packed(data, offsets=None, lengths=None, stride=0, flags=0, ip_offset=0, window=128,
-                 use_fast=False):
+                 use_fast=False, poison=0xA5):
+    """poison: the byte pattern the harness puts past each frame's length
+    where the kernels would hold the next frame's bytes (they must not matter)."""
+    lib().harness_set_poison(poison)
     data = np.ascontiguousarray(data, dtype=np.uint8)
     count = (len(lengths) if lengths is not None else
              (len(offsets) - 1 if offsets is not None else len(data) // stride))

@@ -47,6 +47,9 @@ def test_core_matches_oracle(oracle, corpus, flags, layout):
                                        use_fast=mode)
             helpers.records_equal(got, want, [buf[p:p + l] for p, l in zip(offs, lens)],
                                   f"flags={flags} layout={layout} window={window} mode={mode}")
+    # a second poison past len: the unmasked span window must not depend on it
+    got = harness.parse_packed(buf, offs, lens, flags=flags, ip_offset=ipo, use_fast=5, poison=0xFF)
+    helpers.records_equal(got, want, None, f"flags={flags} layout={layout} poison=0xFF")
 
 
 def test_core_bad_extent(oracle):

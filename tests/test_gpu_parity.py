@@ -76,6 +76,11 @@ def test_fixed_stride_matches_oracle(engine, oracle, corpus, stride):
     want = oracle.parse_frames(full)
     got = engine.parse_to_numpy(FrameBatch.from_strided(arr))
     helpers.records_equal(got, want, full, f"stride={stride} full")
+    # NEXG_OUT_DESC: staged through LDS, two descriptors per 16-B store; a
+    # ragged last tile (odd frame count) ends in one 8-B store
+    for m in (len(full), len(full) - 1 - (len(full) % 2 == 0)):
+        got_d = engine.parse_to_numpy(FrameBatch.from_strided(arr[:m]), out_kind=abi.OUT_DESC)
+        helpers.records_equal(got_d, desc_of(want[:m]), full[:m], f"stride={stride} desc count={m}")
 
 
 def test_generators_match_oracle(engine, oracle):
@@ -537,6 +542,28 @@ def test_build_udp4_tuples_aos(engine, oracle):
         assert (aos[: m * 42].cpu().numpy().reshape(m, 42) == want).all(), n
     rec = tup[:1].cpu().numpy().view(abi.UDP4_TUPLE_DTYPE)[0]
     assert rec["src_ip"] == int(p[0][0].item()) & 0xFFFFFFFF and rec["dst_port"] == int(p[3][0].item()) & 0xFFFF
+    # the other AOS instantiations: a payload (stride 82: the 128-B tile; stride
+    # 142: direct global writes) and an output 1 B off 16-B alignment (direct)
+    n = 3000
+    p = engine.gen_udp4_params(n, first_index=11)
+    tup = engine.pack_udp4_tuples(*p)
+    for plen, shift in ((40, 0), (100, 0), (0, 1), (40, 1)):
+        pay = torch.arange(plen, dtype=torch.uint8, device="cuda") if plen else None
+        stride = 42 + plen
+        buf_a = torch.zeros(n * stride + 16, dtype=torch.uint8, device="cuda")
+        buf_s = torch.zeros(n * stride + 16, dtype=torch.uint8, device="cuda")
+        engine.build_udp4_tuples(tup, src_mac=smac, dst_mac=dmac, ip_flags=2, payload=pay,
+                                 out=buf_a[shift:], out_stride=stride)
+        engine.build_udp4(*p, src_mac=smac, dst_mac=dmac, ip_flags=2, payload=pay, out=buf_s[shift:],
+                          out_stride=stride)
+        torch.cuda.synchronize()
+        assert torch.equal(buf_a, buf_s), (plen, shift)
+        host = [t.cpu().numpy().view(np.uint32 if t.element_size() == 4 else np.uint16) for t in p]
+        frames = buf_a[shift: shift + n * stride].cpu().numpy().reshape(n, stride)
+        for i in list(range(0, n, 97)) + [n - 1]:
+            want = oracle.build_udp4(smac, dmac, int(host[0][i]), int(host[1][i]), int(host[2][i]),
+                                     int(host[3][i]), int(host[4][i]), 64, 2, 0, bytes(range(plen)))
+            assert bytes(frames[i]) == want, (plen, shift, i)
     bad = abi.Udp4Build()
     bad.count, bad.dst_ip = 4, p[1].data_ptr()
     out = torch.empty(4 * 42, dtype=torch.uint8, device="cuda")

@@ -29,6 +29,15 @@ def test_rank_under_torchrun_runs():
 def test_rank_world_mismatch_is_an_error():
     action, msg = launch.decide(["--gpus", "8"], {"WORLD_SIZE": "1"}, 8)
     assert action == "error" and "WORLD_SIZE=1" in msg
+    action, msg = launch.decide(["--gpus=2"], {"WORLD_SIZE": "8"}, 2)
+    assert action == "error" and "WORLD_SIZE=8" in msg
+
+
+def test_torchrun_without_gpus_takes_world_size():
+    """`torchrun --nproc-per-node 8 bench.py` with --gpus left at its default:
+    the ranks run (world size from the launcher), no refusal."""
+    env = {"WORLD_SIZE": "8", "RANK": "0", "LOCAL_RANK": "0"}
+    assert launch.decide(["--steps", "5"], env, 1, n_devices=lambda: 1 / 0) == ("run", None)
 
 
 def test_spawn_command():
