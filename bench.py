@@ -389,9 +389,31 @@ def object_clocks(eng, batch, sampler, stream, device):
             _, st = eng.probe_span_clock(batch, stream=stream)
             torch.cuda.synchronize(device)
             r["span"] = clocks.span_summary(st.cpu().numpy())
+            r["hbm_latency"] = hbm_latency(eng, device)
         except Exception as e:  # reported, never fatal to the measurement
             r["span"] = {"error": repr(e)}
     return r
+
+
+_LAT_BUF = {}
+
+
+def hbm_latency(eng, device, steps=2000):
+    """Dependent HBM load latency on this box (nexg_probe_latency over a
+    1-GiB scratch ring, a ~1-MiB stride per step): alone and while 4
+    workgroups per CU stream-read the ring — the condition the span kernel's
+    generic section waits in."""
+    import random
+
+    import torch
+    buf = _LAT_BUF.get(device.index)
+    if buf is None:
+        buf = _LAT_BUF[device.index] = torch.empty(1 << 30, dtype=torch.uint8, device=device)
+    start = random.randrange(1 << 24)  # another chain each call: no line left in the caches by the last
+    idle_ns, idle_cyc = eng.probe_latency(buf, steps=steps, start=start)
+    loaded_ns, loaded_cyc = eng.probe_latency(buf, steps=steps, start=start + 7919, loaded=True)
+    return {"idle_ns": round(idle_ns, 1), "idle_cycles": round(idle_cyc, 1), "loaded_ns": round(loaded_ns, 1),
+            "loaded_cycles": round(loaded_cyc, 1), "steps": steps}
 
 
 def parse_object(eng, args, batch, out_kind, stream, device, rank, world, workload, traffic_key,

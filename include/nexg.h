@@ -523,6 +523,18 @@ int nexg_probe_stream(nexg_ctx* ctx, const void* data, uint64_t bytes, uint32_t 
 int nexg_probe_span_clock(nexg_ctx* ctx, const nexg_frames* frames, const nexg_parse_option* option,
                           void* out, uint64_t* stamps, void* stream);
 
+/* Calibration (not a reference entry point): dependent HBM load latency.
+ * Writes a ring into `buf` (device, `bytes` >= 4 MiB, 16-B aligned; 64-B
+ * line i holds the index of line (i + 16411) mod (bytes / 64)) and has one lane
+ * chase it for `steps` (1..2^20) dependent loads from line `start`, alone
+ * (loaded = 0) or while 4 workgroups per CU stream-read the buffer (loaded =
+ * 1: the conditions of a parse kernel's dependent loads). out (device, 4 u64,
+ * 8-B aligned): [0] shader-clock ticks and [1] 100-MHz ticks over the chain;
+ * per step = [1] / steps x 10 ns. The App. C mix's generic section waits on
+ * such loads. */
+int nexg_probe_latency(nexg_ctx* ctx, void* buf, uint64_t bytes, uint32_t steps, uint32_t start, uint32_t loaded,
+                       uint64_t* out, void* stream);
+
 /* ---- serialize path (udp_ping.rs:68-109 shape) -------------------------- */
 typedef struct nexg_udp4_build {
     const uint32_t* src_ip;   /* per frame, IPv4 address as BE u32 value, or

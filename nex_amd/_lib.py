@@ -47,6 +47,7 @@ def load():
                                                U32, P, P]),
         "nexg_probe_stream": (I, [P, P, U64, U32, P, P]),
         "nexg_probe_span_clock": (I, [P, ctypes.POINTER(abi.Frames), ctypes.POINTER(abi.ParseOptionC), P, P, P]),
+        "nexg_probe_latency": (I, [P, P, U64, U32, U32, U32, P, P]),
         "nexg_decode_options": (I, [P, ctypes.POINTER(abi.Frames), P, P, P]),
         "nexg_build_udp4_batch": (I, [P, ctypes.POINTER(abi.Udp4Build), P, U32, P]),
         "nexg_build_udp4_tuples": (I, [P, ctypes.POINTER(abi.Udp4Build), P, P, U32, P]),

@@ -352,7 +352,7 @@ HEADER_INLINE = ("nexg_sparse_decode", "nexg_grouped_code")
 EXPORTED_SYMBOLS = (
     "nexg_abi_version", "nexg_strerror", "nexg_ctx_create", "nexg_ctx_destroy",
     "nexg_ctx_last_error", "nexg_ctx_cu_count", "nexg_parse_batch", "nexg_checksum_batch", "nexg_decode_options", "nexg_probe_stream",
-    "nexg_probe_span_clock",
+    "nexg_probe_span_clock", "nexg_probe_latency",
     "nexg_sparse_expand", "nexg_grouped_expand", "nexg_recompute_checksums_batch",
     "nexg_rx_config_default", "nexg_rx_open", "nexg_rx_next_batch", "nexg_rx_stats", "nexg_rx_close",
     "nexg_tpacket3_walk", "nexg_tx_open", "nexg_tx_send_batch", "nexg_tx_close",

@@ -93,6 +93,10 @@ def sysfs(device_index=0, path=None):
         lvl = _current_level(_read(os.path.join(path, f"pp_dpm_{k}")))
         if lvl is not None:
             r[k] = lvl
+    for k in ("current_compute_partition", "current_memory_partition"):  # SPX / NPS1 etc.
+        v = _read(os.path.join(path, k))
+        if v is not None:
+            r[k.replace("current_", "")] = v.strip()
     for hw in sorted(glob.glob(os.path.join(path, "hwmon", "hwmon*"))):
         for name, key, scale in (("power1_average", "power_w", 1e-6), ("power1_input", "power_w", 1e-6),
                                  ("power1_cap", "power_cap_w", 1e-6)):
@@ -166,5 +170,6 @@ class Sampler:
         if pw:
             r["power_w"] = {"min": min(pw), "max": max(pw)}
         last = self.samples[-1]
-        r.update({k: v for k, v in last.items() if k.startswith("temp_") or k == "power_cap_w"})
+        r.update({k: v for k, v in last.items()
+                  if k.startswith("temp_") or k in ("power_cap_w", "compute_partition", "memory_partition")})
         return r

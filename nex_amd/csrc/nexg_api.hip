@@ -284,6 +284,20 @@ int nexg_probe_span_clock(nexg_ctx* ctx, const nexg_frames* frames, const nexg_p
     return hip_status(ctx, nexg::launch_span_clock(a, static_cast<hipStream_t>(stream)), NEXG_ELAUNCH);
 }
 
+int nexg_probe_latency(nexg_ctx* ctx, void* buf, uint64_t bytes, uint32_t steps, uint32_t start, uint32_t loaded,
+                       uint64_t* out, void* stream) {
+    if (!ctx) return NEXG_EINVAL;
+    if (!buf || !out || bytes < 64u * 65536u || bytes / 64u > 0xFFFFFFFFull || steps == 0 || steps > (1u << 20) ||
+        (reinterpret_cast<uint64_t>(buf) & 15u) != 0 || (reinterpret_cast<uint64_t>(out) & 7u) != 0)
+        return fail(ctx, NEXG_EINVAL, "probe_latency: buffer of at least 4 MiB (16-B aligned), 1..2^20 steps%s", nullptr);
+    DeviceGuard g(ctx);
+    // loaded: one reading workgroup per CU x 4, at most 64 passes over the buffer
+    const uint32_t wgs = loaded ? (uint32_t)ctx->cu_count * 4u : 0u;
+    return hip_status(ctx, nexg::launch_probe_latency(static_cast<uint32_t*>(buf), (uint32_t)(bytes / 64u), start, steps,
+                                                      wgs, 64u, out, static_cast<hipStream_t>(stream)),
+                      NEXG_ELAUNCH);
+}
+
 int nexg_build_udp4_batch(nexg_ctx* ctx, const nexg_udp4_build* p, uint8_t* out,
                           uint32_t out_stride, void* stream) {
     if (!ctx || !p) return NEXG_EINVAL;

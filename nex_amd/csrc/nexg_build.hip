@@ -139,6 +139,26 @@ __device__ __forceinline__ uint32_t per_or_def(const T* per, uint64_t i, uint32_
 // contiguously in LDS leave as 16-B non-temporal stores (+ byte tail of a
 // partial tile). Non-temporal: the udp_ping build of 16M frames takes 0.132
 // instead of 0.165 ms with identical HBM traffic (PMC).
+// Phase timing of the builders' workgroups (measurement builds only:
+// -DNEXG_PROBE_TIMING=1, tools/probe_timing.py): thread 0 of workgroup b
+// stores s_memtime at phase k into g_build_stamps[8 b + k] (k = 6, 7:
+// s_memrealtime at entry and exit); the product library has none of it.
+#ifndef NEXG_PROBE_TIMING
+#define NEXG_PROBE_TIMING 0
+#endif
+#if NEXG_PROBE_TIMING
+constexpr uint32_t kStampWgs = 1u << 18;
+__device__ uint64_t g_build_stamps[8u * kStampWgs];
+#define NEXG_BUILD_STAMP(k)                                                                    \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x < kStampWgs)                                        \
+            g_build_stamps[8u * blockIdx.x + (k)] = (k) >= 6 ? __builtin_amdgcn_s_memrealtime()  \
+                                                             : __builtin_amdgcn_s_memtime();   \
+    } while (0)
+#else
+#define NEXG_BUILD_STAMP(k) do { } while (0)
+#endif
+
 __device__ __forceinline__ void build_copy_out(const uint8_t* smem, uint8_t* T, uint32_t bytes) {
     const uint32_t tid = threadIdx.x;
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -146,6 +166,15 @@ __device__ __forceinline__ void build_copy_out(const uint8_t* smem, uint8_t* T, 
         __builtin_nontemporal_store(reinterpret_cast<const v4u*>(smem)[c], reinterpret_cast<v4u*>(T) + c);
     const uint32_t tail = bytes & ~15u;
     if (tid < bytes - tail) T[tail + tid] = smem[tail + tid];
+}
+
+// Loads of one batch-wide value (the shared source, the small payload) by every
+// lane of every workgroup: through the scalar cache (constant address space,
+// s_load), not as vector loads of one line that every workgroup of the grid
+// sends to that line's L2 channel. p is 4-B aligned.
+typedef const __attribute__((address_space(4))) uint32_t* uniform_u32_ptr;
+__device__ __forceinline__ uniform_u32_ptr uniform_u32(const void* p) {
+    return reinterpret_cast<uniform_u32_ptr>(reinterpret_cast<uintptr_t>(p));
 }
 
 // BE word sum of the shared payload (it starts at an even L4 offset), once
@@ -177,6 +206,8 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     constexpr bool STAGED = MAXS != 0;
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
     const nexg_udp4_build& p = a.p;
+    NEXG_BUILD_STAMP(0);
+    NEXG_BUILD_STAMP(6);
     const uint64_t first = tile_index(a.tile_order) * kBuildTile;
     const uint64_t left = p.count - first;
     const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
@@ -241,10 +272,19 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
             for (uint32_t k = 0; k < p.payload_len; k++) d[42 + k] = p.payload[k];
         }
     }
+    NEXG_BUILD_STAMP(1);
     if (STAGED) {
         __syncthreads();
+        NEXG_BUILD_STAMP(2);
+        NEXG_BUILD_STAMP(3);
         build_copy_out(smem, a.out + first * a.out_stride, nf * a.out_stride);
     }
+#if NEXG_PROBE_TIMING
+    NEXG_BUILD_STAMP(4);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    NEXG_BUILD_STAMP(5);
+    NEXG_BUILD_STAMP(7);
+#endif
 }
 
 // ---- udp_ping IPv6 branch: builder/udp.rs:67-95 over IPv6 (udp.rs:480-505),
@@ -265,6 +305,8 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
     constexpr bool STAGED = MAXS != 0;
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
     const nexg_udp6_build& p = a.p;
+    NEXG_BUILD_STAMP(0);
+    NEXG_BUILD_STAMP(6);
     const uint64_t first = tile_index(a.tile_order) * kBuildTile;
     const uint64_t left = p.count - first;
     const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
@@ -274,13 +316,19 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
     __shared__ uint32_t s_pay;
     const uint64_t pw = shared_payload_sum(p.payload, p.payload_len, &s_pay);
     if (tid < nf) {
-        const uint64_t si = PROBE || p.src_shared ? 0u : i;  // one source for the whole batch
         // addresses are 4-B aligned (the ABI checks): dword loads
-        const auto* s4 = NEXG_GLOBAL(uint32_t, p.src_ip + 16u * si);
         const auto* d4 = NEXG_GLOBAL(uint32_t, p.dst_ip + 16u * i);
         uint32_t sw[4], dw[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) { sw[k] = s4[k]; dw[k] = d4[k]; }
+        for (int k = 0; k < 4; k++) dw[k] = d4[k];
+        if (PROBE || p.src_shared) {  // one source for the whole batch (uniform branch)
+#pragma unroll
+            for (int k = 0; k < 4; k++) sw[k] = uniform_u32(p.src_ip)[k];
+        } else {
+            const auto* s4 = NEXG_GLOBAL(uint32_t, p.src_ip + 16u * i);
+#pragma unroll
+            for (int k = 0; k < 4; k++) sw[k] = s4[k];
+        }
         const uint32_t sp = PROBE ? p.def_src_port : per_or_def(p.src_port, i, p.def_src_port);
         const uint32_t dp = PROBE ? p.def_dst_port : per_or_def(p.dst_port, i, p.def_dst_port);
         const uint32_t ulen = 8u + p.payload_len;
@@ -330,10 +378,19 @@ __global__ __launch_bounds__(256) void k_build_udp6(Build6Args a) {
             for (uint32_t k = 0; k < p.payload_len; k++) d[62 + k] = p.payload[k];
         }
     }
+    NEXG_BUILD_STAMP(1);
     if (STAGED) {
         __syncthreads();
+        NEXG_BUILD_STAMP(2);
+        NEXG_BUILD_STAMP(3);
         build_copy_out(smem, a.out + first * a.out_stride, nf * a.out_stride);
     }
+#if NEXG_PROBE_TIMING
+    NEXG_BUILD_STAMP(4);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    NEXG_BUILD_STAMP(5);
+    NEXG_BUILD_STAMP(7);
+#endif
 }
 
 // ---- tcp_ping / icmp_ping: one kernel per (family, L4 kind) ----------------
@@ -371,6 +428,51 @@ struct L4Args {
     uint32_t tile_order;  // tile_index order (nexg_internal.hpp), as k_build_udp4
 };
 
+// A shared payload of at most kSmallPay bytes (icmp_ping's "hello"): every
+// lane loads the same dwords (uniform addresses: scalar loads, no barrier)
+// and sums them itself, instead of shared_payload_sum's per-workgroup global
+// loads, LDS atomic and two barriers in front of every tile.
+constexpr uint32_t kSmallPay = 64;
+struct SmallPayload {
+    uint32_t w[kSmallPay / 4];  // payload byte k = byte k & 3 of w[k >> 2] (bytes past n: 0)
+    // k a compile-time index (unrolled loops): no dynamically indexed private array
+    __device__ __forceinline__ uint32_t byte(uint32_t k) const { return (w[k >> 2] >> (8u * (k & 3u))) & 0xFFu; }
+};
+
+__device__ __forceinline__ void load_small_payload(const uint8_t* pl, uint32_t n, SmallPayload& sp, uint32_t& be_sum) {
+    if (n == 0) {  // uniform; pl may be NULL
+#pragma unroll
+        for (uint32_t k = 0; k < kSmallPay / 4; k++) sp.w[k] = 0;
+        be_sum = 0;
+        return;
+    }
+    const uint64_t a = reinterpret_cast<uint64_t>(pl);
+    const uint32_t sh = (uint32_t)(a & 3u);
+    const uniform_u32_ptr src = uniform_u32(reinterpret_cast<const void*>(a & ~3ull));
+    const uint32_t nw = (sh + n + 3u) >> 2;
+    uint32_t raw[kSmallPay / 4 + 1];
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPay / 4 + 1; k++) raw[k] = src[k < nw ? k : nw - 1u];  // clamped: none past n
+    // one empty asm over all 17: the loads issue together, one wait (per-value
+    // statements let the compiler sink each load next to its own wait)
+    asm volatile("" : "+s"(raw[0]), "+s"(raw[1]), "+s"(raw[2]), "+s"(raw[3]), "+s"(raw[4]), "+s"(raw[5]),
+                 "+s"(raw[6]), "+s"(raw[7]), "+s"(raw[8]), "+s"(raw[9]), "+s"(raw[10]), "+s"(raw[11]),
+                 "+s"(raw[12]), "+s"(raw[13]), "+s"(raw[14]), "+s"(raw[15]), "+s"(raw[16]));
+    static_assert(kSmallPay / 4 + 1 == 17, "the asm above names every raw dword");
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPay / 4 + 1; k++) raw[k] = k < nw ? raw[k] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPay / 4; k++) {  // realigned to the payload's first byte, masked to n
+        const uint32_t x = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh);
+        sp.w[k] = 4u * k + 4u <= n ? x : 4u * k >= n ? 0u : x & ((1u << (8u * (n - 4u * k))) - 1u);
+    }
+    uint32_t s = 0;  // BE words from the payload's start (an even L4 offset), odd tail byte high
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPay / 4; k++)  // two BE halfwords per dword (bytes past n are 0)
+        s += bswap16(sp.w[k] & 0xFFFFu) + bswap16(sp.w[k] >> 16);
+    be_sum = s;
+}
+
 // halfword v (memory order: low byte first) at LDS/global byte offset p
 __device__ __forceinline__ void put_hw(uint8_t* base, uint32_t p, uint32_t v, bool odd) {
     if (odd) {
@@ -394,23 +496,32 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGED ? kBuildTile * MAXS : 16];
     __shared__ uint32_t s_pay;
     const uint32_t tid = threadIdx.x;
+    NEXG_BUILD_STAMP(0);
+    NEXG_BUILD_STAMP(6);
     const uint64_t first = tile_index(a.tile_order) * kBuildTile;
     const uint64_t left = a.count - first;
     const uint32_t nf = left < kBuildTile ? (uint32_t)left : kBuildTile;
     const uint64_t i = first + tid;
-    const uint32_t pay_sum = shared_payload_sum(a.payload, a.payload_len, &s_pay);
+    const bool small = a.payload_len <= kSmallPay;  // uniform
+    SmallPayload spay{};
+    uint32_t pay_sum = 0;
+    if (small) load_small_payload(a.payload, a.payload_len, spay, pay_sum);
+    else pay_sum = shared_payload_sum(a.payload, a.payload_len, &s_pay);
     const uint32_t l4_hdr = KIND == kL4Tcp ? 20u + a.opt_padded : 8u;
     const uint32_t l4_len = l4_hdr + a.payload_len;
     const uint32_t flen = 14u + 2u * NIP + l4_len;
     if (tid < nf) {
         const nexg_ip_build& ip = a.ip;
         constexpr uint32_t AW = FAM == 4 ? 1u : 4u;  // address dwords
-        const uint64_t si = PROBE || ip.src_shared ? 0u : i;  // one source for the whole batch
         uint32_t sw[AW], dw[AW];
 #pragma unroll
-        for (uint32_t k = 0; k < AW; k++) {
-            sw[k] = NEXG_GLOBAL(uint32_t, ip.src_ip)[AW * si + k];
-            dw[k] = NEXG_GLOBAL(uint32_t, ip.dst_ip)[AW * i + k];
+        for (uint32_t k = 0; k < AW; k++) dw[k] = NEXG_GLOBAL(uint32_t, ip.dst_ip)[AW * i + k];
+        if (PROBE || ip.src_shared) {  // one source for the whole batch (uniform branch)
+#pragma unroll
+            for (uint32_t k = 0; k < AW; k++) sw[k] = uniform_u32(ip.src_ip)[k];
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < AW; k++) sw[k] = NEXG_GLOBAL(uint32_t, ip.src_ip)[AW * i + k];
         }
         uint32_t addr_le = 0;  // address words as LE halves: x256 gives the BE sum (mod 0xFFFF)
 #pragma unroll
@@ -431,7 +542,7 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
         // ---- L4 header + checksum ----
         uint64_t t;
         constexpr int L = 7 + NIP;  // first L4 halfword
-        if (KIND == kL4Tcp) {
+        if constexpr (KIND == kL4Tcp) {
             const uint32_t sp = PROBE ? a.def_sport : per_or_def(a.sport, i, a.def_sport);
             const uint32_t dp = PROBE ? a.def_dport : per_or_def(a.dport, i, a.def_dport);
             const uint32_t sq = PROBE ? a.def_seq : per_or_def(a.seq, i, a.def_seq);
@@ -498,14 +609,29 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
                 if (k < a.opt_padded) put_hw(base, p + k, a.options[k] | ((uint32_t)a.options[k + 1] << 8), odd);
             p += a.opt_padded;
         }
-        for (uint32_t k = 0; k < a.payload_len; k++) base[p + k] = a.payload[k];
+        if (small) {
+#pragma unroll
+            for (uint32_t k = 0; k < kSmallPay; k++)
+                if (k < a.payload_len) base[p + k] = (uint8_t)spay.byte(k);
+        } else {
+            for (uint32_t k = 0; k < a.payload_len; k++) base[p + k] = a.payload[k];
+        }
         if (STAGED)
             for (uint32_t k = flen; k < a.out_stride; k++) base[d0 + k] = 0;
     }
+    NEXG_BUILD_STAMP(1);
     if (STAGED) {
         __syncthreads();
+        NEXG_BUILD_STAMP(2);
+        NEXG_BUILD_STAMP(3);
         build_copy_out(smem, a.out + first * a.out_stride, nf * a.out_stride);
     }
+#if NEXG_PROBE_TIMING
+    NEXG_BUILD_STAMP(4);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    NEXG_BUILD_STAMP(5);
+    NEXG_BUILD_STAMP(7);
+#endif
 }
 
 template <int FAM, int KIND, bool PROBE>
@@ -515,7 +641,9 @@ static void launch_l4_form(const L4Args& a, hipStream_t s) {
     // IPv6: 16-KiB tile + build_lds_pad() -> 5 workgroups per CU (icmp6 echo
     // 0.29 -> 0.26 ms at 16M frames); IPv4 shapes run faster at 8 per CU (tcp
     // SYN 0.21 vs 0.24-0.26 ms, icmp echo 0.132 vs 0.140; profiles/r04/builders/)
-    const uint32_t pad = FAM == 6 || PROBE ? build_lds_pad() : 0u;
+    // ICMP probe batches (odd frame lengths, 47 / 67 B) run faster at 8 per CU:
+    // 0.437 / 0.570 of 8 TB/s written against 0.385 / 0.485 (profiles/r05/probe/)
+    const uint32_t pad = (FAM == 6 || PROBE) && !(PROBE && KIND == kL4Icmp) ? build_lds_pad() : 0u;
     if (staged && a.out_stride <= 64u)
         hipLaunchKernelGGL((k_build_l4<FAM, KIND, 64, PROBE>), dim3((uint32_t)blocks), dim3(kBuildTile), pad, s, a);
     else if (staged && a.out_stride <= 80u)  // tcp_ping's 66 B: a 20-KiB tile (7 per CU) instead of 32 KiB (4)
@@ -528,13 +656,24 @@ static void launch_l4_form(const L4Args& a, hipStream_t s) {
         hipLaunchKernelGGL((k_build_l4<FAM, KIND, 0, PROBE>), dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);
 }
 
+static bool try_probe_l4(const L4Args& l, int kind, uint8_t* out, uint32_t out_stride, hipStream_t s, hipError_t& e);
+
 template <int FAM, int KIND>
-static void launch_l4_fam(const L4Args& a, hipStream_t s) {
-    // the probe batch: one source, a destination per frame, nothing else per frame
+static void launch_l4_fam(L4Args& a, hipStream_t s) {
+    // the probe batch: one source, a destination per frame, nothing else per
+    // frame. It reads 4 / 16 B per frame, as udp_ping's probe batch, and takes
+    // that builder's tile order (contiguous eighths); the forms with several
+    // parameter arrays keep l4_build_tile_order()
     const bool probe = a.ip.src_shared && !a.ip.ip_id && !a.ip.src_mac && !a.ip.dst_mac &&
                        (KIND == kL4Tcp ? !a.sport && !a.dport && !a.seq && !a.ack : !a.ident && !a.seqno);
-    if (probe) launch_l4_form<FAM, KIND, true>(a, s);
-    else launch_l4_form<FAM, KIND, false>(a, s);
+    hipError_t e = hipSuccess;  // a launch error also reaches launch_l4's hipGetLastError
+    if (probe && try_probe_l4(a, KIND, a.out, a.out_stride, s, e)) return;
+    if (probe) {
+        a.tile_order = build_tile_order();
+        launch_l4_form<FAM, KIND, true>(a, s);
+    } else {
+        launch_l4_form<FAM, KIND, false>(a, s);
+    }
 }
 
 static hipError_t launch_l4(L4Args& a, int kind, hipStream_t s) {
@@ -573,6 +712,377 @@ hipError_t launch_build_icmp_echo(const nexg_icmp_echo_build& p, uint8_t* out, u
     a.payload = p.payload; a.payload_len = p.payload_len; a.count = p.count;
     a.out = out; a.out_stride = out_stride;
     return launch_l4(a, kL4Icmp, s);
+}
+
+
+// ---- probe batches: one template + a per-frame patch ----------------------
+// Every frame of a probe batch (one source, a destination per frame, every
+// other field the batch's) is one template with the destination address and
+// the checksums over it patched. The host builds the template (one frame
+// period P = out_stride, with destination, checksums and the device-resident
+// source / payload bytes 0) and its base sums and passes it in the kernel
+// arguments; a workgroup reads it by scalar loads, merges in the source and
+// payload (scalar loads: every workgroup reads the same line, which as vector
+// loads makes one L2 channel the bottleneck), lays the period out in LDS and
+// fills its tile with it (one ds_write_b128 per 16-B chunk, realigned by
+// v_alignbyte), patches each frame (the other builders' closed-form sums: the
+// batch base sum plus the destination's halfwords), and copies the tile out
+// with 16-B non-temporal stores.
+// Used for tcp_ping (IPv4 / IPv6) and udp_ping's IPv6 batch, where it beats
+// the per-lane builders (tcp_ping 0.75-0.79 of 8 TB/s written against
+// 0.70-0.73); udp_ping's IPv4 batch and the ICMP shapes stay per lane
+// (profiles/r05/probe/). A persistent sweep over the tiles and one-wave
+// workgroups were measured and lose (writes at 0.65-0.72 of 8 TB/s in a
+// sweep, tools/writebench.hip).
+#ifndef NEXG_PROBE_TEMPLATE
+#define NEXG_PROBE_TEMPLATE 1  // 0: the per-lane builders for probe batches too (A/B builds)
+#endif
+constexpr uint32_t kProbeMaxP = 128;
+
+struct ProbeArgs {
+    uint32_t tmpl[kProbeMaxP / 4];  // one period (the frame with destination, checksums and device bytes 0, zero pad)
+    uint64_t ip_sum;           // IPv4 header: congruent sum of every word but the destination's (and a device source's)
+    uint64_t l4_sum;           // L4: the same, without the payload
+    const uint8_t* dst;        // per-frame destination: DW dwords each, 4-B aligned
+    const uint8_t* src;        // the batch's source on the device (DW dwords), written in at src_off; or NULL
+    const uint8_t* payload;    // device payload (<= kSmallPay bytes), written in at pay_off
+    uint8_t* out;
+    uint64_t count;
+    uint32_t period;           // out_stride (<= kProbeMaxP)
+    uint32_t dst_off, ip_ck_off, l4_ck_off;  // byte offsets in the frame; a checksum offset 0 = none
+    uint32_t l4_dst;           // the L4 checksum covers the addresses (all but ICMPv4)
+    uint32_t dst_value;        // udp_ping IPv4: dst is a u32 value (bytes reversed in the frame, BE halves summed)
+    uint32_t src_off, ip_src;  // device source offset; the source is in the IPv4 header checksum
+    uint32_t pay_off, pay_len;
+    uint32_t tile_order;
+};
+
+// halfword v (big-endian: high byte first in memory) at LDS byte position p
+__device__ __forceinline__ void lds_put_be16(uint8_t* lds, uint32_t p, uint32_t v) {
+    if (p & 1u) {
+        lds[p] = (uint8_t)(v >> 8);
+        lds[p + 1] = (uint8_t)v;
+    } else {
+        *reinterpret_cast<uint16_t*>(lds + p) = (uint16_t)bswap16(v);
+    }
+}
+// dword d of network-order bytes (as loaded little-endian) at LDS position p
+__device__ __forceinline__ void lds_put_net32(uint8_t* lds, uint32_t p, uint32_t d) {
+    lds_put_be16(lds, p, bswap16(d & 0xFFFFu));
+    lds_put_be16(lds, p + 2u, bswap16(d >> 16));
+}
+
+// A workgroup of WAVES waves builds a tile of kT = 64 WAVES frames (one per
+// lane). KCH = ceil(P / 16): the 16-B pattern chunks per lane (kT frames x P
+// bytes = kT P / 16 chunks), written unconditionally. With one wave per
+// workgroup the barriers below are wave barriers (no s_barrier).
+template <uint32_t DW, uint32_t KCH, uint32_t WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_build_probe(ProbeArgs a) {
+    constexpr uint32_t kT = 64u * WAVES;
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_tile[];  // kT x P, then the pattern
+    const uint32_t t = threadIdx.x, P = a.period;
+    // (1) once per workgroup, the period in LDS: wave 0 composes template
+    // bytes [0, P + 24) (the period and the start of its next copy, so a 20-B
+    // window at any offset < P is contiguous): the template dwords come from
+    // the kernel arguments by scalar loads and reach their lanes by a cndmask
+    // chain and ds_bpermute; the device payload and source bytes are loaded
+    // into place, so they are part of the pattern and not patched per frame
+    uint8_t* const tp = s_tile + KCH * 16u * kT;  // 2 x kProbeMaxP + 32 B
+    // the first tile's destinations go in flight (clamped index: an
+    // unconditional load; lanes past the batch's end reload its last frame)
+    NEXG_BUILD_STAMP(0);
+    NEXG_BUILD_STAMP(6);
+    const uint64_t tile = tile_index(a.tile_order);
+    uint32_t dw[DW];
+    {
+        const uint64_t i = tile * kT + t;
+        const auto* d4 = NEXG_GLOBAL(uint32_t, a.dst + 4u * DW * (i < a.count ? i : a.count - 1u));
+#pragma unroll
+        for (uint32_t k = 0; k < DW; k++) dw[k] = d4[k];
+    }
+    // the batch's device source and payload by scalar loads (uniform
+    // addresses through the scalar cache: a vector load of one line by every
+    // workgroup of the grid makes that line's L2 channel the bottleneck), and
+    // their BE word sums computed from them (no reduction)
+    uint32_t sx[DW], ssum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < DW; k++) sx[k] = 0;
+#ifndef NEXG_PROBE_NODEV
+#define NEXG_PROBE_NODEV 0  // A/B builds only: no device source / payload loads (wrong bytes)
+#endif
+    if (a.src && !NEXG_PROBE_NODEV) {  // 4-B aligned
+#pragma unroll
+        for (uint32_t k = 0; k < DW; k++) sx[k] = uniform_u32(a.src)[k];
+#pragma unroll
+        for (uint32_t k = 0; k < DW; k++) ssum += bswap16(sx[k] & 0xFFFFu) + bswap16(sx[k] >> 16);
+    }
+    SmallPayload spay;
+    uint32_t psum;
+    load_small_payload(a.payload, NEXG_PROBE_NODEV ? 0u : a.pay_len, spay, psum);  // realigned words, 0 past pay_len
+    if (t < 64u) {
+        // template, source and payload words handed to lane k by cndmask
+        // chains, then each pattern byte picked by ds_bpermute from the lane
+        // holding it (one per source: the source lane returns its own copy of
+        // the operand, so the operand cannot depend on the reading lane)
+        uint32_t v = 0, sv = 0, pv = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kProbeMaxP / 4; k++) v = t == k ? a.tmpl[k] : v;
+#pragma unroll
+        for (uint32_t k = 0; k < DW; k++) sv = t == k ? sx[k] : sv;
+#pragma unroll
+        for (uint32_t k = 0; k < kSmallPay / 4; k++) pv = t == k ? spay.w[k] : pv;
+        uint32_t d = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            const uint32_t j = 4u * t + i, jm = j >= P ? j - P : j;
+            const uint32_t pi = jm - a.pay_off, si = jm - a.src_off;  // wrap: huge when before
+            const bool in_p = pi < a.pay_len, in_s = a.src && si < 4u * DW;
+            const uint32_t xt = (uint32_t)__shfl(v, (int)(jm >> 2));
+            const uint32_t xs = (uint32_t)__shfl(sv, (int)((si >> 2) & 63u));
+            const uint32_t xp = (uint32_t)__shfl(pv, (int)((pi >> 2) & 63u));
+            const uint32_t x = in_p ? xp >> (8u * (pi & 3u)) : in_s ? xs >> (8u * (si & 3u)) : xt >> (8u * (jm & 3u));
+            d |= (x & 0xFFu) << (8u * i);
+        }
+        if (4u * t < P + 24u) reinterpret_cast<uint32_t*>(tp)[t] = d;
+    }
+    __syncthreads();
+    const uint32_t step = (16u * kT) % P, r0 = (16u * t) % P;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    // the pattern over the tile: chunk c = bytes [(16 c) mod P, + 16) of the
+    // period, five dword reads realigned by v_alignbyte
+    auto fill = [&]() {
+        uint32_t r = r0;
+#pragma unroll
+        for (uint32_t k = 0; k < KCH; k++) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(tp + (r & ~3u));
+            const uint32_t sh = r & 3u;
+            const uint4 c = make_uint4(__builtin_amdgcn_alignbyte(w[1], w[0], sh),
+                                       __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                                       __builtin_amdgcn_alignbyte(w[3], w[2], sh),
+                                       __builtin_amdgcn_alignbyte(w[4], w[3], sh));
+            reinterpret_cast<uint4*>(s_tile)[t + kT * k] = c;
+            r += step;
+            r = r >= P ? r - P : r;
+        }
+    };
+    // this lane's frame: the destination and the checksums over it
+    auto patch = [&](const uint32_t (&cur)[DW]) {
+        uint8_t* f = s_tile + t * P;
+        uint32_t dsum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < DW; k++) dsum += halves(cur[k]);
+        uint64_t D;
+        if (a.dst_value) {  // a u32 value: network order in the frame, its BE halves summed
+            lds_put_be16(f, a.dst_off, cur[0] >> 16);
+            lds_put_be16(f, a.dst_off + 2u, cur[0] & 0xFFFFu);
+            D = dsum;
+        } else {  // network-order bytes as stored: LE halves x 256
+#pragma unroll
+            for (uint32_t k = 0; k < DW; k++) lds_put_net32(f, a.dst_off + 4u * k, cur[k]);
+            D = 256ull * dsum;
+        }
+        const uint64_t S = ssum;
+        if (a.ip_ck_off) lds_put_be16(f, a.ip_ck_off, fold_complement(a.ip_sum + (a.ip_src ? S : 0u) + D));
+        if (a.l4_ck_off) lds_put_be16(f, a.l4_ck_off, fold_complement(a.l4_sum + psum + (a.l4_dst ? S + D : 0u)));
+    };
+    // (2) fill, patch, copy out: one tile per workgroup (a persistent sweep
+    // over the tiles writes at 0.65-0.72 of 8 TB/s against 0.77-0.83 for one
+    // tile per workgroup, tools/writebench.hip, profiles/r05/writebench/)
+    const uint64_t first = (uint64_t)tile * kT;
+    const uint32_t nf = a.count - first < kT ? (uint32_t)(a.count - first) : kT;
+    NEXG_BUILD_STAMP(1);
+    fill();
+    __syncthreads();
+    NEXG_BUILD_STAMP(2);
+    if (t < nf) patch(dw);
+    __syncthreads();
+    NEXG_BUILD_STAMP(3);
+    const uint32_t bytes = nf * P;
+    uint8_t* T = a.out + first * P;
+    for (uint32_t c = t; c < bytes / 16u; c += kT)
+        __builtin_nontemporal_store(reinterpret_cast<const v4u*>(s_tile)[c], reinterpret_cast<v4u*>(T) + c);
+    const uint32_t tail = bytes & ~15u;
+    if (t < bytes - tail) T[tail + t] = s_tile[tail + t];
+#if NEXG_PROBE_TIMING
+    NEXG_BUILD_STAMP(4);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // the stores' completion
+    NEXG_BUILD_STAMP(5);
+    NEXG_BUILD_STAMP(7);
+#endif
+}
+
+// ---- host: probe templates (the bytes the per-lane builders write, with the
+// destination, checksums and payload zero) and their base sums
+namespace {
+void put_be16(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 8);
+    p[1] = (uint8_t)v;
+}
+uint64_t be_halves(const uint8_t* p, uint32_t n) {  // BE words of n (even) bytes
+    uint64_t s = 0;
+    for (uint32_t k = 0; k < n; k += 2) s += ((uint32_t)p[k] << 8) | p[k + 1];
+    return s;
+}
+void probe_eth(uint8_t* t, const uint8_t* dmac, const uint8_t* smac, uint32_t ethertype) {
+    for (int k = 0; k < 6; k++) {
+        t[k] = dmac[k];
+        t[6 + k] = smac[k];
+    }
+    put_be16(t + 12, ethertype);
+}
+// IPv4 header (builder/ipv4.rs:94-170) with destination and checksum zero;
+// returns the BE word sum of the rest (the header checksum's base)
+uint64_t probe_ipv4(uint8_t* h, uint32_t tos, uint32_t total, uint32_t id, uint32_t flags, uint32_t ttl,
+                    uint32_t proto, const uint8_t* src) {
+    h[0] = 0x45; h[1] = (uint8_t)tos;
+    put_be16(h + 2, total);
+    put_be16(h + 4, id);
+    put_be16(h + 6, (flags & 7u) << 13);
+    h[8] = (uint8_t)ttl; h[9] = (uint8_t)proto;
+    put_be16(h + 10, 0);
+    for (int k = 0; k < 4; k++) { h[12 + k] = src[k]; h[16 + k] = 0; }
+    return be_halves(h, 20);
+}
+// IPv6 header (builder/ipv6.rs:89-152) with the destination zero
+void probe_ipv6(uint8_t* h, uint32_t tc, uint32_t flow, uint32_t plen, uint32_t next, uint32_t hop, const uint8_t* src) {
+    const uint32_t fl = flow & 0xFFFFFu;
+    h[0] = (uint8_t)(0x60u | (tc >> 4)); h[1] = (uint8_t)(((tc & 0xFu) << 4) | (fl >> 16));
+    h[2] = (uint8_t)(fl >> 8); h[3] = (uint8_t)fl;
+    put_be16(h + 4, plen);
+    h[6] = (uint8_t)next; h[7] = (uint8_t)hop;
+    for (int k = 0; k < 16; k++) { h[8 + k] = src[k]; h[24 + k] = 0; }
+}
+
+bool probe_launch_ok(uint32_t flen, uint32_t period, uint32_t pay_len, const uint8_t* out) {
+    return NEXG_PROBE_TEMPLATE && period <= kProbeMaxP && flen <= period && pay_len <= kSmallPay &&
+           (reinterpret_cast<uint64_t>(out) & 15u) == 0;
+}
+
+// Probe kernel shape (measurement overrides, read once): NEXG_PROBE_WAVES
+// waves per workgroup (1 or 4), NEXG_PROBE_WGS workgroups per CU set by the
+// dynamic LDS (160 KiB per CU; 0 = only the tile's LDS).
+uint32_t probe_env(const char* name, uint32_t def, uint32_t lo, uint32_t hi) {
+    const char* e = getenv(name);
+    const long x = e ? strtol(e, nullptr, 10) : -1;
+    return x >= (long)lo && x <= (long)hi ? (uint32_t)x : def;
+}
+uint32_t probe_waves() {
+    static const uint32_t v = probe_env("NEXG_PROBE_WAVES", 4u, 1u, 4u) == 1u ? 1u : 4u;
+    return v;
+}
+uint32_t probe_wgs_per_cu() {
+    static const uint32_t v = probe_env("NEXG_PROBE_WGS", 5u, 0u, 64u);
+    return v;
+}
+
+// tmpl: one period (P bytes, zero past the frame), one tile per workgroup
+hipError_t launch_probe(ProbeArgs& a, const uint8_t* tmpl, uint32_t dw, hipStream_t s) {
+    if (a.count == 0) return hipSuccess;
+    const uint32_t P = a.period;
+    for (uint32_t k = 0; k < kProbeMaxP / 4; k++)
+        a.tmpl[k] = (uint32_t)tmpl[4 * k] | ((uint32_t)tmpl[4 * k + 1] << 8) | ((uint32_t)tmpl[4 * k + 2] << 16) |
+                    ((uint32_t)tmpl[4 * k + 3] << 24);
+    const uint32_t waves = probe_waves(), kT = 64u * waves;
+    const uint64_t ntiles = (a.count + kT - 1) / kT;
+    if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t need = (P + 15u) / 16u;  // 16-B chunks per lane, rounded to an instantiated KCH
+    const uint32_t kch = need <= 3u ? 3u : need <= 6u ? need : 8u;
+    const uint32_t tile_lds = kch * 16u * kT + 2u * kProbeMaxP + 32u, wgs = probe_wgs_per_cu();
+    const uint32_t cap = wgs ? 160u * 1024u / wgs - 1024u : 0u;
+    const uint32_t lds = tile_lds > cap ? tile_lds : cap;
+    a.tile_order = build_tile_order();
+    const dim3 g((uint32_t)ntiles), b(kT);
+#define NEXG_PROBE_LAUNCH(DW, K)                                                     \
+    do {                                                                             \
+        if (waves == 1u) hipLaunchKernelGGL((k_build_probe<DW, K, 1>), g, b, lds, s, a); \
+        else hipLaunchKernelGGL((k_build_probe<DW, K, 4>), g, b, lds, s, a);             \
+    } while (0)
+    if (dw == 1) {
+        if (kch == 3) NEXG_PROBE_LAUNCH(1, 3); else if (kch == 4) NEXG_PROBE_LAUNCH(1, 4);
+        else if (kch == 5) NEXG_PROBE_LAUNCH(1, 5); else if (kch == 6) NEXG_PROBE_LAUNCH(1, 6);
+        else NEXG_PROBE_LAUNCH(1, 8);
+    } else {
+        if (kch == 3) NEXG_PROBE_LAUNCH(4, 3); else if (kch == 4) NEXG_PROBE_LAUNCH(4, 4);
+        else if (kch == 5) NEXG_PROBE_LAUNCH(4, 5); else if (kch == 6) NEXG_PROBE_LAUNCH(4, 6);
+        else NEXG_PROBE_LAUNCH(4, 8);
+    }
+#undef NEXG_PROBE_LAUNCH
+    return hipGetLastError();
+}
+}  // namespace
+
+// udp_ping's IPv6 probe batch (src_shared, dst per frame): builder/udp.rs:67-95
+// over IPv6 (udp.rs:480-505) as k_build_udp6 sums it
+static bool try_probe_udp6(const nexg_udp6_build& p, uint8_t* out, uint32_t out_stride, hipStream_t s, hipError_t& e) {
+    const uint32_t flen = 62u + p.payload_len;
+    if (!probe_launch_ok(flen, out_stride, p.payload_len, out)) return false;
+    ProbeArgs a{};
+    uint8_t t[kProbeMaxP] = {0};
+    const uint8_t zero[16] = {0};
+    const uint32_t ulen = 8u + p.payload_len;
+    probe_eth(t, p.def_dst_mac, p.def_src_mac, 0x86DD);
+    probe_ipv6(t + 14, p.traffic_class, p.flow_label, ulen, 17, p.hop_limit, zero);
+    uint8_t* u = t + 54;
+    put_be16(u, p.def_src_port); put_be16(u + 2, p.def_dst_port); put_be16(u + 4, ulen); put_be16(u + 6, 0);
+    a.l4_sum = 17u + ulen + (uint64_t)p.def_src_port + p.def_dst_port + ulen;
+    a.src = p.src_ip; a.src_off = 22; a.ip_src = 0;
+    a.dst = p.dst_ip; a.dst_off = 38;
+    a.payload = p.payload; a.pay_off = 62; a.pay_len = p.payload_len;
+    a.out = out; a.count = p.count; a.period = out_stride;
+    a.l4_ck_off = 60; a.l4_dst = 1;
+    e = launch_probe(a, t, 4, s);
+    return true;
+}
+
+// tcp_ping / icmp_ping probe batches (ip.src_shared, dst per frame): the
+// layouts and sums of k_build_l4
+static bool try_probe_l4(const L4Args& l, int kind, uint8_t* out, uint32_t out_stride, hipStream_t s, hipError_t& e) {
+    const nexg_ip_build& ip = l.ip;
+    const bool v4 = ip.family == 4;
+    const uint32_t l3 = v4 ? 20u : 40u;
+    const uint32_t l4_hdr = kind == kL4Tcp ? 20u + l.opt_padded : 8u;
+    const uint32_t l4_len = l4_hdr + l.payload_len;
+    const uint32_t flen = 14u + l3 + l4_len;
+    // tcp_ping only: the ICMP shapes run faster per lane (0.44 / 0.57 of 8 TB/s
+    // against 0.41 / 0.37 for the template kernel, profiles/r05/probe/)
+    if (kind != kL4Tcp || !probe_launch_ok(flen, out_stride, l.payload_len, out)) return false;
+    ProbeArgs a{};
+    uint8_t t[kProbeMaxP] = {0};
+    const uint8_t zero[16] = {0};
+    const uint32_t proto = kind == kL4Tcp ? 6u : (v4 ? 1u : 58u);
+    probe_eth(t, ip.def_dst_mac, ip.def_src_mac, v4 ? 0x0800 : 0x86DD);
+    if (v4) a.ip_sum = probe_ipv4(t + 14, ip.tos, 20u + l4_len, ip.def_ip_id, ip.ip_flags, ip.ttl, proto, zero);
+    else probe_ipv6(t + 14, ip.tos, ip.flow_label, l4_len, proto, ip.ttl, zero);
+    uint8_t* h = t + 14 + l3;
+    uint64_t sum;
+    if (kind == kL4Tcp) {
+        const uint32_t w6 = ((l4_hdr / 4u) << 12) | (l.flags & 0xFFu);
+        put_be16(h, l.def_sport); put_be16(h + 2, l.def_dport);
+        put_be16(h + 4, l.def_seq >> 16); put_be16(h + 6, l.def_seq & 0xFFFFu);
+        put_be16(h + 8, l.def_ack >> 16); put_be16(h + 10, l.def_ack & 0xFFFFu);
+        put_be16(h + 12, w6); put_be16(h + 14, l.window); put_be16(h + 16, 0); put_be16(h + 18, l.urg);
+        for (uint32_t k = 0; k < l.opt_padded; k++) h[20 + k] = l.options[k];
+        sum = (uint64_t)l.def_sport + l.def_dport + (l.def_seq >> 16) + (l.def_seq & 0xFFFFu) + (l.def_ack >> 16) +
+              (l.def_ack & 0xFFFFu) + w6 + l.window + l.urg + l.opt_sum;
+        a.l4_ck_off = 14 + l3 + 16;
+    } else {
+        const uint32_t w0 = (l.icmp_type << 8) | l.icmp_code;
+        put_be16(h, w0); put_be16(h + 2, 0); put_be16(h + 4, l.def_ident); put_be16(h + 6, l.def_seqno);
+        sum = (uint64_t)w0 + l.def_ident + l.def_seqno;
+        a.l4_ck_off = 14 + l3 + 2;
+    }
+    const bool pseudo = !v4 || kind == kL4Tcp;  // ICMPv4 sums the message alone
+    if (pseudo) sum += proto + l4_len;
+    a.l4_sum = sum;
+    a.l4_dst = pseudo ? 1u : 0u;
+    a.ip_ck_off = v4 ? 24u : 0u;
+    a.ip_src = v4 ? 1u : 0u;
+    a.src = ip.src_ip; a.src_off = v4 ? 26u : 22u;
+    a.dst = ip.dst_ip; a.dst_off = v4 ? 30u : 38u;
+    a.payload = l.payload; a.pay_off = 14 + l3 + l4_hdr; a.pay_len = l.payload_len;
+    a.out = out; a.count = l.count; a.period = out_stride;
+    e = launch_probe(a, t, v4 ? 1u : 4u, s);
+    return true;
 }
 
 // ---- arp / ndp probes ------------------------------------------------------
@@ -908,6 +1418,8 @@ hipError_t launch_build_udp4(const nexg_udp4_build& p, uint8_t* out, uint32_t ou
     const bool full = p.src_ip && p.src_port && p.dst_port && p.ip_id && !p.src_mac && !p.dst_mac;
     const bool probe = !p.src_ip && !p.src_port && !p.dst_port && !p.ip_id && !p.src_mac && !p.dst_mac;
     // the udp_ping shapes: a 16-KiB tile + build_lds_pad() -> 5 workgroups per CU
+    // (the probe batch stays per lane: 0.84-0.85 of 8 TB/s written against
+    // 0.69-0.83 for the template kernel, profiles/r05/probe/)
     const uint32_t pad = build_lds_pad();
     if (staged && out_stride <= 64u && full)
         hipLaunchKernelGGL((k_build_udp4<64, true>), dim3((uint32_t)blocks), dim3(kBuildTile), pad, s, a);
@@ -929,6 +1441,9 @@ hipError_t launch_build_udp6(const nexg_udp6_build& p, uint8_t* out, uint32_t ou
     const uint64_t blocks = (p.count + kBuildTile - 1) / kBuildTile;
     const bool staged = out_stride <= kBuildMaxStride && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
     const bool probe = p.src_shared && !p.src_port && !p.dst_port && !p.src_mac && !p.dst_mac;
+    hipError_t e = hipSuccess;
+    if (probe && try_probe_udp6(p, out, out_stride, s, e)) return e;
+    if (probe) a.tile_order = build_tile_order();  // udp_ping's probe batch order (see launch_l4_fam)
     // a 16-KiB tile for the udp_ping shapes + build_lds_pad(): 5 workgroups per CU (0.279 -> 0.253 ms)
     if (staged && out_stride <= 64u && probe)
         hipLaunchKernelGGL((k_build_udp6<64, true>), dim3((uint32_t)blocks), dim3(kBuildTile), build_lds_pad(), s, a);
@@ -970,3 +1485,20 @@ hipError_t launch_gen_udp4_params(uint64_t seed, uint64_t first, uint64_t count,
 }
 
 }  // namespace nexg
+
+#if NEXG_PROBE_TIMING
+// measurement builds only: copy the builders' workgroup stamps to the host
+extern "C" int nexg_debug_build_stamps(uint64_t* host, uint64_t n, int reset) {
+    if (n > 8ull * nexg::kStampWgs) n = 8ull * nexg::kStampWgs;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(nexg::g_build_stamps), n * 8u, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    if (reset) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(nexg::g_build_stamps)) != hipSuccess ||
+            hipMemset(p, 0, 8ull * 8u * nexg::kStampWgs) != hipSuccess)
+            return -1;
+    }
+    return 0;
+}
+#endif

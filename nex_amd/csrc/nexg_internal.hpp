@@ -87,6 +87,8 @@ hipError_t launch_decode_options(const ParseArgs& a, const nexg_record* recs, ne
                                  hipStream_t s);
 
 hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, uint32_t mode, void* out, hipStream_t s);
+hipError_t launch_probe_latency(uint32_t* buf, uint32_t lines, uint32_t start, uint32_t steps, uint32_t loaded_wgs,
+                                uint32_t rounds, uint64_t* out, hipStream_t s);
 
 hipError_t launch_build_udp4_tuples(const nexg_udp4_build& p, const nexg_udp4_tuple* tuples, uint8_t* out,
                                     uint32_t out_stride, hipStream_t s);

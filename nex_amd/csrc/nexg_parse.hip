@@ -326,6 +326,57 @@ hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, uint32_t mod
     return hipGetLastError();
 }
 
+// dependent-load latency probe (include/nexg.h nexg_probe_latency): a ring
+// of 64-B lines, line i holding the index of line (i + kChaseStride) mod n
+// (a stride of ~1 MiB: every step another DRAM page), chased by one lane
+constexpr uint32_t kChaseStride = 16411;  // prime: one cycle through every line when n is not a multiple
+__global__ __launch_bounds__(256) void k_chase_init(uint32_t* buf, uint32_t n, uint64_t* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i < n) buf[i * 16u] = (uint32_t)((i + kChaseStride) % n);
+    if (i < 4) out[i] = 0;
+}
+// workgroup 0, lane 0: `steps` dependent loads from line `start`, then
+// out[0] = shader-clock ticks, out[1] = 100-MHz ticks, out[3] = the last line
+// (keeps the chain live), and the done flag out[2] raised. The other
+// workgroups (the loaded case) stream-read the buffer in 16-B chunks until the
+// flag is up or `rounds` passes are done, whichever comes first.
+__global__ __launch_bounds__(256) void k_chase(const uint32_t* buf, uint32_t n, uint32_t start, uint32_t steps,
+                                               uint32_t rounds, uint64_t* out) {
+    uint32_t* done = reinterpret_cast<uint32_t*>(out + 2);
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            const auto* b = NEXG_GLOBAL(uint32_t, buf);
+            uint32_t j = start % n;
+            j = b[(uint64_t)j * 16u];  // first touch outside the timed chain
+            const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t k = 0; k < steps; k++) j = b[(uint64_t)j * 16u];
+            const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            out[0] = c1 - c0;
+            out[1] = r1 - r0;
+            out[3] = j;
+            __hip_atomic_store(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    const uint64_t chunks = (uint64_t)n * 4u, lanes = (uint64_t)(gridDim.x - 1u) * 256u;
+    uint32_t x = 0;
+    for (uint32_t r = 0; r < rounds; r++) {
+        if (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        for (uint64_t c = (uint64_t)(blockIdx.x - 1u) * 256u + threadIdx.x; c < chunks; c += lanes) {
+            const uint4 v = load16<true>(reinterpret_cast<const uint8_t*>(buf) + 16u * c);
+            x ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (x == 0x9e3779b9u) out[3] = x;  // never true on the ring's contents: a pure read stream
+}
+
+hipError_t launch_probe_latency(uint32_t* buf, uint32_t lines, uint32_t start, uint32_t steps, uint32_t loaded_wgs,
+                                uint32_t rounds, uint64_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_chase_init, dim3((lines + 255u) / 256u), dim3(256), 0, s, buf, lines, out);
+    hipLaunchKernelGGL(k_chase, dim3(1u + loaded_wgs), dim3(256), 0, s, buf, lines, start, steps, rounds, out);
+    return hipGetLastError();
+}
+
 // util.rs:65-71 checksum(buf, skipword) per buffer; words outside the buffer
 // and the skipped word contribute nothing; empty -> 0.
 __global__ __launch_bounds__(256) void k_checksum(ParseArgs a, uint32_t skipword, uint16_t* out) {

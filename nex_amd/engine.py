@@ -290,6 +290,19 @@ class Engine:
                                                    _ptr(stamps), self._stream(stream)))
         return out, stamps
 
+    def probe_latency(self, buf, steps: int = 2000, start: int = 0, loaded: bool = False, stream=None):
+        """Dependent HBM load latency (nexg_probe_latency; calibration, not a
+        reference entry point) over a uint8 device scratch tensor (>= 4 MiB):
+        returns (ns per step, shader-clock cycles per step)."""
+        torch = _torch()
+        out = torch.zeros(4, dtype=torch.int64, device=self.torch_device)
+        nbytes = buf.numel() // 64 * 64
+        self._check(self.lib.nexg_probe_latency(self.ctx, _ptr(buf), nbytes, int(steps), int(start) & 0xFFFFFFFF,
+                                                1 if loaded else 0, _ptr(out), self._stream(stream)))
+        torch.cuda.synchronize(self.torch_device)
+        cyc, ticks = (int(v) for v in out[:2].cpu())
+        return ticks * 10.0 / steps, cyc / steps
+
     def checksum(self, batch: FrameBatch, skipword: int, stream=None):
         """util::checksum(buf, skipword) per buffer (util.rs:65)."""
         torch = _torch()

@@ -101,3 +101,72 @@ def test_probe_batch_16m(engine, oracle, shape):
     flags = v[: n * 4].view(torch.int32)
     need = abi.C_L4_OK | (abi.C_IP_OK if probes.SHAPES[shape][0] == 4 else 0)
     assert int(((flags & need) != need).sum().item()) == 0
+
+
+@pytest.mark.parametrize("plen,stride", [(0, 42), (5, 47), (5, 64), (13, 63), (64, 128), (65, 107), (0, 129)])
+def test_udp4_probe_payload_stride(engine, oracle, plen, stride):
+    """udp_ping's IPv4 probe batch with a payload and a frame stride past the
+    frame (zero padding) or odd: the per-lane kernel's staged (stride <= 128)
+    and direct forms give the oracle's bytes."""
+    import torch
+    n = 1000
+    L = 42 + plen
+    dst = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda",
+                        generator=torch.Generator(device="cuda").manual_seed(plen + stride))
+    pay = bytes(range(7, 7 + plen))
+    pt = torch.tensor(list(pay), dtype=torch.uint8, device="cuda") if plen else None
+    smac, dmac = bytes([2, 0, 0, 0, 0, 1]), bytes([2, 0, 0, 0, 0, 2])
+    out = engine.build_udp4(None, dst, def_src_ip=0xC0A80164, def_src_port=53443, def_dst_port=33435, def_ip_id=9,
+                            src_mac=smac, dst_mac=dmac, ttl=61, ip_flags=2, dscp_ecn=0x2e, payload=pt, out_stride=stride)
+    torch.cuda.synchronize()
+    data = out.cpu().numpy()[: n * stride].reshape(n, stride)
+    hd = dst.cpu().numpy().view(np.uint32)
+    for i in list(range(0, n, 13)) + [n - 1]:
+        want = oracle.build_udp4(smac, dmac, 0xC0A80164, int(hd[i]), 53443, 33435, 9, 61, 2, 0x2e, pay)
+        assert bytes(data[i, :L]) == want, (plen, stride, i)
+        if stride <= 128:  # the LDS-staged kernels zero the gap (the direct one leaves it)
+            assert not data[i, L:].any(), (plen, stride, i)
+
+
+@pytest.mark.parametrize("family", [4, 6])
+@pytest.mark.parametrize("plen,stride", [(5, None), (0, 71), (33, None), (64, 128)])
+def test_l4_probe_payload_stride(engine, oracle, family, plen, stride):
+    """tcp / icmp probe batches with other payloads and strides (odd, padded,
+    the 64-B payload limit of the template kernel, which builds the tcp
+    shapes) against the oracle."""
+    import torch
+    n = 777
+    w = 4 if family == 4 else 16
+    g = torch.Generator(device="cuda").manual_seed(family * 100 + plen)
+    dst = torch.randint(0, 256, (n, w), dtype=torch.uint8, device="cuda", generator=g)
+    src = torch.randint(0, 256, (w,), dtype=torch.uint8, device="cuda", generator=g)
+    pay = bytes((3 * k + 1) & 0xFF for k in range(plen))
+    pt = torch.tensor(list(pay), dtype=torch.uint8, device="cuda") if plen else None
+    smac, dmac = bytes([2, 0, 0, 0, 0, 3]), bytes([2, 0, 0, 0, 0, 4])
+    hs, hd = bytes(src.cpu().numpy()), dst.cpu().numpy()
+    Lt = 14 + (20 if family == 4 else 40) + 20 + 12 + plen
+    St = stride or Lt
+    if St >= Lt:
+        out = engine.build_tcp(family, src, dst, def_src_port=1234, def_dst_port=443, def_seq=0x01020304,
+                               def_ack=0x0a0b0c0d, flags=0x12, window=501, urgent_ptr=7, options=probes.TCP_PING_OPTS,
+                               payload=pt, def_ip_id=0x55, src_mac=smac, dst_mac=dmac, ttl=33, ip_flags=2, tos=0x10,
+                               flow_label=0x12345, out_stride=St)
+        torch.cuda.synchronize()
+        data = out.cpu().numpy()[: n * St].reshape(n, St)
+        for i in list(range(0, n, 11)) + [n - 1]:
+            spec = oracle.ip_spec(family, hs, bytes(hd[i]), smac, dmac, 0x55, 33, 2, 0x10, 0x12345)
+            want = oracle.build_tcp(spec, 1234, 443, 0x01020304, 0x0a0b0c0d, 0x12, 501, 7, probes.TCP_PING_OPTS, pay)
+            assert bytes(data[i, :Lt]) == want, ("tcp", family, plen, St, i)
+    Li = 14 + (20 if family == 4 else 40) + 8 + plen
+    Si = stride or Li
+    if Si >= Li:
+        out = engine.build_icmp_echo(family, src, dst, def_identifier=0x77, def_sequence=0x88, payload=pt,
+                                     def_ip_id=0x99, src_mac=smac, dst_mac=dmac, ttl=12, ip_flags=2,
+                                     flow_label=0x54321, out_stride=Si)
+        torch.cuda.synchronize()
+        data = out.cpu().numpy()[: n * Si].reshape(n, Si)
+        typ = 8 if family == 4 else 128
+        for i in list(range(0, n, 11)) + [n - 1]:
+            spec = oracle.ip_spec(family, hs, bytes(hd[i]), smac, dmac, 0x99, 12, 2, 0, 0x54321)
+            want = oracle.build_icmp_echo(spec, typ, 0, 0x77, 0x88, pay)
+            assert bytes(data[i, :Li]) == want, ("icmp", family, plen, Si, i)

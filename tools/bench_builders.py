@@ -22,9 +22,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=16 << 20)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--probe", action="store_true", help="time the probe batches (nex_amd/probes.py) instead")
+    ap.add_argument("--lib", default=None, help="another build of libnexg.so (A/B)")
     args = ap.parse_args()
     import torch
+    from nex_amd import _lib
     from nex_amd.engine import Engine
+    if args.lib:
+        _lib._lib, _lib.LIB_PATH = None, os.path.abspath(args.lib)
     eng = Engine(0)
     n = args.frames
     g = torch.Generator(device="cuda").manual_seed(7)
@@ -42,8 +47,17 @@ def main():
         "icmp4_echo_42B": (42, lambda out: eng.build_icmp_echo(4, a4s, a4d, sp, dp, ip_id=ipid, out=out)),
         "icmp6_echo_62B": (62, lambda out: eng.build_icmp_echo(6, a6s, a6d, sp, dp, out=out)),
     }
-    res = {"frames": n, "lds_pad": os.environ.get("NEXG_BUILD_LDS_PAD", "default"),
-           "order": os.environ.get("NEXG_L4_ORDER", "default")}
+    if args.probe:  # the probe batches of nex_amd/probes.py (one source, a destination per frame)
+        from nex_amd import probes
+        shapes = {}
+        for name in probes.SHAPES:
+            d = rb(n, probes.dst_bytes(name))
+            shapes[f"probe_{name}_{probes.frame_len(name)}B"] = (
+                probes.frame_len(name), lambda out, name=name, d=d: probes.build(eng, name, d, out=out))
+    res = {"frames": n, "lib": args.lib or "default", "lds_pad": os.environ.get("NEXG_BUILD_LDS_PAD", "default"),
+           "probe_wgs": os.environ.get("NEXG_PROBE_WGS", "default"), "probe_waves": os.environ.get("NEXG_PROBE_WAVES", "default"),
+           "order": os.environ.get("NEXG_L4_ORDER", "default"),
+           "build_order": os.environ.get("NEXG_BUILD_ORDER", "default")}
     for name, (flen, fn) in shapes.items():
         out = torch.empty(n * flen, dtype=torch.uint8, device="cuda")
         for _ in range(10):

@@ -20,8 +20,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--frames", type=int, default=16 << 20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--shape", choices=["tuples", "aos"], default="tuples",
-                    help="five tuple arrays (nexg_build_udp4_batch) or 16-B records (nexg_build_udp4_tuples)")
+    ap.add_argument("--shape", choices=["tuples", "aos", "probe"], default="tuples",
+                    help="five tuple arrays (nexg_build_udp4_batch), 16-B records (nexg_build_udp4_tuples) or "
+                         "udp_ping's probe batch (a destination per frame)")
     args = ap.parse_args()
     import torch
     from nex_amd import _lib
@@ -43,6 +44,9 @@ def main():
     def step(e):
         if tup is not None:
             e.build_udp4_tuples(tup, src_mac=macs[0], dst_mac=macs[1], ip_flags=2, out=out, stream=s)
+        elif args.shape == "probe":
+            e.build_udp4(None, p[1], def_src_ip=0xC0A80164, def_src_port=53443, def_dst_port=33435, src_mac=macs[0],
+                         dst_mac=macs[1], ip_flags=2, out=out, stream=s)
         else:
             e.build_udp4(p[0], p[1], p[2], p[3], p[4], src_mac=macs[0], dst_mac=macs[1], ip_flags=2, out=out,
                          stream=s)

@@ -3,7 +3,7 @@
 for one kernel, its scratch spill / reload instructions and its barriers in
 program order, with the sub-tile loop marked (the basic block range between a
 loop header label and its backward branch that holds the loop's barriers).
-usage: [NEXG_DEFS="-DX=1 ..."] python tools/isa_spills.py [mangled-kernel-substring]"""
+usage: [NEXG_DEFS="-DX=1 ..."] [NEXG_SRC=file.hip] python tools/isa_spills.py [mangled-kernel-substring]"""
 import os
 import re
 import subprocess
@@ -13,7 +13,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 name = sys.argv[1] if len(sys.argv) > 1 else "k_parse_spanILi6ELi1ELj20480ELi6E"
 out = "/tmp/nexg_parse_isa.s"
 subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950"] + os.environ.get("NEXG_DEFS", "").split() + [
-                       "--cuda-device-only", "-S", "-o", out, os.path.join(ROOT, "nex_amd/csrc/nexg_parse.hip")],
+                       "--cuda-device-only", "-S", "-o", out,
+                       os.environ.get("NEXG_SRC", os.path.join(ROOT, "nex_amd/csrc/nexg_parse.hip"))],
                       stderr=subprocess.DEVNULL)
 s = open(out).read()
 start = [m.start() for m in re.finditer(r"^_ZN4nexg\w*:", s, re.M) if name in s[m.start():m.start() + 200]][0]
