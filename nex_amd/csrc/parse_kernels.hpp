@@ -332,10 +332,25 @@ __device__ __forceinline__ uint32_t* handoff_slot(const ParseArgs& a, uint64_t i
     return reinterpret_cast<uint32_t*>(a.out) + idx * (OUT == NEXG_OUT_FLAGS ? 1u : OUT == NEXG_OUT_DESC ? 2u : 16u);
 }
 
+// Each layout's loads in one block of uniform control flow, issued together
+// (the one-expression form compiled the packed case to offsets[idx], a wait,
+// then offsets[idx + 1]: two dependent round trips at every workgroup's start)
 __device__ __forceinline__ bool frame_extent(const ParseArgs& a, uint64_t idx, uint64_t& off, uint32_t& len) {
-    off = a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride;
-    const uint64_t l64 = a.lengths ? (uint64_t)a.lengths[idx]
-                                   : (a.offsets ? a.offsets[idx + 1] - off : (uint64_t)a.stride);
+    uint64_t l64;
+    if (a.offsets && !a.lengths) {  // packed: the next frame's offset ends this one
+        const auto* op = NEXG_GLOBAL(uint64_t, a.offsets);
+        const uint64_t o0 = op[idx], o1 = op[idx + 1];
+        off = o0;
+        l64 = o1 - o0;
+    } else if (a.offsets) {
+        const uint64_t o0 = NEXG_GLOBAL(uint64_t, a.offsets)[idx];
+        const uint32_t l = NEXG_GLOBAL(uint32_t, a.lengths)[idx];
+        off = o0;
+        l64 = l;
+    } else {
+        off = idx * (uint64_t)a.stride;
+        l64 = a.lengths ? (uint64_t)NEXG_GLOBAL(uint32_t, a.lengths)[idx] : (uint64_t)a.stride;
+    }
     const bool bad = l64 > 65535u || off > a.data_bytes || l64 > a.data_bytes - off;
     len = bad ? 0u : (uint32_t)l64;
     return !bad;
@@ -630,7 +645,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint64_t off = 0;
     uint32_t len = 0;
     const bool have = t < nf;
-    if (OUT == NEXG_OUT_GROUPED && lane == 0 && have) reinterpret_cast<uint8_t*>(a.out)[idx >> 6] = 0;  // every group mixed
+#ifndef NEXG_SPAN_HEAD_LATE
+#define NEXG_SPAN_HEAD_LATE 0
+#endif
+    // every group mixed: head 0 (NEXG_SPAN_HEAD_LATE: with the final stores)
+    if (!NEXG_SPAN_HEAD_LATE && OUT == NEXG_OUT_GROUPED && lane == 0 && have)
+        reinterpret_cast<uint8_t*>(a.out)[idx >> 6] = 0;
     const bool ok = have && frame_extent(a, idx, off, len);
     if (t == 0) s_span[0] = off;
     if (t == nf - 1) s_span[1] = off + len;
@@ -883,6 +903,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // uniformity test and the head store out of the generic section's register
     // budget: with them the App. C mix ran 10 % slower, profiles/r03/grouped)
     NEXG_SPAN_STAMP(4);
+    if (NEXG_SPAN_HEAD_LATE && OUT == NEXG_OUT_GROUPED && lane == 0 && have)
+        reinterpret_cast<uint8_t*>(a.out)[idx >> 6] = 0;
     if (sparse_like(OUT)) store_sparse_coded<OUT, false>(a, idx, have, r, code);
     else if (OUT == NEXG_OUT_DESC && NEXG_DESC_MODE == 2) {  // 256 x 8 B through the slots: 16-B NT stores
         // own slot only (the generic section's reads of other lanes' slots

@@ -3,7 +3,7 @@
 UDP64 (and optionally IMIX) batch and output buffer, each build timed with HIP
 events, interleaved A B C A B C. Output-width experiments write different
 bytes, so outputs are compared only with --check.
-usage: python tools/bench_parse_ab.py --libs A.so,B.so [--workloads udp64,imix] [--out sparse]"""
+usage: python tools/bench_parse_ab.py --libs A.so,B.so [--workloads udp64,imix,mix,real] [--out sparse]"""
 import argparse
 import json
 import os
@@ -36,7 +36,13 @@ def main():
         engines.append(Engine(0))
     s = torch.cuda.current_stream()
     for wl in args.workloads.split(","):
-        b = engines[0].gen_batch(abi.WL_UDP64 if wl == "udp64" else abi.WL_IMIX, 16 << 20)
+        if wl in ("mix", "real"):  # bench.py's App. C malformed mix / real-traffic batch (1M distinct, tiled)
+            from nex_amd import workloads
+            mk = workloads.malformed_mix if wl == "mix" else workloads.real_traffic
+            m, _ = mk(engines[0], 1 << 20, seed=abi.DEFAULT_SEED + (0 if wl == "mix" else 7))
+            b = workloads.tiled(m, 16)
+        else:
+            b = engines[0].gen_batch(abi.WL_UDP64 if wl == "udp64" else abi.WL_IMIX, 16 << 20)
         out = torch.empty(Engine.out_bytes(ok, b.count), dtype=torch.uint8, device="cuda")
         if args.check:
             ref = None

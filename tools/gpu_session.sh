@@ -19,9 +19,12 @@ for s in ${STEPS:-tests}; do
     kbench) step kbench 300 ./tools/kbench ;;
     probetests) step pytest_probe 600 python -u -m pytest tests/test_gpu_probe_batches.py tests/test_gpu_build_l4.py tests/test_gpu_parity.py -k "probe or build or fixed_stride" -q -x --timeout 300 --timeout-method thread ;;
     probebench) step probe_bench 600 bash -c 'for r in 1 2; do python tools/bench_builders.py --probe || exit 1; python tools/bench_builders.py --probe --lib abvar/libnexg_noprobe.so || exit 1; NEXG_BUILD_LDS_PAD=0 python tools/bench_builders.py --probe --lib abvar/libnexg_noprobe.so || exit 1; done' ;;
-    probewgs) step probe_wgs 900 bash -c 'for cfg in "xcd 1 0 def" "xcd 4 5 def" "xcd 4 0 def" "xcd 4 5 0"; do set -- $cfg; export NEXG_BUILD_ORDER=$1 NEXG_PROBE_WAVES=$2 NEXG_PROBE_WGS=$3; if [ $4 = 0 ]; then export NEXG_BUILD_LDS_PAD=0; fi; echo "cfg $cfg"; for l in nex_amd/libnexg.so abvar/libnexg_noprobe.so; do python tools/bench_builders.py --probe --lib $l || exit 1; done; python -u tools/bench_ser_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_noprobe.so --shape probe --rounds 2 || exit 1; done' ;;
+    probewgs) step probe_wgs 900 bash -c 'for cfg in "0 def" "1 def" "1 0"; do set -- $cfg; export NEXG_PROBE_ICMP=$1; if [ $2 = 0 ]; then export NEXG_BUILD_LDS_PAD=0; fi; echo "cfg $cfg"; for l in nex_amd/libnexg.so abvar/libnexg_noprobe.so; do python tools/bench_builders.py --probe --lib $l || exit 1; done; done' ;;
        probetime) step probe_time 600 bash -c 'python -u tools/probe_timing.py --lib abvar/libnexg_ptime.so && NEXG_PROBE_WAVES=4 NEXG_PROBE_WGS=5 python -u tools/probe_timing.py --lib abvar/libnexg_ptime.so && python -u tools/probe_timing.py --lib abvar/libnexg_ptime_noprobe.so' ;;
     nodev) step nodev 600 bash -c 'for w in 1 4; do for l in nex_amd/libnexg.so abvar/libnexg_nodev.so; do NEXG_PROBE_WAVES=$w NEXG_PROBE_WGS=5 python tools/bench_builders.py --probe --lib $l || exit 1; done; done' ;;
+    mixprobe) step mix_probe 400 python3 bench.py --steps 20 --warmup 5 --no-large --no-ser --no-cpu-baseline ;;
+    headab) step head_ab 600 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_headlate.so --workloads imix,mix,real --out grouped --check --rounds 4 ;;
+    r04ab) step r04_ab 900 env NEXG_AB_LIB_LENIENT=1 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_r04.so,abvar/libnexg_headlate.so --workloads imix,mix,real --out grouped --check --rounds 4 ;;
     serab) step ser_ab 300 python -u tools/bench_ser_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_noprobe.so --shape probe --rounds 4 ;;
     descab) step desc_ab 600 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_desc1.so,abvar/libnexg_desc0.so --workloads udp64,imix --out desc --rounds 3 ;;
     newtests) step pytest_new 600 python -u -m pytest tests/test_gpu_sparse.py tests/test_gpu_fixup.py -q -x --timeout 300 --timeout-method thread ;;
