@@ -24,6 +24,7 @@ struct ParseArgs {
     uint32_t* tail = nullptr; // TwoPass tail-sum hand-off (count entries) for outputs
                               // narrower than 4 B per frame; null -> the output itself
     uint64_t* stamps = nullptr;  // k_parse_span<..., TIMING>: 8 clock stamps per workgroup
+    uint8_t* grouped_heads = nullptr;  // span kernel, NEXG_OUT_GROUPED run as SPARSE at the code offset: head bytes (all 0)
 };
 
 // Kernel variants of the parse path.

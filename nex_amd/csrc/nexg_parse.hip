@@ -79,6 +79,17 @@ ParseVariant choose_parse_variant(const ParseArgs& a) {
 #define NEXG_SPAN_WPE 6  // span kernel waves per SIMD (its VGPR cap)
 #endif
 
+// The span kernel's NEXG_OUT_GROUPED output: every group mixed (head 0), so
+// from NEXG_GROUPED_CODE_OFFSET on it is NEXG_OUT_SPARSE's layout (codes, then
+// the exceptions at the next 16-B boundary): the SPARSE instance writes it there
+// and stores the heads.
+static ParseArgs grouped_as_sparse(const ParseArgs& a) {
+    ParseArgs b = a;
+    b.grouped_heads = static_cast<uint8_t*>(a.out);
+    b.out = static_cast<uint8_t*>(a.out) + NEXG_GROUPED_CODE_OFFSET(a.count);
+    return b;
+}
+
 template <int OUT>
 static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream_t s) {
     const uint64_t blocks = (a.count + kTile - 1) / kTile;
@@ -102,6 +113,9 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             // (Two-barrier / double-buffered generations measured slower,
             // 0.66-0.69 vs 0.75: tools/kbench.hip keeps them for A/B.)
             if (OUT == NEXG_OUT_RECORD) hipLaunchKernelGGL((k_parse_span<OUT, 1, 16384, 1>), grid, block, 0, s, a);
+            else if (OUT == NEXG_OUT_GROUPED)
+                hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, NEXG_SPAN_SUB, NEXG_SPAN_WPE>), grid, block, 0, s,
+                                   grouped_as_sparse(a));
             else hipLaunchKernelGGL((k_parse_span<OUT, 1, NEXG_SPAN_SUB, NEXG_SPAN_WPE>), grid, block, 0, s, a);
             break;
         case ParseVariant::TwoPass:
@@ -130,8 +144,8 @@ static hipError_t launch_slice(ParseVariant v, const ParseArgs& a, hipStream_t s
 hipError_t launch_span_clock(const ParseArgs& a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const uint64_t blocks = (a.count + kTile - 1) / kTile;
-    hipLaunchKernelGGL((k_parse_span<NEXG_OUT_GROUPED, 1, NEXG_SPAN_SUB, NEXG_SPAN_WPE, true>), dim3((uint32_t)blocks),
-                       dim3(kTile), 0, s, a);
+    hipLaunchKernelGGL((k_parse_span<NEXG_OUT_SPARSE, 1, NEXG_SPAN_SUB, NEXG_SPAN_WPE, true>), dim3((uint32_t)blocks),
+                       dim3(kTile), 0, s, grouped_as_sparse(a));
     return hipGetLastError();
 }
 

@@ -645,12 +645,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint64_t off = 0;
     uint32_t len = 0;
     const bool have = t < nf;
-#ifndef NEXG_SPAN_HEAD_LATE
-#define NEXG_SPAN_HEAD_LATE 0
-#endif
-    // every group mixed: head 0 (NEXG_SPAN_HEAD_LATE: with the final stores)
-    if (!NEXG_SPAN_HEAD_LATE && OUT == NEXG_OUT_GROUPED && lane == 0 && have)
-        reinterpret_cast<uint8_t*>(a.out)[idx >> 6] = 0;
+    // NEXG_OUT_GROUPED runs as the SPARSE instance on the grouped output's
+    // code / exception area (the same layout from NEXG_GROUPED_CODE_OFFSET on)
+    // with every group stored mixed: head 0. A GROUPED instance of this kernel
+    // ran the App. C mix 7 % slower than SPARSE on the same batch (register
+    // allocation of the generic section: a spill inside its loop,
+    // profiles/r05/grouped_as_sparse/)
+    if (OUT == NEXG_OUT_SPARSE && a.grouped_heads && lane == 0 && have) a.grouped_heads[idx >> 6] = 0;
+    if (OUT == NEXG_OUT_GROUPED && lane == 0 && have) reinterpret_cast<uint8_t*>(a.out)[idx >> 6] = 0;
     const bool ok = have && frame_extent(a, idx, off, len);
     if (t == 0) s_span[0] = off;
     if (t == nf - 1) s_span[1] = off + len;
@@ -903,8 +905,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // uniformity test and the head store out of the generic section's register
     // budget: with them the App. C mix ran 10 % slower, profiles/r03/grouped)
     NEXG_SPAN_STAMP(4);
-    if (NEXG_SPAN_HEAD_LATE && OUT == NEXG_OUT_GROUPED && lane == 0 && have)
-        reinterpret_cast<uint8_t*>(a.out)[idx >> 6] = 0;
     if (sparse_like(OUT)) store_sparse_coded<OUT, false>(a, idx, have, r, code);
     else if (OUT == NEXG_OUT_DESC && NEXG_DESC_MODE == 2) {  // 256 x 8 B through the slots: 16-B NT stores
         // own slot only (the generic section's reads of other lanes' slots

@@ -24,7 +24,8 @@ for s in ${STEPS:-tests}; do
     nodev) step nodev 600 bash -c 'for w in 1 4; do for l in nex_amd/libnexg.so abvar/libnexg_nodev.so; do NEXG_PROBE_WAVES=$w NEXG_PROBE_WGS=5 python tools/bench_builders.py --probe --lib $l || exit 1; done; done' ;;
     mixprobe) step mix_probe 400 python3 bench.py --steps 20 --warmup 5 --no-large --no-ser --no-cpu-baseline ;;
     headab) step head_ab 600 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_headlate.so --workloads imix,mix,real --out grouped --check --rounds 4 ;;
-    r04ab) step r04_ab 900 env NEXG_AB_LIB_LENIENT=1 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_r04.so,abvar/libnexg_headlate.so --workloads imix,mix,real --out grouped --check --rounds 4 ;;
+    r04ab) step r04_ab 900 env NEXG_AB_LIB_LENIENT=1 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_head.so,abvar/libnexg_r04.so --workloads imix,mix,real --out grouped --check --rounds 4 ;;
+    sparseab) step sparse_ab 600 env NEXG_AB_LIB_LENIENT=1 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_head.so --workloads mix --out sparse --check --rounds 4 ;;
     serab) step ser_ab 300 python -u tools/bench_ser_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_noprobe.so --shape probe --rounds 4 ;;
     descab) step desc_ab 600 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_desc1.so,abvar/libnexg_desc0.so --workloads udp64,imix --out desc --rounds 3 ;;
     newtests) step pytest_new 600 python -u -m pytest tests/test_gpu_sparse.py tests/test_gpu_fixup.py -q -x --timeout 300 --timeout-method thread ;;
