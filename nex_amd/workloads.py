@@ -152,12 +152,15 @@ def tiled(batch, times: int):
 
     from .engine import FrameBatch
     n, span = batch.count, int(batch.offsets[batch.count].item())
-    data = batch.data[:span].repeat(times)
+    # one allocation for the result, filled in place (repeat + cat made two
+    # full-size allocations, the batch living in the second)
+    buf = torch.zeros(times * span + 16, dtype=batch.data.dtype, device=batch.data.device)
+    for k in range(times):
+        buf[k * span:(k + 1) * span].copy_(batch.data[:span])
     base = batch.offsets[:n]
     offs = torch.cat([base + k * span for k in range(times)] +
                      [torch.tensor([times * span], dtype=base.dtype, device=base.device)])
-    pad = torch.zeros(16, dtype=data.dtype, device=data.device)
-    return FrameBatch(data=torch.cat([data, pad])[: times * span], count=n * times, offsets=offs)
+    return FrameBatch(data=buf[: times * span], count=n * times, offsets=offs)
 
 
 #: the real-traffic TCP option shapes of tcp.rs:731-836 timed in bench.py's
