@@ -923,404 +923,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 }
 
 
-// ---- persistent span kernel: the next group's first sub-tile by LDS-DMA ----
-//
-// k_parse_span's per-group work, with each workgroup walking groups g =
-// blockIdx.x + k * gridDim.x (a grid of a few workgroups per CU). When a
-// group's sub-tile loop has consumed the stage buffer, the next group's first
-// sub-tile is requested into it by LDS-DMA (global_load_lds_dwordx4: no
-// VGPRs), so it streams in while this group runs its fast path, instead of
-// after the next group's offset loads (round 4's phase timing: 20 % of a
-// workgroup's life in that start, 23 % in the fast path, neither with a
-// sub-tile in flight). The declined frames' 80-B slots therefore no longer
-// alias the stage buffer: up to kSpanSlots of them sit in the prefix area
-// (idle after the loop), slot numbers from an LDS counter; a group with more
-// re-gathers the rest from HBM into the stage buffer and re-requests the
-// next group's sub-tile after its generic section. Sub-tiles after the first
-// stream through registers as in k_parse_span.
-constexpr uint32_t kSpanSlots = 52;  // declined-frame slots beside the stage buffer
-
-// one 16-B LDS-DMA load per lane: lane l's 16 bytes land at wave_base + 16 l
-__device__ __forceinline__ void glds16(uint64_t gaddr, uint8_t* wave_base) {
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const __attribute__((address_space(1))) void*>(gaddr),
-                                     reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                         reinterpret_cast<uintptr_t>(wave_base)),
-                                     16, 0, 2 /* nt */);
-}
-
-// [lo, hi) of a group of nf frames starting at f0 (uniform): the span bounds
-// k_parse_span takes from its first and last lanes
-__device__ __forceinline__ void span_bounds(const ParseArgs& a, uint64_t f0, uint32_t nf, uint64_t& lo,
-                                            uint64_t& hi) {
-    if (a.offsets) {
-        lo = NEXG_GLOBAL(uint64_t, a.offsets)[f0];
-        hi = a.lengths ? NEXG_GLOBAL(uint64_t, a.offsets)[f0 + nf - 1] + NEXG_GLOBAL(uint32_t, a.lengths)[f0 + nf - 1]
-                       : NEXG_GLOBAL(uint64_t, a.offsets)[f0 + nf];
-    } else {
-        lo = f0 * a.stride;
-        hi = (f0 + nf) * (uint64_t)a.stride;
-    }
-}
-
-// a value every lane holds, in scalar registers (its load waited for here)
-__device__ __forceinline__ uint64_t uni64(uint64_t v) {
-    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-           __builtin_amdgcn_readfirstlane((uint32_t)v);
-}
-
-__device__ __forceinline__ bool span_plausible(const ParseArgs& a, uint64_t lo, uint64_t hi) {
-    return hi >= lo && hi <= a.data_bytes && hi - lo <= (1ull << 30);
-}
-
-template <int OUT, uint32_t SUB = 20480, int WPE = 6, bool TIMING = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_parse_spanp(ParseArgs a) {
-    static_assert(OUT != NEXG_OUT_RECORD, "records stage through the stage buffer: k_parse_span");
-    constexpr uint32_t kStage = kApron + SUB + kApron;
-    constexpr uint32_t kPfx = SUB / 16u + 4u;
-    constexpr uint32_t kSlotBytes = kSpanSlots * SpanFrame::kSlot;
-    constexpr uint32_t kOvfSlots = kTile - kSpanSlots;
-    static_assert(kSlotBytes + kSpanSlots * 16u <= kPfx * 4u, "slots + items fit the prefix area");
-    static_assert(kOvfSlots * SpanFrame::kSlot + kTile * 16u <= kStage, "overflow slots + items fit the stage");
-    static_assert(kTile * 8u <= kPfx * 4u, "descriptor staging fits the prefix area");
-    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[kStage];
-    __shared__ __attribute__((aligned(16))) uint32_t s_pfx[kPfx];
-    __shared__ uint32_t s_wsum[4];
-    __shared__ uint32_t s_hist[2 * kBuckets + 2];  // bucket counts, bases, total, slot counter
-    constexpr int CPT = SUB / 4096u;  // 16-B chunks per thread per sub-tile
-    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    const uint32_t wvu = __builtin_amdgcn_readfirstlane(wv);
-    const uint64_t base = reinterpret_cast<uint64_t>(a.data);
-    const uint64_t ngroups = (a.count + kTile - 1) / kTile;
-    uint8_t* const sb = s_bytes + kApron;
-    uint8_t* const pslots = reinterpret_cast<uint8_t*>(s_pfx);  // after the loop: kSpanSlots slots + items
-    uint32_t& s_nslot = s_hist[2 * kBuckets + 1];
-
-    // group g's span bounds (uniform: scalar registers)
-    auto bounds_of = [&](uint64_t g, uint64_t& lo, uint64_t& hi) {
-        const uint64_t f0 = g * kTile;
-        const uint32_t nf = a.count - f0 < kTile ? (uint32_t)(a.count - f0) : kTile;
-        span_bounds(a, f0, nf, lo, hi);
-    };
-    // the first sub-tile of the span [lo, hi) into the stage buffer by LDS-DMA
-    // (when it is a plausible range of the batch: every load inside its 16-B blocks)
-    auto request_first = [&](uint64_t lo_v, uint64_t hi_v) {
-        const uint64_t lo = uni64(lo_v), hi = uni64(hi_v);
-        if (!span_plausible(a, lo, hi)) return;
-        const uint64_t A0 = (base + lo) & ~15ull;
-        const uint32_t span = (uint32_t)(((base + hi + 15u) & ~15ull) - A0);
-#pragma unroll
-        for (int i = 0; i < CPT; i++) {
-            const uint32_t c = 16u * (t + 256u * i);
-            if (c < span) glds16(A0 + c, sb + 16u * (64u * wvu + 256u * i));
-        }
-    };
-
-    uint64_t g = blockIdx.x;
-    uint64_t lo = 0, hi = 0;  // this group's span bounds (loaded one group ahead)
-    if (g < ngroups) {
-        bounds_of(g, lo, hi);
-        request_first(lo, hi);
-    }
-    for (; g < ngroups; g += gridDim.x) {
-        const uint64_t gn = g + gridDim.x;  // this workgroup's next group
-        lo = uni64(lo);
-        hi = uni64(hi);
-        if constexpr (TIMING) {
-            if (t == 0) a.stamps[g * 8ull + 6] = __builtin_amdgcn_s_memrealtime();
-            if (t == 0) a.stamps[g * 8ull + 0] = __builtin_amdgcn_s_memtime();
-        }
-        const uint64_t f0 = g * kTile;
-        const uint64_t idx = f0 + t;
-        const uint32_t nf = a.count - f0 < kTile ? (uint32_t)(a.count - f0) : kTile;
-        uint64_t off = 0;
-        uint32_t len = 0;
-        const bool have = t < nf;
-        if (OUT == NEXG_OUT_GROUPED && lane == 0 && have) reinterpret_cast<uint8_t*>(a.out)[idx >> 6] = 0;
-        const bool ok = have && frame_extent(a, idx, off, len);
-        // the next group's bounds, loaded behind this group's extent words (one
-        // round trip for both) into scalar registers
-        uint64_t lo_n = 0, hi_n = 0;
-        if (gn < ngroups) {
-            bounds_of(gn, lo_n, hi_n);
-            lo_n = uni64(lo_n);
-            hi_n = uni64(hi_n);
-        }
-        const uint64_t A0 = (base + lo) & ~15ull;
-        const uint32_t span = (uint32_t)(((base + hi + 15u) & ~15ull) - A0);
-        const bool plausible = span_plausible(a, lo, hi);
-        const bool inside = !have || (ok && off >= lo && off + len <= hi);
-        if (t == 0) s_nslot = 0;
-        // this wave's LDS-DMA of the first sub-tile has landed; the barrier
-        // makes every wave's visible
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const bool span_ok = __syncthreads_and(inside) && plausible;
-        if constexpr (TIMING) { if (t == 0) a.stamps[g * 8ull + 1] = __builtin_amdgcn_s_memtime(); }
-        nexg_record r{};
-        if (!span_ok) {  // not packed here: every lane parses its own frame from HBM
-            if (gn < ngroups) request_first(lo_n, hi_n);  // the stage buffer is idle
-            if (have) {
-                if (!ok) {
-                    r.flags = (uint32_t)NEXG_ERR_BAD_EXTENT << NEXG_STATUS_SHIFT;
-                } else {
-                    GlobalFrame f{a.data + off};
-                    parse_frame(f, (uint32_t)((base + off) & 1u), len, a.opt_flags, a.ip_offset, r);
-                }
-            }
-            store_out<OUT>(a, idx, have, r);
-            if constexpr (TIMING) {
-                if (t == 0) a.stamps[g * 8ull + 5] = __builtin_amdgcn_s_memtime();
-                if (t == 0) a.stamps[g * 8ull + 7] = __builtin_amdgcn_s_memrealtime();
-            }
-            lo = lo_n;
-            hi = hi_n;
-            continue;
-        }
-        const uint32_t hr = (uint32_t)(base + off - A0);
-        const bool want_tail = have && len > kLaneWin;
-        const uint32_t sh = (uint32_t)((base + off) & 3u);
-        uint32_t qa = 0, qb = 0, run = 0;
-        uint32_t qend = len;
-        uint32_t u[21];
-#pragma unroll
-        for (int j = 0; j < 21; j++) u[j] = 0;
-        uint4 cur[CPT];
-        auto fetch = [&](uint32_t S, uint4 (&v)[CPT]) {
-#pragma unroll
-            for (int i = 0; i < CPT; i++) {
-                const uint32_t c = S + 16u * (t + 256u * i);
-                v[i] = c < span ? load16g<true>(A0 + c) : make_uint4(0, 0, 0, 0);
-            }
-        };
-        uint32_t* const sp = s_pfx;
-        for (uint32_t S = 0; S < span; S += SUB) {
-            // (1) stage bytes + chunk sums, next sub-tile in flight. Sub-tile 0
-            // arrived by LDS-DMA: its chunks are read back from the stage buffer
-            if (S > 0 && t >= kTile - kApron / 16u) {
-                const uint8_t* prev = sb + SUB - kApron;
-                *reinterpret_cast<uint4*>(sb - kApron + 16u * (t - (kTile - kApron / 16u))) =
-                    *reinterpret_cast<const uint4*>(prev + 16u * (t - (kTile - kApron / 16u)));
-            }
-#pragma unroll
-            for (int i = 0; i < CPT; i++) {
-                const uint32_t c = t + 256u * i;
-                if (S == 0) {
-                    cur[i] = 16u * c < span ? *reinterpret_cast<const uint4*>(sb + 16u * c) : make_uint4(0, 0, 0, 0);
-                } else {
-                    *reinterpret_cast<uint4*>(sb + 16u * c) = cur[i];
-                }
-                sp[c] = chunk_le_sum(cur[i]);
-            }
-            const uint32_t E = S + SUB;
-            if (E < span) fetch(E, cur);
-            __syncthreads();
-            // (2) block exclusive scan of the chunk sums (CPT consecutive per thread)
-            uint32_t cs[CPT];
-            uint32_t own = 0;
-#pragma unroll
-            for (int i = 0; i < CPT; i++) own += (cs[i] = sp[CPT * t + i]);
-            const uint32_t incl = wave_incl_scan_dpp(own);
-            if (lane == 63u) s_wsum[wv] = incl;
-            __syncthreads();
-            const uint4 ws = *reinterpret_cast<const uint4*>(s_wsum);
-            const uint32_t wbase = (wv > 0 ? ws.x : 0u) + (wv > 1 ? ws.y : 0u) + (wv > 2 ? ws.z : 0u);
-            const uint32_t total = ws.x + ws.y + ws.z + ws.w;
-            uint32_t ex = wbase + incl - own;
-#pragma unroll
-            for (int i = 0; i < CPT; i++) {
-                sp[CPT * t + i] = ex;
-                ex += cs[i];
-            }
-            if (t == 0) sp[(SUB / 16u)] = total;
-            __syncthreads();
-            // (3) prefix values at this sub-tile's positions, head window copy
-            const bool last = E >= span;
-            auto q_at = [&](uint32_t d) {
-                const uint32_t c = d >> 4, m = d & 15u;
-                return run + sp[c] + (m ? chunk_prefix_sum(sb + 16u * c, m) : 0u);
-            };
-            const int dh = (int)((hr & ~3u) - S);
-            if (have && dh >= -(int)kLaneWin && (dh <= (int)(SUB - kLaneWin - 4u) || (last && dh < (int)SUB))) {
-#pragma unroll
-                for (int j = 0; j < 21; j++) u[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4 * j);
-                qend = span_tail_end(__builtin_amdgcn_alignbyte(u[4], u[3], sh),
-                                     __builtin_amdgcn_alignbyte(u[5], u[4], sh), len, a.opt_flags);
-            }
-            const uint32_t da = hr + kLaneWin - S, db = hr + qend - S;
-            if (want_tail && (da < SUB || (last && da == SUB))) qa = q_at(da);
-            if (have && (db < SUB || (last && db == SUB))) qb = q_at(db);
-            run += total;
-            __syncthreads();
-        }
-        // the stage buffer is idle until the next group: its first sub-tile
-        // streams in while this group runs its fast path
-        if (gn < ngroups) request_first(lo_n, hi_n);
-        if constexpr (TIMING) { if (t == 0) a.stamps[g * 8ull + 2] = __builtin_amdgcn_s_memtime(); }
-        // (A) every lane: the canonical fast path on its head window; a declined
-        // frame takes a slot number and, when there is one beside the stage
-        // buffer, puts its window there
-        uint32_t code = 0, key = 0, myslot = 0;
-        bool gen = false;
-        const uint32_t tq = want_tail ? qb - qa : 0u;
-        if (have) {
-            uint32_t w[20];
-#pragma unroll
-            for (int k = 0; k < 20; k++) w[k] = __builtin_amdgcn_alignbyte(u[k + 1], u[k], sh);
-            const uint64_t tail = (sh & 1u) ? (uint64_t)tq * 256u : (uint64_t)tq;
-            if (fast_canonical80(w, len, a.opt_flags, tail, qend, r)) {
-                if (sparse_like(OUT)) code = canonical80_code(r);
-            } else {
-                gen = true;
-#pragma unroll
-                for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
-                key = span_bucket(w[3], w[5], a.opt_flags);
-                myslot = atomicAdd(&s_nslot, 1u);
-                if (myslot < kSpanSlots) {
-#pragma unroll
-                    for (int k = 0; k < 5; k++)
-                        reinterpret_cast<uint4*>(pslots + SpanFrame::kSlot * myslot)[k] =
-                            make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-                }
-            }
-        }
-        if constexpr (TIMING) { if (t == 0) a.stamps[g * 8ull + 3] = __builtin_amdgcn_s_memtime(); }
-        // (B) the declined frames, bucketed by (family, L4 protocol), parsed
-        // densely in bucket order (k_parse_span (B)); item = {span position,
-        // len | tail end << 16, tail sum, owner | slot << 8}
-        if (__syncthreads_or(gen)) {
-            const uint32_t nslot = s_nslot;
-            const bool ovf = nslot > kSpanSlots;  // uniform
-            uint8_t* const oslots = sb - kApron;  // overflow slots: the stage buffer
-            auto slot_of = [&](uint32_t sl) {
-                return sl < kSpanSlots ? pslots + SpanFrame::kSlot * sl : oslots + SpanFrame::kSlot * (sl - kSpanSlots);
-            };
-            if (ovf) {
-                // the next group's sub-tile in the stage buffer is given up (requested
-                // again below): every wave's LDS-DMA lands first; overflow frames
-                // re-gather their window from HBM
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (gen && myslot >= kSpanSlots) {
-                    // 21 dwords from the frame's dword-aligned start (each inside the span's 16-B blocks)
-                    const uint64_t a4 = (base + off) & ~3ull, end = A0 + span;
-                    const auto* src = NEXG_GLOBAL(uint32_t, reinterpret_cast<const uint8_t*>(a4));
-                    uint32_t v[21];
-#pragma unroll
-                    for (int k = 0; k < 21; k++) v[k] = a4 + 4u * k + 4u <= end ? src[k] : 0u;
-                    uint32_t w[20];
-#pragma unroll
-                    for (int k = 0; k < 20; k++) {
-                        const uint32_t x = __builtin_amdgcn_alignbyte(v[k + 1], v[k], sh);
-                        w[k] = 4u * k < len ? (x & range_mask(4u * k, 0, len)) : 0u;
-                    }
-#pragma unroll
-                    for (int k = 0; k < 5; k++)
-                        reinterpret_cast<uint4*>(slot_of(myslot))[k] =
-                            make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-                }
-            }
-            if (t < kBuckets) s_hist[t] = 0;
-            __syncthreads();
-            const uint32_t rank = gen ? atomicAdd(&s_hist[key], 1u) : 0u;
-            __syncthreads();
-            if (t == 0) {
-                uint32_t acc = 0;
-                for (uint32_t k = 0; k < kBuckets; k++) {
-                    const uint32_t c = s_hist[k];
-                    s_hist[kBuckets + k] = acc;
-                    acc += c;
-                }
-                s_hist[2 * kBuckets] = acc;
-            }
-            __syncthreads();
-            uint4* const items = ovf ? reinterpret_cast<uint4*>(oslots + kOvfSlots * SpanFrame::kSlot)
-                                     : reinterpret_cast<uint4*>(pslots + kSlotBytes);
-            if (gen) items[s_hist[kBuckets + key] + rank] = make_uint4(hr, len | qend << 16, tq, t | myslot << 8);
-            const uint32_t ngen = s_hist[2 * kBuckets];
-            __syncthreads();
-            const bool work = t < ngen;
-            nexg_record rr{};
-            SpanDeferred dfr{};
-            uint32_t wslot = 0, ghr = 0;
-            if (work) {
-                const uint4 it = items[t];
-                ghr = it.x;
-                wslot = it.w >> 8;
-                SpanFrame f{slot_of(wslot), reinterpret_cast<const uint8_t*>(A0 + ghr), it.y >> 16, ghr & 1u, it.z};
-                parse_frame(f, ghr & 1u, it.y & 0xFFFFu, a.opt_flags, a.ip_offset, rr);
-                dfr = f.d;
-            }
-            uint32_t mine = 0;
-            const uint32_t grp = lane >> 4, gl = lane & 15u;
-            for (uint64_t m = __ballot(dfr.which() != 0u); m;) {
-                const uint64_t curm = m;
-                uint64_t rest = curm;
-                uint32_t pick = 64u;
-#pragma unroll
-                for (uint32_t k = 0; k < 4; k++) {
-                    const uint32_t b = rest ? (uint32_t)__builtin_ctzll(rest) : 64u;
-                    pick = k == grp ? b : pick;
-                    rest &= rest - 1;
-                }
-                m = rest;
-                const int src = (int)(pick & 63u);
-                const uint32_t rg = (uint32_t)__shfl((int)dfr.rng, src, 64);
-                const uint64_t A = A0 + (uint32_t)__shfl((int)ghr, src, 64) + (rg & 0xFFFFu);
-                const uint64_t B = pick < 64u ? A + (rg >> 16) : A;
-                uint32_t sacc = 0;
-                for (uint64_t c = (A & ~15ull) + 16u * gl; c < B; c += 1024u) {
-                    uint4 v[4];
-#pragma unroll
-                    for (uint32_t k = 0; k < 4; k++)
-                        v[k] = c + 256u * k < B ? load16(reinterpret_cast<const void*>(c + 256u * k)) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-                    for (uint32_t k = 0; k < 4; k++) sacc += chunk_range_sum(v[k], c + 256u * k, A, B);
-                }
-                sacc += __shfl_xor(sacc, 8, 16);
-                sacc += __shfl_xor(sacc, 4, 16);
-                sacc += __shfl_xor(sacc, 2, 16);
-                sacc += __shfl_xor(sacc, 1, 16);
-                const uint32_t rk = (uint32_t)__builtin_popcountll(curm & ((1ull << lane) - 1ull));
-                const uint32_t tot = (uint32_t)__shfl((int)sacc, (int)((rk & 3u) << 4), 64);
-                if (((curm >> lane) & 1ull) && rk < 4u) mine = tot;
-            }
-            if (dfr.which()) span_patch(dfr, mine, rr);
-            if (work) {  // the result goes back through the worker's slot
-                const uint32_t c = sparse_like(OUT) ? sparse_encode(rr, a.opt_flags, a.ip_offset) : 0u;
-                *reinterpret_cast<uint4*>(slot_of(wslot)) =
-                    make_uint4(rr.flags, (uint32_t)rr.payload_off | ((uint32_t)rr.payload_len << 16), c, 0u);
-            }
-            __syncthreads();
-            if (gen) {
-                const uint4 v = *reinterpret_cast<const uint4*>(slot_of(myslot));
-                r.flags = v.x;
-                r.payload_off = (uint16_t)v.y;
-                r.payload_len = (uint16_t)(v.y >> 16);
-                code = v.z;
-            }
-            if (ovf) {  // the overflow slots used the stage buffer: request the next group's sub-tile again
-                __syncthreads();
-                if (gn < ngroups) request_first(lo_n, hi_n);
-            }
-        }
-        if constexpr (TIMING) { if (t == 0) a.stamps[g * 8ull + 4] = __builtin_amdgcn_s_memtime(); }
-        if (sparse_like(OUT)) {
-            store_sparse_coded<OUT, false>(a, idx, have, r, code);
-        } else if (OUT == NEXG_OUT_DESC) {  // 256 x 8 B through the idle prefix area: 16-B non-temporal stores
-            __syncthreads();  // the owners' reads of the prefix-area slots are done
-            if (have) stage_desc(pslots + 8u * t, r);
-            __syncthreads();
-            copy_out_descs<8>(pslots, a.out, f0, nf);
-        } else {
-            store_out<OUT>(a, idx, have, r);
-        }
-        if constexpr (TIMING) {
-            if (t == 0) a.stamps[g * 8ull + 5] = __builtin_amdgcn_s_memtime();
-            if (t == 0) a.stamps[g * 8ull + 7] = __builtin_amdgcn_s_memrealtime();
-        }
-        // the next group's first reads of the prefix area follow its start barrier
-        lo = lo_n;
-        hi = hi_n;
-    }
-}
+// (A persistent variant that prefetched the next group's first sub-tile by
+// LDS-DMA was measured in round 5 and removed: every variant spilled, DESIGN.md
+// §6 round 5; it is in the history at commit 2c6e6f3.)
 
 }  // namespace nexg

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--kind", default="clean")
     ap.add_argument("--launches", type=int, default=8)
     ap.add_argument("--share", type=float, default=0.5)
+    ap.add_argument("--old-tiled", action="store_true", help="the round-4 tiled() construction (A/B)")
     args = ap.parse_args()
     import torch
     from nex_amd import abi, workloads
@@ -27,7 +28,17 @@ def main():
     else:
         kinds = workloads.MUTATIONS if args.kind == "all" else (args.kind,)
         base, _ = workloads.malformed_mix(eng, 1 << 20, mutate_share=args.share, kinds=kinds)
-    b = workloads.tiled(base, 16)
+    if args.old_tiled:  # round 4's construction: repeat, then cat with a 16-B pad (two full-size allocations)
+        n, span = base.count, int(base.offsets[base.count].item())
+        data = base.data[:span].repeat(16)
+        offs = torch.cat([base.offsets[:n] + k * span for k in range(16)] +
+                         [torch.tensor([16 * span], dtype=torch.int64, device="cuda")])
+        pad = torch.zeros(16, dtype=data.dtype, device=data.device)
+        from nex_amd.engine import FrameBatch
+        b = FrameBatch(data=torch.cat([data, pad])[: 16 * span], count=n * 16, offsets=offs)
+        del data
+    else:
+        b = workloads.tiled(base, 16)
     out = torch.empty(Engine.out_bytes(abi.OUT_GROUPED, b.count), dtype=torch.uint8, device="cuda")
     for _ in range(args.launches):
         eng.parse(b, out_kind=abi.OUT_GROUPED, out=out)
