@@ -192,6 +192,65 @@ __device__ __forceinline__ uint32_t shared_payload_sum(const uint8_t* pl, uint32
     return *s;
 }
 
+// A shared payload of at most kSmallPay bytes (icmp_ping's "hello"): every
+// lane loads the same dwords (uniform addresses: scalar loads, no barrier)
+// and sums them itself, instead of shared_payload_sum's per-workgroup global
+// loads, LDS atomic and two barriers in front of every tile.
+constexpr uint32_t kSmallPay = 64;
+struct SmallPayload {
+    uint32_t w[kSmallPay / 4];  // payload byte k = byte k & 3 of w[k >> 2] (bytes past n: 0)
+    // k a compile-time index (unrolled loops): no dynamically indexed private array
+    __device__ __forceinline__ uint32_t byte(uint32_t k) const { return (w[k >> 2] >> (8u * (k & 3u))) & 0xFFu; }
+};
+
+__device__ __forceinline__ void load_small_payload(const uint8_t* pl, uint32_t n, SmallPayload& sp, uint32_t& be_sum) {
+    if (n == 0) {  // uniform; pl may be NULL
+#pragma unroll
+        for (uint32_t k = 0; k < kSmallPay / 4; k++) sp.w[k] = 0;
+        be_sum = 0;
+        return;
+    }
+    const uint64_t a = reinterpret_cast<uint64_t>(pl);
+    const uint32_t sh = (uint32_t)(a & 3u);
+    const uniform_u32_ptr src = uniform_u32(reinterpret_cast<const void*>(a & ~3ull));
+    const uint32_t nw = (sh + n + 3u) >> 2;
+    uint32_t raw[kSmallPay / 4 + 1];
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPay / 4 + 1; k++) raw[k] = src[k < nw ? k : nw - 1u];  // clamped: none past n
+    // one empty asm over all 17: the loads issue together, one wait (per-value
+    // statements let the compiler sink each load next to its own wait)
+    asm volatile("" : "+s"(raw[0]), "+s"(raw[1]), "+s"(raw[2]), "+s"(raw[3]), "+s"(raw[4]), "+s"(raw[5]),
+                 "+s"(raw[6]), "+s"(raw[7]), "+s"(raw[8]), "+s"(raw[9]), "+s"(raw[10]), "+s"(raw[11]),
+                 "+s"(raw[12]), "+s"(raw[13]), "+s"(raw[14]), "+s"(raw[15]), "+s"(raw[16]));
+    static_assert(kSmallPay / 4 + 1 == 17, "the asm above names every raw dword");
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPay / 4 + 1; k++) raw[k] = k < nw ? raw[k] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPay / 4; k++) {  // realigned to the payload's first byte, masked to n
+        const uint32_t x = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh);
+        sp.w[k] = 4u * k + 4u <= n ? x : 4u * k >= n ? 0u : x & ((1u << (8u * (n - 4u * k))) - 1u);
+    }
+    uint32_t s = 0;  // BE words from the payload's start (an even L4 offset), odd tail byte high
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPay / 4; k++)  // two BE halfwords per dword (bytes past n are 0)
+        s += bswap16(sp.w[k] & 0xFFFFu) + bswap16(sp.w[k] >> 16);
+    be_sum = s;
+}
+
+// The small payload's words into LDS (s_w, 16 dwords) for byte copies with a
+// run-time count: every wave writes the same (uniform) values itself, so no
+// barrier is needed before its own reads (a wave's LDS operations execute in
+// order). A byte loop over the uniform words in registers was a private array
+// with a dynamic index (scratch), and 64 compile-time guarded stores cost 128
+// scalar instructions per wave.
+__device__ __forceinline__ void stage_small_payload(const SmallPayload& sp, uint32_t* s_w) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPay / 4; k++) v = lane == k ? sp.w[k] : v;
+    if (lane < kSmallPay / 4) s_w[lane] = v;
+}
+
 // MAXS = largest stride the LDS tile holds (0: direct global writes).
 // FULL: per-tuple address, port and id arrays present, MACs from the defaults —
 // every parameter load is unconditional, so a lane issues all five before its
@@ -215,6 +274,8 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     const uint64_t i = first + tid;
     const uint32_t flen = 42u + p.payload_len;
     __shared__ uint32_t s_pay;
+    // (the per-lane small-payload path of k_build_l4 measured slower here:
+    // 1-5 B payloads 0.40-0.51 of 8 TB/s against 0.54-0.62, tools/stride_probe.py)
     const uint64_t pw = shared_payload_sum(p.payload, p.payload_len, &s_pay);
     if (tid < nf) {
 #ifndef NEXG_AOS_NT
@@ -428,51 +489,6 @@ struct L4Args {
     uint32_t tile_order;  // tile_index order (nexg_internal.hpp), as k_build_udp4
 };
 
-// A shared payload of at most kSmallPay bytes (icmp_ping's "hello"): every
-// lane loads the same dwords (uniform addresses: scalar loads, no barrier)
-// and sums them itself, instead of shared_payload_sum's per-workgroup global
-// loads, LDS atomic and two barriers in front of every tile.
-constexpr uint32_t kSmallPay = 64;
-struct SmallPayload {
-    uint32_t w[kSmallPay / 4];  // payload byte k = byte k & 3 of w[k >> 2] (bytes past n: 0)
-    // k a compile-time index (unrolled loops): no dynamically indexed private array
-    __device__ __forceinline__ uint32_t byte(uint32_t k) const { return (w[k >> 2] >> (8u * (k & 3u))) & 0xFFu; }
-};
-
-__device__ __forceinline__ void load_small_payload(const uint8_t* pl, uint32_t n, SmallPayload& sp, uint32_t& be_sum) {
-    if (n == 0) {  // uniform; pl may be NULL
-#pragma unroll
-        for (uint32_t k = 0; k < kSmallPay / 4; k++) sp.w[k] = 0;
-        be_sum = 0;
-        return;
-    }
-    const uint64_t a = reinterpret_cast<uint64_t>(pl);
-    const uint32_t sh = (uint32_t)(a & 3u);
-    const uniform_u32_ptr src = uniform_u32(reinterpret_cast<const void*>(a & ~3ull));
-    const uint32_t nw = (sh + n + 3u) >> 2;
-    uint32_t raw[kSmallPay / 4 + 1];
-#pragma unroll
-    for (uint32_t k = 0; k < kSmallPay / 4 + 1; k++) raw[k] = src[k < nw ? k : nw - 1u];  // clamped: none past n
-    // one empty asm over all 17: the loads issue together, one wait (per-value
-    // statements let the compiler sink each load next to its own wait)
-    asm volatile("" : "+s"(raw[0]), "+s"(raw[1]), "+s"(raw[2]), "+s"(raw[3]), "+s"(raw[4]), "+s"(raw[5]),
-                 "+s"(raw[6]), "+s"(raw[7]), "+s"(raw[8]), "+s"(raw[9]), "+s"(raw[10]), "+s"(raw[11]),
-                 "+s"(raw[12]), "+s"(raw[13]), "+s"(raw[14]), "+s"(raw[15]), "+s"(raw[16]));
-    static_assert(kSmallPay / 4 + 1 == 17, "the asm above names every raw dword");
-#pragma unroll
-    for (uint32_t k = 0; k < kSmallPay / 4 + 1; k++) raw[k] = k < nw ? raw[k] : 0u;
-#pragma unroll
-    for (uint32_t k = 0; k < kSmallPay / 4; k++) {  // realigned to the payload's first byte, masked to n
-        const uint32_t x = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh);
-        sp.w[k] = 4u * k + 4u <= n ? x : 4u * k >= n ? 0u : x & ((1u << (8u * (n - 4u * k))) - 1u);
-    }
-    uint32_t s = 0;  // BE words from the payload's start (an even L4 offset), odd tail byte high
-#pragma unroll
-    for (uint32_t k = 0; k < kSmallPay / 4; k++)  // two BE halfwords per dword (bytes past n are 0)
-        s += bswap16(sp.w[k] & 0xFFFFu) + bswap16(sp.w[k] >> 16);
-    be_sum = s;
-}
-
 // halfword v (memory order: low byte first) at LDS/global byte offset p
 __device__ __forceinline__ void put_hw(uint8_t* base, uint32_t p, uint32_t v, bool odd) {
     if (odd) {
@@ -505,8 +521,13 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
     const bool small = a.payload_len <= kSmallPay;  // uniform
     SmallPayload spay{};
     uint32_t pay_sum = 0;
-    if (small) load_small_payload(a.payload, a.payload_len, spay, pay_sum);
-    else pay_sum = shared_payload_sum(a.payload, a.payload_len, &s_pay);
+    __shared__ uint32_t s_payw[kSmallPay / 4];
+    if (small) {
+        load_small_payload(a.payload, a.payload_len, spay, pay_sum);
+        if (STAGED && a.payload_len) stage_small_payload(spay, s_payw);
+    } else {
+        pay_sum = shared_payload_sum(a.payload, a.payload_len, &s_pay);
+    }
     const uint32_t l4_hdr = KIND == kL4Tcp ? 20u + a.opt_padded : 8u;
     const uint32_t l4_len = l4_hdr + a.payload_len;
     const uint32_t flen = 14u + 2u * NIP + l4_len;
@@ -609,7 +630,10 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
                 if (k < a.opt_padded) put_hw(base, p + k, a.options[k] | ((uint32_t)a.options[k + 1] << 8), odd);
             p += a.opt_padded;
         }
-        if (small) {
+        if (small && STAGED) {
+            const uint8_t* pb = reinterpret_cast<const uint8_t*>(s_payw);
+            for (uint32_t k = 0; k < a.payload_len; k++) base[p + k] = pb[k];
+        } else if (small) {
 #pragma unroll
             for (uint32_t k = 0; k < kSmallPay; k++)
                 if (k < a.payload_len) base[p + k] = (uint8_t)spay.byte(k);

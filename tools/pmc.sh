@@ -16,7 +16,12 @@ for cfg in $CONFIGS; do
     ser_aos) wl=ser; extra="--ser-shape tuples_aos" ;;
     udp64_large) wl=udp64; extra="--frames $((52 << 20))" ;; esac
   for c in FETCH_SIZE WRITE_SIZE; do
-    run ${cfg}_$c 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc/${cfg}_$c -o run -- python3 bench.py --workload $wl --out $out --steps 5 --warmup 1 --no-cpu-baseline --no-imix --no-malformed --no-real --no-large --no-ser $extra
+    case $wl in
+      ser_tcp_ping|ser_icmp_ping|ser_udp6)  # bench.py's ser.<shape> probe objects
+        run ${cfg}_$c 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc/${cfg}_$c -o run -- python3 tools/probe_run.py --shape ${wl#ser_} ;;
+      *)
+        run ${cfg}_$c 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc/${cfg}_$c -o run -- python3 bench.py --workload $wl --out $out --steps 5 --warmup 1 --no-cpu-baseline --no-imix --no-malformed --no-real --no-large --no-ser $extra ;;
+    esac
   done
 done
 echo done
