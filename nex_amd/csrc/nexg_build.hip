@@ -274,8 +274,9 @@ __global__ __launch_bounds__(256) void k_build_udp4(BuildArgs a) {
     const uint64_t i = first + tid;
     const uint32_t flen = 42u + p.payload_len;
     __shared__ uint32_t s_pay;
-    // (the per-lane small-payload path of k_build_l4 measured slower here:
-    // 1-5 B payloads 0.40-0.51 of 8 TB/s against 0.54-0.62, tools/stride_probe.py)
+    // (the ICMP/TCP builder's wave-0 small-payload path measured slower here:
+    // 1-5 B payloads 0.43-0.47 of 8 TB/s against 0.52-0.55 in one session,
+    // profiles/r05/payload/: udp_ping's lean per-lane work does not hide it)
     const uint64_t pw = shared_payload_sum(p.payload, p.payload_len, &s_pay);
     if (tid < nf) {
 #ifndef NEXG_AOS_NT
@@ -521,8 +522,21 @@ __global__ __launch_bounds__(256) void k_build_l4(L4Args a) {
     const bool small = a.payload_len <= kSmallPay;  // uniform
     SmallPayload spay{};
     uint32_t pay_sum = 0;
-    __shared__ uint32_t s_payw[kSmallPay / 4];
-    if (small) {
+    __shared__ uint32_t s_payw[kSmallPay / 4 + 1];  // the staged words, then their sum
+    if (small && STAGED) {
+        // staged tile: wave 0 realigns and sums the payload once for the
+        // workgroup (the other waves skip ~100 VALU instructions each): icmp_ping's
+        // 47-B batch 0.525 -> 0.70 of 8 TB/s written (profiles/r05/payload/)
+        if (a.payload_len) {  // uniform
+            if (tid < 64u) {
+                load_small_payload(a.payload, a.payload_len, spay, pay_sum);
+                stage_small_payload(spay, s_payw);
+                if (tid == 0) s_payw[kSmallPay / 4] = pay_sum;
+            }
+            __syncthreads();
+            pay_sum = s_payw[kSmallPay / 4];
+        }
+    } else if (small) {
         load_small_payload(a.payload, a.payload_len, spay, pay_sum);
         if (STAGED && a.payload_len) stage_small_payload(spay, s_payw);
     } else {

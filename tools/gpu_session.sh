@@ -30,7 +30,7 @@ for s in ${STEPS:-tests}; do
     counters) step counters 120 bash -c 'rocprofv3 -L > gpurun_out/rocprof_counters.txt 2>&1 || rocprofv3 --list-avail > gpurun_out/rocprof_counters.txt 2>&1; true' ;;
     drift) step drift 600 bash -c 'python -u tools/placement_ab.py --workload mix --drift 8 && python -u tools/placement_ab.py --workload real --drift 6' ;;
     tlb) step tlb 900 bash tools/tlb_pmc.sh ;;
-    stride) step stride 600 python -u tools/stride_probe.py ;;
+    stride) step stride 600 bash -c 'python -u tools/stride_probe.py && NEXG_AB_LIB_LENIENT=1 python -u tools/stride_probe.py --lib abvar/libnexg_head.so' ;;
     tstride) step template_stride 600 python -u tools/template_stride.py ;;
     serab) step ser_ab 300 python -u tools/bench_ser_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_noprobe.so --shape probe --rounds 4 ;;
     descab) step desc_ab 600 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_desc1.so,abvar/libnexg_desc0.so --workloads udp64,imix --out desc --rounds 3 ;;

@@ -13,9 +13,16 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", default=None, help="another build of libnexg.so (A/B)")
+    ap.add_argument("--payloads", default="0,1,4,5,6,22,25,26")
+    args = ap.parse_args()
     import torch
-    from nex_amd import probes
+    from nex_amd import _lib, probes
     from nex_amd.engine import Engine
+    if args.lib:
+        _lib._lib, _lib.LIB_PATH = None, os.path.abspath(args.lib)
     eng = Engine(0)
     n = 16 << 20
     g = torch.Generator(device="cuda").manual_seed(7)
@@ -25,7 +32,7 @@ def main():
     macs = (b"\x02\0\0\0\0\1", b"\x02\0\0\0\0\2")
     out = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
     res = {}
-    for plen in (0, 1, 4, 5, 6, 22, 25, 26):
+    for plen in (int(x) for x in args.payloads.split(",")):
         pay = torch.tensor(list(range(1, plen + 1)), dtype=torch.uint8, device="cuda") if plen else None
         L = 42 + plen
         shapes = {
@@ -47,7 +54,7 @@ def main():
             ms = e0.elapsed_time(e1) / 20
             res[f"{name}_{L}B"] = {"kernel_ms": round(ms, 4), "frac_written": round(n * L / (ms * 1e-3) / 8e12, 4)}
             print(name, L, res[f"{name}_{L}B"], flush=True)
-    print(json.dumps(res), flush=True)
+    print(json.dumps({"lib": args.lib or "default", **res}), flush=True)
 
 
 if __name__ == "__main__":
