@@ -32,6 +32,8 @@ for s in ${STEPS:-tests}; do
     tlb) step tlb 900 bash tools/tlb_pmc.sh ;;
     stride) step stride 600 bash -c 'python -u tools/stride_probe.py && NEXG_AB_LIB_LENIENT=1 python -u tools/stride_probe.py --lib abvar/libnexg_head.so' ;;
     tstride) step template_stride 600 python -u tools/template_stride.py ;;
+    fresh) step fresh 600 bash -c 'python -u tools/placement_ab.py --workload real --fresh 8' ;;
+    freshpmc) step fresh_pmc 1000 bash tools/fresh_pmc.sh ;;
     serab) step ser_ab 300 python -u tools/bench_ser_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_noprobe.so --shape probe --rounds 4 ;;
     descab) step desc_ab 600 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_desc1.so,abvar/libnexg_desc0.so --workloads udp64,imix --out desc --rounds 3 ;;
     newtests) step pytest_new 600 python -u -m pytest tests/test_gpu_sparse.py tests/test_gpu_fixup.py -q -x --timeout 300 --timeout-method thread ;;

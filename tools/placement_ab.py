@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--copies", type=int, default=6)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--drift", type=int, default=0, help="rounds of original / copy alternated (0: copies mode)")
+    ap.add_argument("--fresh", type=int, default=0, help="N copies in N live allocations, each timed twice")
     args = ap.parse_args()
     import torch
     from nex_amd import abi, workloads
@@ -49,6 +50,21 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / args.steps
 
+    if args.fresh:  # N copies kept alive (N distinct allocations), each timed twice
+        copies = []
+        rows = []
+        for k in range(args.fresh):
+            data = torch.empty_like(b.data)
+            data.copy_(b.data)
+            copies.append(FrameBatch(data=data, count=b.count, offsets=b.offsets))
+        for r in range(2):
+            for k, c in enumerate(copies):
+                ms = time_batch(c)
+                rows.append({"round": r, "copy": k, "ptr": hex(c.data.data_ptr()), "kernel_ms": round(ms, 4),
+                             "frac": round(b.total_bytes / (ms * 1e-3) / 8e12, 4)})
+                print(json.dumps(rows[-1]), flush=True)
+        print(json.dumps({"workload": args.workload, "bytes": b.total_bytes, "fresh": rows}), flush=True)
+        return
     if args.drift:  # the batch as built and one copy, alternated: drift over time vs placement
         data = torch.empty_like(b.data)
         data.copy_(b.data)
