@@ -767,7 +767,7 @@ hipError_t launch_build_icmp_echo(const nexg_icmp_echo_build& p, uint8_t* out, u
 // batch base sum plus the destination's halfwords), and copies the tile out
 // with 16-B non-temporal stores.
 // Used for tcp_ping (IPv4 / IPv6) and udp_ping's IPv6 batch, where it beats
-// the per-lane builders (tcp_ping 0.75-0.79 of 8 TB/s written against
+// the per-lane builders (tcp_ping 0.72-0.89 of 8 TB/s written against
 // 0.70-0.73); udp_ping's IPv4 batch and the ICMP shapes stay per lane
 // (profiles/r05/probe/). A persistent sweep over the tiles and one-wave
 // workgroups were measured and lose (writes at 0.65-0.72 of 8 TB/s in a
@@ -826,8 +826,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_build_probe(ProbeArgs a) {
     // chain and ds_bpermute; the device payload and source bytes are loaded
     // into place, so they are part of the pattern and not patched per frame
     uint8_t* const tp = s_tile + KCH * 16u * kT;  // 2 x kProbeMaxP + 32 B
-    // the first tile's destinations go in flight (clamped index: an
-    // unconditional load; lanes past the batch's end reload its last frame)
+    // this lane's destination goes in flight (clamped index: an unconditional
+    // load; lanes past the batch's end reload its last frame)
     NEXG_BUILD_STAMP(0);
     NEXG_BUILD_STAMP(6);
     const uint64_t tile = tile_index(a.tile_order);
@@ -838,26 +838,26 @@ __global__ __launch_bounds__(64 * WAVES) void k_build_probe(ProbeArgs a) {
 #pragma unroll
         for (uint32_t k = 0; k < DW; k++) dw[k] = d4[k];
     }
-    // the batch's device source and payload by scalar loads (uniform
-    // addresses through the scalar cache: a vector load of one line by every
-    // workgroup of the grid makes that line's L2 channel the bottleneck), and
-    // their BE word sums computed from them (no reduction)
+    // the batch's device source by scalar loads (uniform addresses through the
+    // scalar cache: a vector load of one line by every workgroup of the grid
+    // makes that line's L2 channel the bottleneck) and its BE word sum
     uint32_t sx[DW], ssum = 0;
 #pragma unroll
     for (uint32_t k = 0; k < DW; k++) sx[k] = 0;
-#ifndef NEXG_PROBE_NODEV
-#define NEXG_PROBE_NODEV 0  // A/B builds only: no device source / payload loads (wrong bytes)
-#endif
-    if (a.src && !NEXG_PROBE_NODEV) {  // 4-B aligned
+    if (a.src) {  // 4-B aligned
 #pragma unroll
         for (uint32_t k = 0; k < DW; k++) sx[k] = uniform_u32(a.src)[k];
 #pragma unroll
         for (uint32_t k = 0; k < DW; k++) ssum += bswap16(sx[k] & 0xFFFFu) + bswap16(sx[k] >> 16);
     }
-    SmallPayload spay;
-    uint32_t psum;
-    load_small_payload(a.payload, NEXG_PROBE_NODEV ? 0u : a.pay_len, spay, psum);  // realigned words, 0 past pay_len
+    uint32_t* const psum_lds = reinterpret_cast<uint32_t*>(tp) + (kProbeMaxP + 32u) / 4u;  // past the pattern
     if (t < 64u) {
+        // the payload (scalar loads) realigned and summed by wave 0 only; its
+        // sum reaches the other waves through LDS
+        SmallPayload spay;
+        uint32_t psum0;
+        load_small_payload(a.payload, a.pay_len, spay, psum0);  // realigned words, 0 past pay_len
+        if (t == 0) *psum_lds = psum0;
         // template, source and payload words handed to lane k by cndmask
         // chains, then each pattern byte picked by ds_bpermute from the lane
         // holding it (one per source: the source lane returns its own copy of
@@ -884,6 +884,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_build_probe(ProbeArgs a) {
         if (4u * t < P + 24u) reinterpret_cast<uint32_t*>(tp)[t] = d;
     }
     __syncthreads();
+    const uint32_t psum = *psum_lds;
     const uint32_t step = (16u * kT) % P, r0 = (16u * t) % P;
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     // the pattern over the tile: chunk c = bytes [(16 c) mod P, + 16) of the
@@ -1083,7 +1084,8 @@ static bool try_probe_l4(const L4Args& l, int kind, uint8_t* out, uint32_t out_s
     const uint32_t flen = 14u + l3 + l4_len;
     // tcp_ping only: the ICMP shapes run faster per lane (0.44 / 0.57 of 8 TB/s
     // against 0.41 / 0.37 for the template kernel, profiles/r05/probe/)
-    if (kind != kL4Tcp || !probe_launch_ok(flen, out_stride, l.payload_len, out)) return false;
+    static const bool icmp_template = probe_env("NEXG_PROBE_ICMP", 0u, 0u, 1u) == 1u;  // measurement override
+    if ((kind != kL4Tcp && !icmp_template) || !probe_launch_ok(flen, out_stride, l.payload_len, out)) return false;
     ProbeArgs a{};
     uint8_t t[kProbeMaxP] = {0};
     const uint8_t zero[16] = {0};

@@ -34,6 +34,7 @@ for s in ${STEPS:-tests}; do
     tstride) step template_stride 600 python -u tools/template_stride.py ;;
     fresh) step fresh 600 bash -c 'python -u tools/placement_ab.py --workload real --fresh 8' ;;
     freshpmc) step fresh_pmc 1000 bash tools/fresh_pmc.sh ;;
+    icmpab) step icmp_ab 600 bash -c 'python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 NEXG_PROBE_WGS=3 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 NEXG_PROBE_WGS=0 python tools/bench_builders.py --probe' ;;
     serab) step ser_ab 300 python -u tools/bench_ser_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_noprobe.so --shape probe --rounds 4 ;;
     descab) step desc_ab 600 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_desc1.so,abvar/libnexg_desc0.so --workloads udp64,imix --out desc --rounds 3 ;;
     newtests) step pytest_new 600 python -u -m pytest tests/test_gpu_sparse.py tests/test_gpu_fixup.py -q -x --timeout 300 --timeout-method thread ;;
