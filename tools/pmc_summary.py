@@ -5,7 +5,8 @@ bytes for the parse path of each workload.
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. On gfx950, FETCH_SIZE counts
 exactly half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md
 §HBM), so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
-Only nexg:: kernels count; generator kernels (k_gen_*), calibration streams (k_probe_*), the
+Only nexg:: kernels count; generator kernels (k_gen_*), calibration kernels (k_probe_*,
+k_chase*, the stamped k_parse_span<..., true> instance), the
 real-traffic batch's one checksum fix-up (k_recompute) and torch setup kernels are skipped.
 
 usage: tools/pmc_summary.py <pmc dir> <out dir>   (writes pmc_summary.json and
@@ -30,9 +31,12 @@ def main():
         vals = defaultdict(list)
         with open(path) as f:
             for r in csv.DictReader(f):
-                if "nexg::" not in r["Kernel_Name"] or "k_gen_" in r["Kernel_Name"] or "k_probe_" in r["Kernel_Name"] \
-                        or "k_recompute" in r["Kernel_Name"]:
+                kn = r["Kernel_Name"]
+                if "nexg::" not in kn or "k_gen_" in kn or "k_probe_" in kn or "k_recompute" in kn or "k_chase" in kn:
                     continue
+                if "k_parse_span" in kn and kn.split("(")[0].rstrip().endswith("true>"):
+                    continue  # the stamped calibration instance (nexg_probe_span_clock), one launch per object
+
                 vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
         for kern, v in vals.items():
             kb = sum(v) / len(v)
