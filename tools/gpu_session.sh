@@ -33,6 +33,7 @@ for s in ${STEPS:-tests}; do
     stride) step stride 600 bash -c 'python -u tools/stride_probe.py && NEXG_AB_LIB_LENIENT=1 python -u tools/stride_probe.py --lib abvar/libnexg_head.so' ;;
     tstride) step template_stride 600 python -u tools/template_stride.py ;;
     fresh) step fresh 600 bash -c 'python -u tools/placement_ab.py --workload real --fresh 8' ;;
+    reserve) step reserve 900 bash -c 'python -u tools/placement_ab.py --workload real --fresh 6 --reserve 32 && python -u tools/placement_ab.py --workload imix --fresh 6 && python -u tools/placement_ab.py --workload imix --fresh 6 --reserve 32' ;;
     freshpmc) step fresh_pmc 1000 bash tools/fresh_pmc.sh ;;
     icmpab) step icmp_ab 600 bash -c 'python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 NEXG_PROBE_WGS=3 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 NEXG_PROBE_WGS=0 python tools/bench_builders.py --probe' ;;
     serab) step ser_ab 300 python -u tools/bench_ser_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_noprobe.so --shape probe --rounds 4 ;;

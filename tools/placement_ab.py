@@ -22,11 +22,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--drift", type=int, default=0, help="rounds of original / copy alternated (0: copies mode)")
     ap.add_argument("--fresh", type=int, default=0, help="N copies in N live allocations, each timed twice")
+    ap.add_argument("--reserve", type=int, default=0, help="GiB allocated (unused) before anything else")
     args = ap.parse_args()
     import torch
     from nex_amd import abi, workloads
     from nex_amd.engine import Engine, FrameBatch
     eng = Engine(0)
+    reserve = torch.empty(args.reserve << 30, dtype=torch.uint8, device="cuda") if args.reserve else None  # noqa: F841
     if args.workload == "imix":
         b = eng.gen_batch(abi.WL_IMIX, 16 << 20)
     else:
