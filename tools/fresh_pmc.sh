@@ -7,9 +7,12 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/fresh_pmc
 export TMPDIR=/tmp
-for set in "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum" \
-           "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_HIT_sum TCC_MISS_sum" \
-           "GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE"; do
+# SET="<counters>" runs that one set only
+sets=("TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum"
+      "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_HIT_sum TCC_MISS_sum"
+      "GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE")
+[ -n "$SET" ] && sets=("$SET")
+for set in "${sets[@]}"; do
   tag=$(echo $set | cut -d' ' -f1 | tr 'A-Z' 'a-z')
   timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/fresh_pmc/$tag -o run -- python3 tools/placement_ab.py --workload real --fresh 8 > gpurun_out/fresh_pmc/$tag.log 2>&1
   rc=$?; echo "$tag rc=$rc"; [ $rc -ne 0 ] && exit $rc
