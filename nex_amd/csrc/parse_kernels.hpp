@@ -622,6 +622,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 // sub-tile k also retires every lookup into sub-tile k-2's buffer (3 barriers
 // per sub-tile, ~42 KB LDS); NB = 1 (the library's): one buffer and a 4th
 // barrier (~25 KB LDS, 6 workgroups per CU).
+#ifndef NEXG_SPAN_NT
+#define NEXG_SPAN_NT true  // sub-tile fetch cache policy (A/B builds override)
+#endif
 template <int OUT, int NB = 1, uint32_t SUB = 16384, int WPE = 1, bool TIMING = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_parse_span(ParseArgs a) {
     // each stage buffer: [96-B apron | SUB bytes | 96-B pad]; the apron holds
@@ -669,7 +672,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int i = 0; i < CPT; i++) {
             const uint32_t c = S + 16u * (t + 256u * i);
-            v[i] = c < span ? load16g<true>(A0 + c) : make_uint4(0, 0, 0, 0);
+            v[i] = c < span ? load16g<NEXG_SPAN_NT>(A0 + c) : make_uint4(0, 0, 0, 0);
         }
     };
     const bool plausible = hi >= lo && hi <= a.data_bytes && hi - lo <= (1ull << 30);

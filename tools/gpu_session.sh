@@ -35,6 +35,14 @@ for s in ${STEPS:-tests}; do
     fresh) step fresh 600 bash -c 'python -u tools/placement_ab.py --workload real --fresh 8' ;;
     reserve) step reserve 900 bash -c 'python -u tools/placement_ab.py --workload real --fresh 6 --reserve 32 && python -u tools/placement_ab.py --workload imix --fresh 6 && python -u tools/placement_ab.py --workload imix --fresh 6 --reserve 32' ;;
     freshpmc) step fresh_pmc 1000 bash tools/fresh_pmc.sh ;;
+    contigclk) step contig_clk 600 bash -c 'python -u tools/contig_ab.py --workload real --map 12 --clock' ;;
+    contiglat) step contig_lat 600 bash -c 'python -u tools/contig_ab.py --workload real --map 12 --latency' ;;
+    contigout) step contig_out 600 bash -c 'python -u tools/contig_ab.py --workload real --map 12 --outs flags,desc,sparse,fresh_grouped' ;;
+    contignt) step contig_nt 600 bash -c 'python -u tools/contig_ab.py --workload real --map 16 --libs abvar/libnexg_spant.so,abvar/libnexg_sub24576.so' ;;
+    contigspan) step contig_span 600 bash -c 'python -u tools/contig_ab.py --workload real --map 24' ;;
+    contigsub) step contig_sub 600 bash -c 'python -u tools/contig_ab.py --workload real --map 24 --libs abvar/libnexg_sub12288.so,abvar/libnexg_sub16384.so,abvar/libnexg_sub24576.so' ;;
+    contigmap) step contig_map 600 bash -c 'python -u tools/contig_ab.py --workload real --map 32' ;;
+    contig) step contig 600 bash -c 'python -u tools/contig_ab.py --workload real --copies 4 && python -u tools/contig_ab.py --workload imix --copies 3' ;;
     icmpab) step icmp_ab 600 bash -c 'python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 NEXG_PROBE_WGS=3 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 NEXG_PROBE_WGS=0 python tools/bench_builders.py --probe' ;;
     spanorder) step span_order 1000 bash -c 'for o in linear xcd xcd2 xcd8; do echo "order $o"; NEXG_TILE_ORDER=$o python -u tools/placement_ab.py --workload real --fresh 4 || exit 1; done' ;;
     freshpmc2) step fresh_pmc 1000 env SET="TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_GMI_CREDIT_STALL_sum TCC_EA0_RDREQ_IO_CREDIT_STALL_sum TCC_EA0_RDREQ_LEVEL_sum" bash tools/fresh_pmc.sh ;;
