@@ -73,10 +73,10 @@ ParseVariant choose_parse_variant(const ParseArgs& a) {
 }
 
 #ifndef NEXG_SPAN_SUB
-#define NEXG_SPAN_SUB 20480  // span kernel sub-tile bytes (A/B builds override)
+#define NEXG_SPAN_SUB 24576  // span kernel sub-tile bytes (A/B builds override)
 #endif
 #ifndef NEXG_SPAN_WPE
-#define NEXG_SPAN_WPE 6  // span kernel waves per SIMD (its VGPR cap)
+#define NEXG_SPAN_WPE 5  // span kernel waves per SIMD (its VGPR cap)
 #endif
 
 // The span kernel's NEXG_OUT_GROUPED output: every group mixed (head 0), so
@@ -105,10 +105,12 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
             hipLaunchKernelGGL((k_parse<1, OUT, 0, 128>), grid, block, 0, s, a);
             break;
         case ParseVariant::SpanTile:
-            // 20-KiB sub-tiles at 6 waves/SIMD (80 VGPRs, 26 KB LDS, 6 workgroups
-            // per CU: 120 KB in flight per CU): +2.6 % over 16 KiB on IMIX in the
-            // same process, 24 KiB at 5 waves equal, 28-32 KiB slower
-            // (profiles/r02_kbench/kbench_subtile.log). Records (about 100
+            // 24-KiB sub-tiles at 5 waves/SIMD (31 KB LDS, 5 workgroups per CU:
+            // 120 KB in flight per CU): in one process +0.9 % over 20 KiB at 6
+            // waves on IMIX and real traffic, the mix equal
+            // (profiles/r05/subtile_ab.log; round 2 had measured 20 KiB +2.6 %
+            // over 16 KiB and 24 KiB equal, 28-32 KiB slower:
+            // profiles/r02_kbench/kbench_subtile.log). Records (about 100
             // VGPRs) run uncapped on 16 KiB: capping them spills 44+ B.
             // (Two-barrier / double-buffered generations measured slower,
             // 0.66-0.69 vs 0.75: tools/kbench.hip keeps them for A/B.)
