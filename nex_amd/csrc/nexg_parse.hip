@@ -107,7 +107,9 @@ static hipError_t launch_parse_out(ParseVariant v, const ParseArgs& a, hipStream
         case ParseVariant::SpanTile:
             // 24-KiB sub-tiles at 5 waves/SIMD (31 KB LDS, 5 workgroups per CU:
             // 120 KB in flight per CU): in one process +0.9 % over 20 KiB at 6
-            // waves on IMIX and real traffic, the mix equal
+            // waves on IMIX and real traffic, the mix equal. 4 waves (24 or 28
+            // KiB) run IMIX +1.9 % and real +1.4 % but the App. C mix -5.8 %:
+            // its generic section needs the fifth workgroup to hide its latency
             // (profiles/r05/subtile_ab.log; round 2 had measured 20 KiB +2.6 %
             // over 16 KiB and 24 KiB equal, 28-32 KiB slower:
             // profiles/r02_kbench/kbench_subtile.log). Records (about 100
