@@ -41,9 +41,9 @@ for s in ${STEPS:-tests}; do
     contigclk) step contig_clk 600 bash -c 'python -u tools/contig_ab.py --workload real --map 12 --clock' ;;
     contiglat) step contig_lat 600 bash -c 'python -u tools/contig_ab.py --workload real --map 12 --latency' ;;
     contigout) step contig_out 600 bash -c 'python -u tools/contig_ab.py --workload real --map 12 --outs flags,desc,sparse,fresh_grouped' ;;
-    contignt) step contig_nt 600 bash -c 'python -u tools/contig_ab.py --workload real --map 16 --libs abvar/libnexg_spant.so,abvar/libnexg_sub24576.so' ;;
+    contignt) step contig_nt 600 bash -c 'python -u tools/contig_ab.py --workload real --map 16 --libs abvar/libnexg_sub20480.so' ;;
     contigspan) step contig_span 600 bash -c 'python -u tools/contig_ab.py --workload real --map 24' ;;
-    contigsub) step contig_sub 600 bash -c 'python -u tools/contig_ab.py --workload real --map 24 --libs abvar/libnexg_sub12288.so,abvar/libnexg_sub16384.so,abvar/libnexg_sub24576.so' ;;
+    contigsub) step contig_sub 600 bash -c 'python -u tools/contig_ab.py --workload real --map 24 --libs abvar/libnexg_sub20480.so,abvar/libnexg_sub28672.so' ;;
     contigmap) step contig_map 600 bash -c 'python -u tools/contig_ab.py --workload real --map 32' ;;
     contig) step contig 600 bash -c 'python -u tools/contig_ab.py --workload real --copies 4 && python -u tools/contig_ab.py --workload imix --copies 3' ;;
     icmpab) step icmp_ab 600 bash -c 'python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 NEXG_PROBE_WGS=3 python tools/bench_builders.py --probe && NEXG_PROBE_ICMP=1 NEXG_PROBE_WAVES=8 NEXG_PROBE_WGS=0 python tools/bench_builders.py --probe' ;;
