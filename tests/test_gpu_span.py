@@ -110,3 +110,35 @@ def test_partial_groups(engine, oracle, mixed, count):
     want = _oracle_same_layout(oracle, batch)
     got = engine.parse_to_numpy(batch, out_kind=abi.OUT_RECORD)
     helpers.records_equal(got, want, None, f"count={count}")
+
+
+class _ShiftedOffsets:
+    """An offset table copied to `shift` bytes past a 16-B aligned device
+    buffer: FrameBatch.to_c reads only data_ptr()."""
+
+    def __init__(self, offsets, shift):
+        import torch
+        n = offsets.numel() * 8
+        self.buf = torch.zeros(n + 16, dtype=torch.uint8, device=offsets.device)
+        self.buf[shift: shift + n].copy_(offsets.view(torch.uint8))
+        self.shift = shift
+
+    def data_ptr(self):
+        return self.buf.data_ptr() + self.shift
+
+
+@pytest.mark.parametrize("shift", [4, 1])
+def test_packed_offsets_table_alignment(engine, mixed, shift):
+    """An offset table at 4 mod 8 or at an odd address gives the aligned
+    table's output (the span kernel reads it with per-lane loads; scalar loads
+    of its span bounds would need dword alignment and measured 0.1-0.5 %
+    slower, profiles/r05/scalar_bounds_ab.log)."""
+    batch = FrameBatch.from_packed(mixed, pad_to=1, shift=0)
+    moved = FrameBatch(data=batch.data, count=batch.count, offsets=_ShiftedOffsets(batch.offsets, shift))
+    import torch
+    for kind in (abi.OUT_RECORD, abi.OUT_GROUPED, abi.OUT_DESC):
+        n = max(engine.out_bytes(kind, batch.count), 16)
+        want, got = (torch.zeros(n, dtype=torch.uint8, device=batch.data.device) for _ in range(2))
+        engine.parse(batch, out_kind=kind, out=want)
+        engine.parse(moved, out_kind=kind, out=got)
+        assert torch.equal(got, want), kind

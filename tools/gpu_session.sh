@@ -35,6 +35,7 @@ for s in ${STEPS:-tests}; do
     fresh) step fresh 600 bash -c 'python -u tools/placement_ab.py --workload real --fresh 8' ;;
     reserve) step reserve 900 bash -c 'python -u tools/placement_ab.py --workload real --fresh 6 --reserve 32 && python -u tools/placement_ab.py --workload imix --fresh 6 && python -u tools/placement_ab.py --workload imix --fresh 6 --reserve 32' ;;
     freshpmc) step fresh_pmc 1000 bash tools/fresh_pmc.sh ;;
+    boundsab) step bounds_ab 700 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_lanebounds.so --workloads imix,mix,real --out grouped --check --rounds 4 ;;
     phasesab) step phases_ab 600 python -u tools/span_phases_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_sub24w4.so ;;
     subab3) step sub_ab3 600 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_sub28672.so,abvar/libnexg_sub24w4.so --workloads imix,mix,real --out grouped --check --rounds 3 ;;
     subab2) step sub_ab2 600 bash -c 'python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_sub20480.so --workloads imix,real --out desc --check --rounds 3 && python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_sub20480.so --workloads imix,mix,real --out grouped --check --rounds 3' ;;
