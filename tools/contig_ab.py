@@ -40,6 +40,65 @@ class RawBuf:
         self.hip.hipFree(ctypes.c_void_p(self.ptr))
 
 
+class _Loc(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int), ("id", ctypes.c_int)]
+
+
+class _AllocFlags(ctypes.Structure):
+    _fields_ = [("compressionType", ctypes.c_ubyte), ("gpuDirectRDMACapable", ctypes.c_ubyte),
+                ("usage", ctypes.c_ushort)]
+
+
+class _AllocProp(ctypes.Structure):  # hipMemAllocationProp
+    _fields_ = [("type", ctypes.c_int), ("requestedHandleType", ctypes.c_int), ("location", _Loc),
+                ("win32HandleMetaData", ctypes.c_void_p), ("allocFlags", _AllocFlags)]
+
+
+class _AccessDesc(ctypes.Structure):  # hipMemAccessDesc
+    _fields_ = [("location", _Loc), ("flags", ctypes.c_int)]
+
+
+class VmmBuf:
+    """A device allocation through the virtual memory API: one physical
+    handle (hipMemCreate) mapped into a reserved range aligned to `align`."""
+
+    def __init__(self, hip, nbytes, align=1 << 30, device=0):
+        prop = _AllocProp(type=1, requestedHandleType=0, location=_Loc(1, device))
+        g = ctypes.c_size_t()
+        rc = hip.hipMemGetAllocationGranularity(ctypes.byref(g), ctypes.byref(prop), ctypes.c_int(1))
+        if rc != 0:
+            raise RuntimeError(f"hipMemGetAllocationGranularity = {rc}")
+        self.gran = g.value
+        size = (nbytes + self.gran - 1) // self.gran * self.gran
+        p, h = ctypes.c_void_p(), ctypes.c_void_p()
+        for call, args in (("hipMemAddressReserve", (ctypes.byref(p), ctypes.c_size_t(size), ctypes.c_size_t(align),
+                                                      None, ctypes.c_ulonglong(0))),
+                           ("hipMemCreate", (ctypes.byref(h), ctypes.c_size_t(size), ctypes.byref(prop),
+                                             ctypes.c_ulonglong(0)))):
+            rc = getattr(hip, call)(*args)
+            if rc != 0:
+                raise RuntimeError(f"{call} = {rc}")
+        rc = hip.hipMemMap(p, ctypes.c_size_t(size), ctypes.c_size_t(0), h, ctypes.c_ulonglong(0))
+        if rc != 0:
+            raise RuntimeError(f"hipMemMap = {rc}")
+        desc = _AccessDesc(location=_Loc(1, device), flags=3)
+        rc = hip.hipMemSetAccess(p, ctypes.c_size_t(size), ctypes.byref(desc), ctypes.c_size_t(1))
+        if rc != 0:
+            raise RuntimeError(f"hipMemSetAccess = {rc}")
+        self.hip, self.ptr, self.h, self.size, self.nbytes = hip, p.value, h, size, nbytes
+
+    def data_ptr(self):
+        return self.ptr
+
+    def numel(self):
+        return self.nbytes
+
+    def free(self):
+        self.hip.hipMemUnmap(ctypes.c_void_p(self.ptr), ctypes.c_size_t(self.size))
+        self.hip.hipMemRelease(self.h)
+        self.hip.hipMemAddressFree(ctypes.c_void_p(self.ptr), ctypes.c_size_t(self.size))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="real")
@@ -49,6 +108,8 @@ def main():
     ap.add_argument("--clock", action="store_true", help="map mode: span kernel clock stamps on each allocation")
     ap.add_argument("--latency", action="store_true", help="map mode: k_chase latency on each allocation")
     ap.add_argument("--libs", default="", help="map mode: extra library builds timed on each allocation")
+    ap.add_argument("--vmm", type=int, default=0,
+                    help="N default and N virtual-memory-API allocations, interleaved, each timed twice")
     ap.add_argument("--map", type=int, default=0,
                     help="N default allocations timed in order; then the first half freed and refilled")
     args = ap.parse_args()
@@ -123,6 +184,26 @@ def main():
         torch.cuda.synchronize()
         return round(n / (e0.elapsed_time(e1) / args.steps * 1e-3) / 8e12, 4)
 
+    if args.vmm:  # does the virtual memory API's mapping take the slow class?
+        bufs = []
+        for k in range(args.vmm):
+            for name in ("default", "vmm"):
+                buf = RawBuf(hip, nbytes, HIP_DEVICE_MALLOC_DEFAULT) if name == "default" else VmmBuf(hip, nbytes)
+                rc = hip.hipMemcpy(ctypes.c_void_p(buf.ptr), ctypes.c_void_p(b.data.data_ptr()),
+                                   ctypes.c_size_t(nbytes), ctypes.c_int(HIP_MEMCPY_D2D))
+                if rc != 0:
+                    raise RuntimeError(f"hipMemcpy = {rc}")
+                bufs.append((k, name, buf))
+        torch.cuda.synchronize()
+        print(json.dumps({"vmm_granularity": [x for x in bufs if x[1] == "vmm"][0][2].gran}), flush=True)
+        for r in range(2):
+            for k, name, buf in bufs:
+                ms = time_batch(FrameBatch(data=buf, count=b.count, offsets=b.offsets))
+                print(json.dumps({"round": r, "copy": k, "alloc": name, "ptr": hex(buf.ptr),
+                                  "frac": round(b.total_bytes / (ms * 1e-3) / 8e12, 4)}), flush=True)
+        for _, _, buf in bufs:
+            buf.free()
+        return
     if args.map:  # which allocations of a process are slow, and does freed memory stay slow?
         def one(tag, k):
             buf = RawBuf(hip, nbytes, HIP_DEVICE_MALLOC_DEFAULT)
