@@ -35,6 +35,7 @@ for s in ${STEPS:-tests}; do
     fresh) step fresh 600 bash -c 'python -u tools/placement_ab.py --workload real --fresh 8' ;;
     reserve) step reserve 900 bash -c 'python -u tools/placement_ab.py --workload real --fresh 6 --reserve 32 && python -u tools/placement_ab.py --workload imix --fresh 6 && python -u tools/placement_ab.py --workload imix --fresh 6 --reserve 32' ;;
     freshpmc) step fresh_pmc 1000 bash tools/fresh_pmc.sh ;;
+    pmcspan) step pmc_span 1100 env CONFIGS="imix.grouped imix_pcap.grouped malformed.grouped real_traffic.grouped imix.sparse" bash tools/pmc.sh ;;
     spantests) step pytest_span 600 python -u -m pytest tests/test_gpu_span.py -q -x --timeout 300 --timeout-method thread ;;
     contigvmm) step contig_vmm 700 bash -c 'python -u tools/contig_ab.py --workload real --vmm 8' ;;
     freshtcp) step fresh_tcp 1100 bash -c 'SET="TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_UTCL1_STALL_INFLIGHT_MAX_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TD_TC_STALL_sum TD_TD_BUSY_sum" bash tools/fresh_pmc.sh && SET="TCP_UTCL1_SERIALIZATION_STALL_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_UTCL1_THRASHING_STALL_sum TA_ADDR_STALLED_BY_TD_CYCLES_sum TA_TA_BUSY_sum" bash tools/fresh_pmc.sh' ;;
