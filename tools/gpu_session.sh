@@ -35,6 +35,7 @@ for s in ${STEPS:-tests}; do
     fresh) step fresh 600 bash -c 'python -u tools/placement_ab.py --workload real --fresh 8' ;;
     reserve) step reserve 900 bash -c 'python -u tools/placement_ab.py --workload real --fresh 6 --reserve 32 && python -u tools/placement_ab.py --workload imix --fresh 6 && python -u tools/placement_ab.py --workload imix --fresh 6 --reserve 32' ;;
     freshpmc) step fresh_pmc 1000 bash tools/fresh_pmc.sh ;;
+    subab4) step sub_ab4 700 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abvar/libnexg_sub20480w5.so,abvar/libnexg_sub16384w5.so,abvar/libnexg_sub20480.so --workloads imix,mix,real --out grouped --check --rounds 3 ;;
     pmcspan) step pmc_span 1100 env CONFIGS="imix.grouped imix_pcap.grouped malformed.grouped real_traffic.grouped imix.sparse" bash tools/pmc.sh ;;
     spantests) step pytest_span 600 python -u -m pytest tests/test_gpu_span.py -q -x --timeout 300 --timeout-method thread ;;
     contigvmm) step contig_vmm 700 bash -c 'python -u tools/contig_ab.py --workload real --vmm 8' ;;
