@@ -35,11 +35,9 @@ WARMUP_SECONDS = 0.25
 #: --out name -> nexg out_kind (include/nexg.h NEXG_OUT_*)
 OUT_KINDS = {"desc": 1, "record": 2, "flags": 4, "verdict": 5, "sparse": 6, "grouped": 7}
 OUT_NOTE = {
-    "sparse": "lossless sparse descriptors (NEXG_OUT_SPARSE: 1-B shape code per frame + 8-B "
-              "exceptions; expands to nexg_desc bit-exactly)",
-    "grouped": "lossless grouped descriptors (NEXG_OUT_GROUPED: NEXG_OUT_SPARSE with each 64-frame group "
-               "of one shape stored as a head byte + 2 verdict bits per frame; expands to nexg_desc "
-               "bit-exactly)",
+    "sparse": "lossless sparse descriptors (NEXG_OUT_SPARSE: 1-B shape code/frame + 8-B exceptions)",
+    "grouped": "lossless grouped descriptors (NEXG_OUT_GROUPED: 64-frame groups as head + 2 verdict "
+               "bits/frame, else 1-B codes + 8-B exceptions)",
     "desc": "8-B nexg_desc per frame", "record": "64-B nexg_record per frame",
     "flags": "4-B flags word per frame (no payload location)",
     "verdict": "2-B lossless flags per frame (no payload location)"}
@@ -90,10 +88,9 @@ def cpu_baseline(batch, workload, count, seconds, nthreads=1):
     mpps = n * reps / t / 1e6
     return {"value": round(mpps, 3), "unit": "Mpkt/s", "cores": nthreads, "kind": "port",
             "gib_s": round(nbytes * reps / t / 2**30, 3),
-            "sample": f"{nthreads} thread(s), first {n} frames of the same {workload} workload, {reps} passes "
-                      f"({t:.1f} s), oracle/nex_oracle.c (literal restatement of "
-                      "Frame::try_from_buf + ipv4/udp/tcp/icmp checksum; Rust reference "
-                      "not buildable here)"}
+            "sample": f"{nthreads} thr, first {n} frames of {workload}, {reps} passes, {t:.1f} s",
+            "desc": "oracle/nex_oracle.c (literal restatement of Frame::try_from_buf + ipv4/udp/tcp/icmp "
+                    "checksum; Rust reference not buildable here)"}
 
 
 SER_MACS = (b"\x02\0\0\0\0\1", b"\x02\0\0\0\0\2")  # udp_ping's interface MACs (synthetic)
@@ -163,9 +160,9 @@ def cpu_baseline_ser(params, count, seconds, nthreads=1):
         reps += 1
     return {"value": round(n * reps / t / 1e6, 3), "unit": "Mpkt/s", "cores": nthreads, "kind": "port",
             "gib_s": round(42 * n * reps / t / 2**30, 3),
-            "sample": f"{nthreads} thread(s), first {n} tuples of the same parameter batch, {reps} passes "
-                      f"({t:.1f} s), oracle/nex_oracle.c nexo_build_udp4 (literal restatement of the "
-                      "udp_ping.rs:68-109 builder chain; Rust reference not buildable here)"}
+            "sample": f"{nthreads} thr, first {n} tuples, {reps} passes, {t:.1f} s",
+            "desc": "oracle/nex_oracle.c nexo_build_udp4 (literal restatement of the udp_ping.rs:68-109 "
+                    "builder chain; Rust reference not buildable here)"}
 
 
 def write_ceiling(eng, out, args, stream, device):
@@ -203,8 +200,9 @@ def ser_line(eng, args, F, first, stream, device, rank, world):
         if rank != 0:
             continue
         ach = alg / kernel_s / 1e9
-        r = {"workload": f"configs[3]: build+checksum {F} udp_ping Eth/IPv4/UDP frames (42 B) per GPU, "
-                         + SER_SHAPE_NOTE[shape],
+        r = {"workload": f"configs[3] udp_ping {shape}",
+             "desc": f"configs[3]: build+checksum {F} udp_ping Eth/IPv4/UDP frames (42 B) per GPU, "
+                     + SER_SHAPE_NOTE[shape],
              "value": tp["value"], "unit": "Mpkt/s", "steps": args.steps, "ms_per_step": tp["ms_per_step"],
              "gib_s": tp["gib_s"], "bytes_per_gpu": alg,
              "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -253,9 +251,9 @@ def cpu_baseline_probe(shape, dst_host, seconds, nthreads):
     L = probes.frame_len(shape)
     return {"value": round(n * reps / t / 1e6, 3), "unit": "Mpkt/s", "cores": nthreads, "kind": "port",
             "gib_s": round(L * n * reps / t / 2**30, 3),
-            "sample": f"{nthreads} thread(s), first {n} destinations of the same batch, {reps} passes ({t:.1f} s), "
-                      "oracle/nex_oracle.c nexo_build_probe_batch (literal restatement of the example's builder "
-                      "chain per frame; Rust reference not buildable here)"}
+            "sample": f"{nthreads} thr, first {n} destinations, {reps} passes, {t:.1f} s",
+            "desc": "oracle/nex_oracle.c nexo_build_probe_batch (literal restatement of the example's builder "
+                    "chain per frame; Rust reference not buildable here)"}
 
 
 def probe_object(eng, args, F, first, shape, stream, device, rank, world):
@@ -279,8 +277,9 @@ def probe_object(eng, args, F, first, shape, stream, device, rank, world):
         return None
     ach = alg / kernel_s / 1e9
     rd = probes.dst_bytes(shape)
-    r = {"workload": f"SURVEY 8(f)3 probe batch: build+checksum {F} frames per GPU, " + probes.NOTE[shape]
-                     + f"; one source, a destination per frame ({rd} B read), the rest the example's constants",
+    r = {"workload": f"8(f)3 {shape} probe batch",
+         "desc": f"SURVEY 8(f)3 probe batch: build+checksum {F} frames per GPU, " + probes.NOTE[shape]
+                 + f"; one source, a destination per frame ({rd} B read), the rest the example's constants",
          "value": tp["value"], "unit": "Mpkt/s", "steps": args.steps, "ms_per_step": tp["ms_per_step"],
          "gib_s": tp["gib_s"], "bytes_per_gpu": alg,
          "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -417,7 +416,7 @@ def hbm_latency(eng, device, steps=2000):
 
 
 def parse_object(eng, args, batch, out_kind, stream, device, rank, world, workload, traffic_key,
-                 warmup, steps, cpu_label=None, extra=None, also=()):
+                 warmup, steps, cpu_label=None, extra=None, also=(), desc=None):
     """One parse workload beside the default run, same output kind and timing
     discipline: W untimed launches (+ the warmup floor), K timed, max over
     ranks. Returns the object rank 0 adds to the JSON line (None elsewhere)."""
@@ -453,7 +452,7 @@ def parse_object(eng, args, batch, out_kind, stream, device, rank, world, worklo
     if rank != 0:
         return None
     ach = alg / kernel_s / 1e9
-    r = {"workload": workload, "value": tp["value"], "unit": "Mpkt/s", "steps": steps,
+    r = {"workload": workload, "desc": desc, "value": tp["value"], "unit": "Mpkt/s", "steps": steps,
          "ms_per_step": tp["ms_per_step"], "gib_s": tp["gib_s"], "frames_per_gpu": n, "bytes_per_gpu": alg,
          "warmup_run": wstats,
          "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -490,9 +489,9 @@ def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
     so the IMIX objects warm up for IMIX_WARMUP untimed launches."""
     from nex_amd import abi
     batch = eng.gen_batch(abi.WL_IMIX, F, first_index=first)
-    return parse_object(eng, args, batch, out_kind, stream, device, rank, world,
-                        f"configs[2]: {F} IMIX frames per GPU " + IMIX_DESC + OUT_NOTE[args.out], "imix",
-                        max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2), cpu_label="imix")
+    return parse_object(eng, args, batch, out_kind, stream, device, rank, world, f"configs[2] IMIX {args.out}",
+                        "imix", max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2), cpu_label="imix",
+                        desc=f"configs[2]: {F} IMIX frames per GPU " + IMIX_DESC + OUT_NOTE[args.out])
 
 
 def malformed_line(eng, args, F, first, out_kind, stream, device, rank, world):
@@ -504,11 +503,11 @@ def malformed_line(eng, args, F, first, out_kind, stream, device, rank, world):
     distinct = min(F, 1 << 20)
     mix, counts = workloads.malformed_mix(eng, distinct, seed=abi.DEFAULT_SEED + first)
     batch = workloads.tiled(mix, max(1, F // distinct))
-    return parse_object(eng, args, batch, out_kind, stream, device, rank, world,
-                        f"SURVEY App. C malformed mix: {batch.count} frames per GPU ({distinct} distinct, tiled), "
-                        f"IMIX with half the frames mutated {counts}; " + OUT_NOTE[args.out], "malformed",
-                        max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2), cpu_label="malformed",
-                        extra={"shape_share": True})
+    return parse_object(eng, args, batch, out_kind, stream, device, rank, world, f"App. C malformed mix {args.out}",
+                        "malformed", max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2), cpu_label="malformed",
+                        extra={"shape_share": True},
+                        desc=f"SURVEY App. C malformed mix: {batch.count} frames per GPU ({distinct} distinct, "
+                             f"tiled), IMIX with half the frames mutated {counts}; " + OUT_NOTE[args.out])
 
 
 def real_traffic_batch(eng, F, first):
@@ -530,10 +529,11 @@ def real_traffic_line(eng, args, F, first, out_kind, stream, device, rank, world
     from nex_amd import abi
     # the per-frame descriptors a parse_frame / dump caller reads (examples/dump.rs:96-224)
     # on the shape where the grouped output degenerates to per-frame codes
-    return parse_object(eng, args, batch, out_kind, stream, device, rank, world, desc + OUT_NOTE[args.out],
+    return parse_object(eng, args, batch, out_kind, stream, device, rank, world, f"real-traffic IMIX {args.out}",
                         "real_traffic", max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2),
                         cpu_label="real_traffic", extra={"shape_share": True},
-                        also=(("desc_output", abi.OUT_DESC),) if out_kind != abi.OUT_DESC else ())
+                        also=(("desc_output", abi.OUT_DESC),) if out_kind != abi.OUT_DESC else (),
+                        desc=desc + OUT_NOTE[args.out])
 
 
 LARGE_FRAMES = 52 << 20  # 3.25 GiB of 64-B frames: 13x the 256-MiB Infinity Cache
@@ -544,10 +544,10 @@ def large_line(eng, args, first, out_kind, stream, device, rank, world):
     batch no cache can hold between launches, so its rate is HBM's."""
     from nex_amd import abi
     batch = eng.gen_batch(abi.WL_UDP64, LARGE_FRAMES, first_index=rank * LARGE_FRAMES)  # this rank's index range
-    return parse_object(eng, args, batch, out_kind, stream, device, rank, world,
-                        f"configs[1] at {LARGE_FRAMES} x 64-B Eth/IPv4/UDP frames per GPU (3.25 GiB, 13x the "
-                        "256-MiB Infinity Cache: no cross-launch cache reuse possible); " + OUT_NOTE[args.out],
-                        "udp64_large", args.warmup, args.steps)
+    return parse_object(eng, args, batch, out_kind, stream, device, rank, world, f"configs[1] UDP64 52M {args.out}",
+                        "udp64_large", args.warmup, args.steps,
+                        desc=f"configs[1] at {LARGE_FRAMES} x 64-B Eth/IPv4/UDP frames per GPU (3.25 GiB, 13x the "
+                             "256-MiB Infinity Cache: no cross-launch cache reuse possible); " + OUT_NOTE[args.out])
 
 
 def main():
@@ -579,7 +579,13 @@ def main():
                     help="frames start and end in pinned host memory: chunked H2D -> parse -> "
                          "D2H pipeline on two streams (PCIe-inclusive rate, DESIGN.md §6)")
     ap.add_argument("--e2e-chunk", type=int, default=1 << 20, help="frames per pipelined chunk")
+    ap.add_argument("--lib", default=None,
+                    help="another build of libnexg.so (A/B tools: nex_amd/libnexg_knobs.so reads the "
+                         "measurement overrides NEXG_TILE_ORDER etc. from the environment)")
     args = ap.parse_args()
+    if args.lib:
+        from nex_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(args.lib)
 
     # --gpus N > 1 outside torchrun: start N ranks as a child process and relay
     # rank 0's line (this process makes no GPU call); exits unless this
@@ -784,17 +790,53 @@ def main():
     res["clocks"] = head_clocks
     if world > 1:
         res["per_rank"] = per_rank
-    if imix is not None:
-        res["imix"] = imix
-    if malformed is not None:
-        res["malformed"] = malformed
-    if real is not None:
-        res["real_traffic"] = real
-    if ser is not None:
-        res["ser"] = ser
-    if large is not None:
-        res["large"] = large
-    print(json.dumps(res), flush=True)
+    # the driver keeps the last ~8 KB of stdout: the configs[2] IMIX object and
+    # the packed-batch mixes go last, after the serialize and 52M objects
+    for key, obj in (("ser", ser), ("large", large), ("imix", imix), ("malformed", malformed),
+                     ("real_traffic", real)):
+        if obj is not None:
+            res[key] = obj
+    log("bench detail: " + json.dumps(res))  # every field, prose and full clock histograms (stderr)
+    print(json.dumps(shrink(res), separators=(",", ":")), flush=True)
+
+
+#: prose fields kept only in the stderr detail line (DESIGN.md §6 "Bench line keys")
+DETAIL_ONLY = ("desc", "source", "basis", "note")
+
+
+def shrink(o, depth=0, parent=None):
+    """The stdout form of the bench line (<= 7 KB): prose fields dropped,
+    `clocks` objects compacted (nex_amd/clocks.py compact), the CPU
+    baseline's single-thread leg reduced to its value. Below the top level
+    (the contract's fields stay whole there): `bytes_per_gpu` (= the
+    roofline's algorithmic bytes) is dropped, `algorithmic_bytes_per_launch`
+    is spelled `alg_bytes`, a roofline omits the top level's bound / peak /
+    unit (hbm, 8000, GB/s) and a CPU baseline its unit / kind (Mpkt/s,
+    port). DESIGN.md §6 lists the keys."""
+    if isinstance(o, dict):
+        r = {}
+        for k, v in o.items():
+            if k in DETAIL_ONLY:
+                continue
+            if depth > 0 and parent != "config" and k == "bytes_per_gpu":
+                continue
+            if depth > 1 and parent == "roofline" and k in ("bound", "peak", "unit") and \
+                    v in ("hbm", HBM_PEAK_GBS, "GB/s"):
+                continue
+            if depth > 1 and parent == "cpu_baseline" and (k, v) in (("unit", "Mpkt/s"), ("kind", "port")):
+                continue
+            if k == "clocks" and isinstance(v, dict):
+                r[k] = clocks.compact(v)
+            elif k == "single_thread" and isinstance(v, dict):
+                r[k] = v.get("value")
+            elif k == "algorithmic_bytes_per_launch" and depth > 1:
+                r["alg_bytes"] = v
+            else:
+                r[k] = shrink(v, depth + 1, k)
+        return r
+    if isinstance(o, list):
+        return [shrink(v, depth + 1, parent) for v in o]
+    return o
 
 
 if __name__ == "__main__":

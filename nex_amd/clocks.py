@@ -45,9 +45,7 @@ def span_summary(stamps):
                          "p90": round(float(np.percentile(ticks, 90)) / 100.0, 3)},
         "workgroup_cycles": {"mean": round(mean_cyc, 1), "p90": round(float(np.percentile(cyc, 90)), 1)},
         "phase_cycles": {k: round(float(v), 1) for k, v in zip(PHASES, d.mean(axis=0))},
-        "phase_share": {k: round(float(v) / mean_cyc, 4) for k, v in zip(PHASES, d.mean(axis=0))},
-        "source": "nexg_probe_span_clock: one stamped launch of the same kernel on the same batch right after the "
-                  "timed region; clock = shader-clock ticks / 100-MHz real time per workgroup"}
+        "phase_share": {k: round(float(v) / mean_cyc, 4) for k, v in zip(PHASES, d.mean(axis=0))}}
 
 
 def _read(path):
@@ -119,6 +117,47 @@ def sysfs(device_index=0, path=None):
                 r["hwmon_sclk_mhz"] = round(int(v.strip()) / 1e6)
             except ValueError:
                 pass
+    return r
+
+
+def _mhz_range(counts):
+    """{'2100Mhz': n, ...} sample counts -> [min, median, max] MHz (ints)."""
+    vals = []
+    for k, n in counts.items():
+        try:
+            vals += [int(str(k).lower().replace("mhz", "").strip())] * int(n)
+        except ValueError:
+            continue
+    if not vals:
+        return None
+    vals.sort()
+    return [vals[0], vals[len(vals) // 2], vals[-1]]
+
+
+def compact(clk):
+    """The short form of a `clocks` object that bench.py's stdout line carries
+    (the full form goes to stderr): sysfs sclk / mclk as [min, median, max]
+    MHz over the samples, board power [min, max] W; the span kernel's
+    median shader clock and its phase shares in PHASES order; the dependent
+    HBM load latency [idle, loaded] ns. Keys are documented in DESIGN.md §6."""
+    r = {}
+    s = clk.get("sysfs") or {}
+    for k in ("sclk", "mclk"):
+        if isinstance(s.get(k), dict):
+            v = _mhz_range(s[k])
+            if v is not None:
+                r[f"{k}_mhz"] = v
+    if isinstance(s.get("power_w"), dict):
+        r["power_w"] = [s["power_w"].get("min"), s["power_w"].get("max")]
+    sp = clk.get("span")
+    if isinstance(sp, dict) and "shader_clock_ghz" in sp:
+        r["span_ghz"] = sp["shader_clock_ghz"]["median"]
+        r["span_share"] = [round(sp["phase_share"][k], 3) for k in PHASES]
+    elif isinstance(sp, dict) and "error" in sp:
+        r["span_error"] = str(sp["error"])[:80]
+    lat = clk.get("hbm_latency")
+    if isinstance(lat, dict):
+        r["lat_ns"] = [lat.get("idle_ns"), lat.get("loaded_ns")]
     return r
 
 

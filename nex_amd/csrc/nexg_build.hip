@@ -64,7 +64,11 @@ struct BuildArgs {
 constexpr uint32_t kBuildCapPad = 160u * 1024u / 5u - (kBuildTile * 64u + 16u) - 256u;
 uint32_t build_lds_pad() {
     static const uint32_t pad = [] {
+#ifdef NEXG_AB_KNOBS
         const char* e = getenv("NEXG_BUILD_LDS_PAD");
+#else
+        const char* e = nullptr;  // product build: no environment overrides
+#endif
         if (!e) return kBuildCapPad;
         const long v = atol(e);  // clamped: a negative or oversized pad fails every build launch
         return v <= 0 ? 0u : v >= (long)kBuildCapPad ? kBuildCapPad : (uint32_t)v;
@@ -697,34 +701,32 @@ static void launch_l4_form(const L4Args& a, hipStream_t s) {
 static bool try_probe_l4(const L4Args& l, int kind, uint8_t* out, uint32_t out_stride, hipStream_t s, hipError_t& e);
 
 template <int FAM, int KIND>
-static void launch_l4_fam(L4Args& a, hipStream_t s) {
+static hipError_t launch_l4_fam(L4Args& a, hipStream_t s) {
     // the probe batch: one source, a destination per frame, nothing else per
     // frame. It reads 4 / 16 B per frame, as udp_ping's probe batch, and takes
     // that builder's tile order (contiguous eighths); the forms with several
     // parameter arrays keep l4_build_tile_order()
     const bool probe = a.ip.src_shared && !a.ip.ip_id && !a.ip.src_mac && !a.ip.dst_mac &&
                        (KIND == kL4Tcp ? !a.sport && !a.dport && !a.seq && !a.ack : !a.ident && !a.seqno);
-    hipError_t e = hipSuccess;  // a launch error also reaches launch_l4's hipGetLastError
-    if (probe && try_probe_l4(a, KIND, a.out, a.out_stride, s, e)) return;
+    // the template kernel's status (its explicit checks and its launch's
+    // hipGetLastError, which also clears HIP's error state) is the result
+    hipError_t e = hipSuccess;
+    if (probe && try_probe_l4(a, KIND, a.out, a.out_stride, s, e)) return e;
     if (probe) {
         a.tile_order = build_tile_order();
         launch_l4_form<FAM, KIND, true>(a, s);
     } else {
         launch_l4_form<FAM, KIND, false>(a, s);
     }
+    return hipGetLastError();
 }
 
 static hipError_t launch_l4(L4Args& a, int kind, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
+    if ((a.count + kBuildTile - 1) / kBuildTile > 0xFFFFFFFFull) return hipErrorInvalidValue;  // one grid
     a.tile_order = l4_build_tile_order();
-    if (kind == kL4Tcp) {
-        if (a.ip.family == 4) launch_l4_fam<4, kL4Tcp>(a, s);
-        else launch_l4_fam<6, kL4Tcp>(a, s);
-    } else {
-        if (a.ip.family == 4) launch_l4_fam<4, kL4Icmp>(a, s);
-        else launch_l4_fam<6, kL4Icmp>(a, s);
-    }
-    return hipGetLastError();
+    if (kind == kL4Tcp) return a.ip.family == 4 ? launch_l4_fam<4, kL4Tcp>(a, s) : launch_l4_fam<6, kL4Tcp>(a, s);
+    return a.ip.family == 4 ? launch_l4_fam<4, kL4Icmp>(a, s) : launch_l4_fam<6, kL4Icmp>(a, s);
 }
 
 hipError_t launch_build_tcp(const nexg_tcp_build& p, uint8_t* out, uint32_t out_stride, hipStream_t s) {
@@ -1001,7 +1003,12 @@ bool probe_launch_ok(uint32_t flen, uint32_t period, uint32_t pay_len, const uin
 // waves per workgroup (1 or 4), NEXG_PROBE_WGS workgroups per CU set by the
 // dynamic LDS (160 KiB per CU; 0 = only the tile's LDS).
 uint32_t probe_env(const char* name, uint32_t def, uint32_t lo, uint32_t hi) {
+#ifdef NEXG_AB_KNOBS
     const char* e = getenv(name);
+#else
+    (void)name;
+    const char* e = nullptr;  // product build: no environment overrides
+#endif
     const long x = e ? strtol(e, nullptr, 10) : -1;
     return x >= (long)lo && x <= (long)hi ? (uint32_t)x : def;
 }
@@ -1010,7 +1017,9 @@ uint32_t probe_waves() {
     return v;
 }
 uint32_t probe_wgs_per_cu() {
-    static const uint32_t v = probe_env("NEXG_PROBE_WGS", 5u, 0u, 64u);
+    // 1 or 2 per CU would ask more than a workgroup's 64 KiB of LDS: 3 at least
+    static const uint32_t v = [] { const uint32_t w = probe_env("NEXG_PROBE_WGS", 5u, 0u, 64u);
+                                   return w && w < 3u ? 3u : w; }();
     return v;
 }
 
@@ -1024,11 +1033,15 @@ hipError_t launch_probe(ProbeArgs& a, const uint8_t* tmpl, uint32_t dw, hipStrea
     const uint32_t waves = probe_waves(), kT = 64u * waves;
     const uint64_t ntiles = (a.count + kT - 1) / kT;
     if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
+#ifdef NEXG_AB_KNOBS
+    // fault injection for the error-path test (tests/test_gpu_probe_batches.py)
+    if (probe_env("NEXG_PROBE_FAIL", 0u, 0u, 1u) == 1u) return hipErrorInvalidValue;
+#endif
     const uint32_t need = (P + 15u) / 16u;  // 16-B chunks per lane, rounded to an instantiated KCH
     const uint32_t kch = need <= 3u ? 3u : need <= 6u ? need : 8u;
     const uint32_t tile_lds = kch * 16u * kT + 2u * kProbeMaxP + 32u, wgs = probe_wgs_per_cu();
     const uint32_t cap = wgs ? 160u * 1024u / wgs - 1024u : 0u;
-    const uint32_t lds = tile_lds > cap ? tile_lds : cap;
+    const uint32_t lds = tile_lds > cap ? tile_lds : cap < 65536u ? cap : 65536u;  // a workgroup's LDS limit
     a.tile_order = build_tile_order();
     const dim3 g((uint32_t)ntiles), b(kT);
 #define NEXG_PROBE_LAUNCH(DW, K)                                                     \
@@ -1485,9 +1498,9 @@ hipError_t launch_build_udp6(const nexg_udp6_build& p, uint8_t* out, uint32_t ou
     if (probe && try_probe_udp6(p, out, out_stride, s, e)) return e;
     if (probe) a.tile_order = build_tile_order();  // udp_ping's probe batch order (see launch_l4_fam)
     // a 16-KiB tile for the udp_ping shapes + build_lds_pad(): 5 workgroups per CU (0.279 -> 0.253 ms)
-    if (staged && out_stride <= 64u && probe)
-        hipLaunchKernelGGL((k_build_udp6<64, true>), dim3((uint32_t)blocks), dim3(kBuildTile), build_lds_pad(), s, a);
-    else if (staged && out_stride <= 64u)
+    // (a probe batch reaching here has a misaligned output or a long frame:
+    // the per-lane kernel's src_shared branch takes it)
+    if (staged && out_stride <= 64u)
         hipLaunchKernelGGL(k_build_udp6<64>, dim3((uint32_t)blocks), dim3(kBuildTile), build_lds_pad(), s, a);
     else if (staged)
         hipLaunchKernelGGL(k_build_udp6<kBuildMaxStride>, dim3((uint32_t)blocks), dim3(kBuildTile), 0, s, a);

@@ -19,14 +19,21 @@
 
 namespace nexg {
 
-// tile_index order named by an env variable (measurement overrides):
+// tile_index order named by an env variable (measurement overrides, compiled
+// only into the -DNEXG_AB_KNOBS build nex_amd/libnexg_knobs.so that the A/B
+// tools and tests/test_gpu_tile_order.py load; the product library has none):
 // linear = 0, xcd = 1 (contiguous eighths), xcdK = XCD-local runs of K tiles;
 // -1 when unset or unrecognised.
 static int order_from_env(const char* name) {
+#ifdef NEXG_AB_KNOBS
     const char* e = getenv(name);
     if (!e) return -1;
     if (strncmp(e, "xcd", 3) == 0 && e[3]) return atoi(e + 3);
     return strcmp(e, "xcd") == 0 ? 1 : (strcmp(e, "linear") == 0 ? 0 : -1);
+#else
+    (void)name;
+    return -1;
+#endif
 }
 
 // Tile order of the parse kernels; NEXG_TILE_ORDER overrides. Fixed-stride

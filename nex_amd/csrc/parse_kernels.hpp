@@ -149,17 +149,20 @@ __device__ __forceinline__ void copy_out_records(const uint8_t* stage, void* out
 // 8-B descriptor at the start of its PITCH-byte slot (call after a barrier);
 // the tile's nf descriptors leave as contiguous 16-B non-temporal stores, two
 // descriptors per thread (threads 0..127), instead of 8-B stores per thread.
+// An output at 8 mod 16 (the API asks 8-B alignment) takes two 8-B stores.
 template <uint32_t PITCH>
 __device__ __forceinline__ void copy_out_descs(const uint8_t* stage, void* out, uint64_t first, uint32_t nf) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     const uint32_t c = threadIdx.x, f = 2u * c;
     if (f >= nf) return;
     const uint2 d0 = *reinterpret_cast<const uint2*>(stage + f * PITCH);
-    if (f + 1u < nf) {
-        const uint2 d1 = *reinterpret_cast<const uint2*>(stage + (f + 1u) * PITCH);
+    const bool pair = f + 1u < nf;
+    const uint2 d1 = pair ? *reinterpret_cast<const uint2*>(stage + (f + 1u) * PITCH) : d0;
+    if (pair && (reinterpret_cast<uint64_t>(out) & 15u) == 0) {
         __builtin_nontemporal_store(u32x4{d0.x, d0.y, d1.x, d1.y}, reinterpret_cast<u32x4*>(out) + (first + f) / 2u);
     } else {
         __builtin_nontemporal_store(v2u{d0.x, d0.y}, reinterpret_cast<v2u*>(out) + first + f);
+        if (pair) __builtin_nontemporal_store(v2u{d1.x, d1.y}, reinterpret_cast<v2u*>(out) + first + f + 1u);
     }
 }
 

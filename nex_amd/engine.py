@@ -314,6 +314,28 @@ class Engine:
         return out[: batch.count]
 
     # --- serialize path ---------------------------------------------------
+    @staticmethod
+    def _check_rows(count, row_bytes, shared_ok=False, **arrays):
+        """Per-frame parameter arrays hold `count` rows of `row_bytes` each
+        (or exactly one row where the builder takes one value for the batch,
+        `shared_ok`): the kernels read row i for frame i, so a short array
+        would be read past on the device."""
+        for name, t in arrays.items():
+            if t is None:
+                continue
+            nb = t.numel() * t.element_size()
+            if shared_ok and nb == row_bytes:
+                continue
+            if nb < count * row_bytes:
+                raise ValueError(f"{name} holds {nb} B; {count} frames need {count * row_bytes} B"
+                                 + (f" (or one {row_bytes}-B value for the batch)" if shared_ok else ""))
+
+    @staticmethod
+    def _check_out(out, count, stride):
+        if out is not None and out.numel() * out.element_size() < count * stride:
+            raise ValueError(f"out holds {out.numel() * out.element_size()} B; {count} frames of stride "
+                             f"{stride} need {count * stride} B")
+
     def build_udp4(self, src_ip, dst_ip, src_port=None, dst_port=None, ip_id=None,
                    def_src_port=0, def_dst_port=0, def_ip_id=0,
                    src_mac=b"\0" * 6, dst_mac=b"\0" * 6, ttl=64, ip_flags=0, dscp_ecn=0,
@@ -327,6 +349,9 @@ class Engine:
         count = dst_ip.numel()
         plen = 0 if payload is None else payload.numel()
         stride = out_stride or (42 + plen)
+        self._check_rows(count, 4, src_ip=src_ip)
+        self._check_rows(count, 2, src_port=src_port, dst_port=dst_port, ip_id=ip_id)
+        self._check_out(out, count, stride)
         if out is None:
             out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
         p = abi.Udp4Build()
@@ -364,6 +389,8 @@ class Engine:
         count = tuples.shape[0]
         plen = 0 if payload is None else payload.numel()
         stride = out_stride or (42 + plen)
+        self._check_rows(count, 16, tuples=tuples)
+        self._check_out(out, count, stride)
         if out is None:
             out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
         p = abi.Udp4Build()
@@ -388,6 +415,9 @@ class Engine:
         count = dst_ip.shape[0] if dst_ip.dim() > 1 else dst_ip.numel() // 16
         plen = 0 if payload is None else payload.numel()
         stride = out_stride or (62 + plen)
+        self._check_rows(count, 16, shared_ok=True, src_ip=src_ip)
+        self._check_rows(count, 2, src_port=src_port, dst_port=dst_port)
+        self._check_out(out, count, stride)
         if out is None:
             out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
         p = abi.Udp6Build()
@@ -440,6 +470,11 @@ class Engine:
         padded = (len(options) + 3) // 4 * 4
         flen = 14 + (20 if family == 4 else 40) + 20 + padded + plen
         stride = out_stride or flen
+        w = 4 if family == 4 else 16
+        self._check_rows(count, w, shared_ok=True, src_ip=src_ip)
+        self._check_rows(count, 2, src_port=src_port, dst_port=dst_port, ip_id=ip_id)
+        self._check_rows(count, 4, seq=seq, ack=ack)
+        self._check_out(out, count, stride)
         if out is None:
             out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
         p = abi.TcpBuild()
@@ -472,6 +507,10 @@ class Engine:
         plen = 0 if payload is None else payload.numel()
         flen = 14 + (20 if family == 4 else 40) + 8 + plen
         stride = out_stride or flen
+        w = 4 if family == 4 else 16
+        self._check_rows(count, w, shared_ok=True, src_ip=src_ip)
+        self._check_rows(count, 2, identifier=identifier, sequence=sequence, ip_id=ip_id)
+        self._check_out(out, count, stride)
         if out is None:
             out = torch.empty(max(count, 1) * stride, dtype=torch.uint8, device=self.torch_device)
         p = abi.IcmpEchoBuild()

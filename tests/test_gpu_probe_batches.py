@@ -170,3 +170,66 @@ def test_l4_probe_payload_stride(engine, oracle, family, plen, stride):
             spec = oracle.ip_spec(family, hs, bytes(hd[i]), smac, dmac, 0x99, 12, 2, 0, 0x54321)
             want = oracle.build_icmp_echo(spec, typ, 0, 0x77, 0x88, pay)
             assert bytes(data[i, :Li]) == want, ("icmp", family, plen, Si, i)
+
+
+@pytest.mark.parametrize("shift,stride,plen", [(1, None, 0), (1, None, 2), (0, 130, 0), (0, 200, 9), (3, 129, 5)])
+def test_udp6_probe_per_lane_forms(engine, oracle, shift, stride, plen):
+    """udp_ping's IPv6 probe batch where the template kernel does not take it
+    (an output not 16-B aligned, a frame period past 128 B): the per-lane
+    kernel's src_shared branch, staged and direct, against the oracle."""
+    import torch
+    n = 1031
+    L = 62 + plen
+    S = stride or L
+    dst = _dst(n, "udp6", 40 + shift + S)
+    src = probes.source("udp6", "cuda")
+    pay = bytes((5 * k + 3) & 0xFF for k in range(plen))
+    pt = torch.tensor(list(pay), dtype=torch.uint8, device="cuda") if plen else None
+    buf = torch.zeros(n * S + 16, dtype=torch.uint8, device="cuda")
+    out = buf[shift: shift + n * S]
+    engine.build_udp6(src, dst, def_src_port=53443, def_dst_port=33435, src_mac=probes.SRC_MAC,
+                      dst_mac=probes.DST_MAC, hop_limit=64, payload=pt, out_stride=S, out=out)
+    torch.cuda.synchronize()
+    data = out.cpu().numpy().reshape(n, S)
+    hs, hd = bytes(src.cpu().numpy()), dst.cpu().numpy()
+    for i in list(range(0, n, 7)) + [n - 1]:
+        want = oracle.build_udp6(probes.SRC_MAC, probes.DST_MAC, hs, bytes(hd[i]), 53443, 33435, 64, 0, 0, pay)
+        assert bytes(data[i, :L]) == want, (shift, S, plen, i)
+
+
+KNOBS_CHILD = r'''
+import sys
+import torch
+from nex_amd import _lib, probes
+_lib.LIB_PATH = sys.argv[1]  # the -DNEXG_AB_KNOBS build: NEXG_PROBE_FAIL=1 fails the template launch
+from nex_amd.engine import Engine, NexgError
+e = Engine(0)
+res = {}
+for shape in ("tcp_ping", "udp6"):
+    d = torch.zeros((300, probes.dst_bytes(shape)), dtype=torch.uint8, device="cuda")
+    try:
+        probes.build(e, shape, d)
+        torch.cuda.synchronize()
+        res[shape] = "ok"
+    except NexgError as x:
+        res[shape] = "error: " + str(x)[:60]
+print(res)
+'''
+
+
+def test_template_launch_failure_reaches_caller():
+    """A failed launch of the template kernel (fault injection in the
+    measurement build) comes back as an error from nexg_build_tcp_batch /
+    nexg_build_udp6_batch, not NEXG_OK with the output unwritten."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "nex_amd", "libnexg_knobs.so")
+    for fail in ("1", "0"):
+        r = subprocess.run([sys.executable, "-c", KNOBS_CHILD, lib], cwd=root, capture_output=True, text=True,
+                           timeout=240, env=dict(os.environ, NEXG_PROBE_FAIL=fail))
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = eval(r.stdout.strip().splitlines()[-1])
+        for shape in ("tcp_ping", "udp6"):
+            assert res[shape].startswith("error") == (fail == "1"), (fail, res)

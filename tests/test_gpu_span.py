@@ -142,3 +142,23 @@ def test_packed_offsets_table_alignment(engine, mixed, shift):
         engine.parse(batch, out_kind=kind, out=want)
         engine.parse(moved, out_kind=kind, out=got)
         assert torch.equal(got, want), kind
+
+
+@pytest.mark.parametrize("layout", ["packed", "udp64"])
+def test_desc_output_at_8_mod_16(engine, mixed, layout):
+    """NEXG_OUT_DESC into an output at 8 mod 16 (the API asks 8-B alignment):
+    the span kernel's paired 16-B copy-out falls back to 8-B stores there;
+    the descriptors equal the aligned output's, and nothing past the last
+    one is written."""
+    import torch
+    batch = (FrameBatch.from_packed(mixed, pad_to=1, shift=0) if layout == "packed"
+             else engine.gen_batch(abi.WL_UDP64, 70_001))
+    n = engine.out_bytes(abi.OUT_DESC, batch.count)
+    want = torch.zeros(n, dtype=torch.uint8, device=batch.data.device)
+    buf = torch.full((n + 32,), 0xA5, dtype=torch.uint8, device=batch.data.device)
+    assert buf.data_ptr() % 16 == 0
+    engine.parse(batch, out_kind=abi.OUT_DESC, out=want)
+    engine.parse(batch, out_kind=abi.OUT_DESC, out=buf[8: 8 + n])
+    torch.cuda.synchronize()
+    assert torch.equal(buf[8: 8 + n], want)
+    assert bool((buf[:8] == 0xA5).all()) and bool((buf[8 + n:] == 0xA5).all())

@@ -5,8 +5,10 @@ the tiles; a wrong one skips some frames and parses others twice.
 - the default order (XCD-local runs of 16 tiles for fixed strides) on a
   mutated-frame batch with whole runs and a ragged tail, every record against
   the oracle;
-- every order the env overrides select (grid, contiguous eighths, runs of
-  3 / 8 / 16 / 64) in a child process per order: the parse outputs of fixed
+- every order the env overrides of the measurement build
+  (nex_amd/libnexg_knobs.so, -DNEXG_AB_KNOBS; the product library reads no
+  environment) select (grid, contiguous eighths, runs of 3 / 8 / 16 / 64) in
+  a child process per order: the parse outputs of fixed
   64-B and 96-B strides and of a packed IMIX batch (span kernel), and the
   udp_ping / udp6 / tcp_ping / icmp_ping builds, hashed and compared with
   the grid-order run."""
@@ -25,6 +27,7 @@ from tests import helpers
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KNOBS_LIB = os.path.join(ROOT, "nex_amd", "libnexg_knobs.so")
 
 # 1172 64-B tiles: 1152 in whole groups of 8 x 16 (and of 8 x 3, 8 x 8), a 20-tile tail
 N_FIXED = 1171 * 256 + 7
@@ -33,7 +36,8 @@ N_IMIX = 200_003
 CHILD = r'''
 import hashlib, json, sys
 import torch
-from nex_amd import abi
+from nex_amd import _lib, abi
+_lib.LIB_PATH = sys.argv[3]  # the -DNEXG_AB_KNOBS build: it reads the order overrides
 from nex_amd.engine import Engine, FrameBatch
 e = Engine(0)
 h = {}
@@ -73,7 +77,7 @@ print(json.dumps(h))
 
 def run_child(order):
     env = dict(os.environ, NEXG_TILE_ORDER=order, NEXG_BUILD_ORDER=order, NEXG_L4_ORDER=order)
-    r = subprocess.run([sys.executable, "-c", CHILD, str(N_FIXED), str(N_IMIX)], cwd=ROOT, env=env,
+    r = subprocess.run([sys.executable, "-c", CHILD, str(N_FIXED), str(N_IMIX), KNOBS_LIB], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     return json.loads(r.stdout.strip().splitlines()[-1])

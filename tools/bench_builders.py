@@ -23,7 +23,8 @@ def main():
     ap.add_argument("--frames", type=int, default=16 << 20)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--probe", action="store_true", help="time the probe batches (nex_amd/probes.py) instead")
-    ap.add_argument("--lib", default=None, help="another build of libnexg.so (A/B)")
+    ap.add_argument("--lib", default=os.path.join(ROOT, "nex_amd", "libnexg_knobs.so"),
+                    help="build of libnexg.so (default: the -DNEXG_AB_KNOBS build, which reads the NEXG_* overrides)")
     args = ap.parse_args()
     import torch
     from nex_amd import _lib

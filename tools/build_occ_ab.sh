@@ -11,7 +11,7 @@ for rnd in 1 2; do
   for c in $L; do
     o=${c%:*}; p=${c#*:}
     for shape in probe tuples; do
-      NEXG_BUILD_ORDER=$o NEXG_BUILD_LDS_PAD=$p timeout -k 10 180 python bench.py --workload ser --ser-shape $shape --steps 50 --warmup 25 \
+      NEXG_BUILD_ORDER=$o NEXG_BUILD_LDS_PAD=$p timeout -k 10 180 python bench.py --lib nex_amd/libnexg_knobs.so --workload ser --ser-shape $shape --steps 50 --warmup 25 \
         --no-cpu-baseline > gpurun_out/buildocc/${shape}_${o}_${p}_$rnd.json 2>/dev/null
       rc=$?; [ $rc -ne 0 ] && { echo "$c rc=$rc"; exit $rc; }
       python -c "

@@ -31,6 +31,8 @@ def timed(fn, steps=10, warmup=3):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 64 << 20
+    from nex_amd import _lib
+    _lib.LIB_PATH = os.path.join(ROOT, "nex_amd", "libnexg_knobs.so")  # reads NEXG_TILE_ORDER
     eng = Engine(0)
     b = eng.gen_batch(abi.WL_UDP64, n)
     out = torch.empty(n * 8, dtype=torch.uint8, device="cuda")

@@ -96,6 +96,8 @@ for s in ${STEPS:-tests}; do
     # in-process A/B of library variants under abvar/ (LIBS=a,b,...): IMIX with an output check, then the mixes
     abspan) step ab_imix 600 python -u tools/bench_parse_ab.py --libs ${LIBS} --workloads imix,udp64 --out grouped --check --rounds 4
             step ab_mixes 600 python -u tools/bench_malformed.py --libs ${LIBS} --kinds ${KINDS:-clean,all,tcp_ts} --out grouped ;;
+    # the driver's own command under the kernel trace: a row for every object of its line (tools/line_trace.py)
+    lineprof) step lineprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lineprof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed --no-real --no-large --no-ser
           step prof_pcap 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pcap -o run -- python3 bench.py --workload imix_pcap --steps 60 --warmup 25 --no-cpu-baseline
           step prof_imix 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_imix -o run -- python3 bench.py --workload imix --steps 60 --warmup 25 --no-cpu-baseline

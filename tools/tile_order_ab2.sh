@@ -10,7 +10,7 @@ REV=$(echo $ORDERS | tr ' ' '\n' | tac | tr '\n' ' ')
 for rnd in 1 2; do
   if [ $rnd = 1 ]; then L="$ORDERS"; else L="$REV"; fi
   for o in $L; do
-    NEXG_TILE_ORDER=$o NEXG_BUILD_ORDER=$o timeout -k 10 240 python bench.py --steps 40 --warmup 20 \
+    NEXG_TILE_ORDER=$o NEXG_BUILD_ORDER=$o timeout -k 10 240 python bench.py --lib nex_amd/libnexg_knobs.so --steps 40 --warmup 20 \
       --no-cpu-baseline --no-large > gpurun_out/tileorder2/${o}_$rnd.json 2>/dev/null
     rc=$?; [ $rc -ne 0 ] && { echo "$o rc=$rc"; exit $rc; }
     python - gpurun_out/tileorder2/${o}_$rnd.json $o <<'EOF'

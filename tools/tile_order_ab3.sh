@@ -10,7 +10,7 @@ REV=$(echo $ORDERS | tr ' ' '\n' | tac | tr '\n' ' ')
 for rnd in 1 2; do
   if [ $rnd = 1 ]; then L="$ORDERS"; else L="$REV"; fi
   for o in $L; do
-    NEXG_BUILD_ORDER=$o timeout -k 10 180 python bench.py --steps 50 --warmup 25 --no-cpu-baseline \
+    NEXG_BUILD_ORDER=$o timeout -k 10 180 python bench.py --lib nex_amd/libnexg_knobs.so --steps 50 --warmup 25 --no-cpu-baseline \
       --no-imix --no-malformed --no-real --no-large > gpurun_out/tileorder3/${o}_$rnd.json 2>/dev/null
     rc=$?; [ $rc -ne 0 ] && { echo "$o rc=$rc"; exit $rc; }
     python - gpurun_out/tileorder3/${o}_$rnd.json $o <<'EOF'

@@ -29,7 +29,9 @@ def main():
         with open(traces[0]) as f:
             for r in csv.DictReader(f):
                 k = r["Kernel_Name"]
-                if "nexg::" not in k or "k_gen_" in k:
+                # generators and calibration kernels (the ser run's write-only ceiling
+                # k_probe_write, the stream probes, the latency chase) are not the object
+                if "nexg::" not in k or any(c in k for c in ("k_gen_", "k_probe_", "k_chase", "k_recompute")):
                     continue
                 launches.setdefault(k, []).append((int(r["Start_Timestamp"]),
                                                    int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
