@@ -952,6 +952,116 @@ __global__ __launch_bounds__(64 * WAVES) void k_build_probe(ProbeArgs a) {
 #endif
 }
 
+// ---- probe batches, frame per lane: k_build_lane ---------------------------
+// The probe template as k_build_probe takes it, but each lane writes its own
+// frame into the LDS tile as whole dwords of the tile, so that odd frame
+// periods (icmp_ping's 47 B) cost no byte or halfword stores and there is no
+// separate fill pass or patch barrier:
+//  * the template dwords (the host's, followed by the next frame's first 8
+//    bytes) are uniform: the device source and payload are merged into them
+//    by scalar loads at compile-time offsets in every wave (no barrier);
+//  * lane t's frame starts at tile byte t P, s = t P mod 4 bytes into its
+//    first dword. Frame dword F[j] (frame bytes [4j, 4j + 4)) gets the lane's
+//    destination and the checksums over it OR-ed in at the shape's
+//    compile-time offsets; tile dword (t P >> 2) + j is
+//    v_alignbyte(F[j], F[j - 1], 4 - s) (F[j] when s = 0);
+//  * a lane writes the dwords from the first one that starts inside its frame
+//    to the one holding its last byte; that last dword's other bytes are the
+//    next frame's head (the Ethernet addresses: batch constants), so every
+//    tile dword has exactly one writer and no lane needs a neighbour's bytes.
+// Then one barrier and the tile leaves with 16-B non-temporal stores.
+template <int FAM, int KIND, uint32_t MAXP>
+__global__ __launch_bounds__(256) void k_build_lane(ProbeArgs a) {
+    constexpr uint32_t DW = FAM == 4 ? 1u : 4u;              // destination dwords
+    constexpr uint32_t SRC = FAM == 4 ? 26u : 22u;           // source address offset (= 2 mod 4)
+    constexpr uint32_t DST = FAM == 4 ? 30u : 38u;           // destination offset (= 2 mod 4)
+    constexpr uint32_t L3 = FAM == 4 ? 20u : 40u;
+    constexpr uint32_t L4CK = 14u + L3 + (KIND == kL4Tcp ? 16u : 2u);  // L4 checksum offset
+    constexpr uint32_t PAY = 14u + L3 + 8u;                  // ICMP payload offset (= 2 mod 4)
+    constexpr bool L4DST = !(FAM == 4 && KIND == kL4Icmp);   // ICMPv4 sums the message alone
+    constexpr uint32_t NF = MAXP / 4u + 3u;                  // frame dwords + the next frame's head
+    static_assert(SRC % 4u == 2u && DST % 4u == 2u && PAY % 4u == 2u, "halfword-shifted fields");
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_tile[];  // 256 x P + 16
+    const uint32_t t = threadIdx.x, P = a.period;
+    NEXG_BUILD_STAMP(0);
+    NEXG_BUILD_STAMP(6);
+    const uint64_t tile = tile_index(a.tile_order);
+    const uint64_t first = tile * kBuildTile;
+    const uint32_t nf = a.count - first < kBuildTile ? (uint32_t)(a.count - first) : kBuildTile;
+    uint32_t dw[DW];
+    {  // this lane's destination in flight first (clamped: lanes past the end reload the last)
+        const uint64_t i = first + t;
+        const auto* d4 = NEXG_GLOBAL(uint32_t, a.dst + 4u * DW * (i < a.count ? i : a.count - 1u));
+#pragma unroll
+        for (uint32_t k = 0; k < DW; k++) dw[k] = d4[k];
+    }
+    // uniform: the template with the batch's device source and payload merged
+    uint32_t F[NF];
+#pragma unroll
+    for (uint32_t k = 0; k < NF; k++) F[k] = a.tmpl[k];
+    uint32_t ssum = 0;
+    {
+        uint32_t sx[DW];
+#pragma unroll
+        for (uint32_t k = 0; k < DW; k++) sx[k] = uniform_u32(a.src)[k];
+#pragma unroll
+        for (uint32_t k = 0; k < DW; k++) {
+            ssum += bswap16(sx[k] & 0xFFFFu) + bswap16(sx[k] >> 16);
+            F[SRC / 4u + k] |= sx[k] << 16;
+            F[SRC / 4u + k + 1u] |= sx[k] >> 16;
+        }
+    }
+    uint32_t psum = 0;
+    if (KIND == kL4Icmp && a.pay_len) {  // uniform
+        SmallPayload sp;
+        load_small_payload(a.payload, a.pay_len, sp, psum);  // realigned words, 0 past pay_len
+#pragma unroll
+        for (uint32_t m = 0; m < kSmallPay / 4u; m++) {
+            if (PAY / 4u + m < NF) F[PAY / 4u + m] |= sp.w[m] << 16;
+            if (PAY / 4u + m + 1u < NF) F[PAY / 4u + m + 1u] |= sp.w[m] >> 16;
+        }
+    }
+    const uint64_t S = ssum;
+    if (!L4DST) {  // ICMPv4: one checksum for the batch
+        const uint32_t ck = fold_complement(a.l4_sum + psum);
+        F[L4CK / 4u] |= bswap16(ck) << (8u * (L4CK % 4u));
+    }
+    if (t < nf) {
+        // the lane's frame: destination (network-order bytes, LE halves x 256) and checksums
+        uint32_t dsum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < DW; k++) {
+            dsum += halves(dw[k]);
+            F[DST / 4u + k] |= dw[k] << 16;
+            F[DST / 4u + k + 1u] |= dw[k] >> 16;
+        }
+        const uint64_t D = 256ull * dsum;
+        if (FAM == 4) F[6] |= bswap16(fold_complement(a.ip_sum + S + D));  // bytes 24-25
+        if (L4DST) F[L4CK / 4u] |= bswap16(fold_complement(a.l4_sum + psum + S + D)) << (8u * (L4CK % 4u));
+        const uint32_t b0 = t * P, s = b0 & 3u, jend = (s + P - 1u) >> 2;
+        uint32_t* const tw = reinterpret_cast<uint32_t*>(s_tile) + (b0 >> 2);
+        // fully unrolled with a guard (a `break` here rolled the loop back up
+        // with dynamic register indexing of F)
+#pragma unroll
+        for (uint32_t j = 0; j < NF; j++) {
+            const uint32_t v = s ? __builtin_amdgcn_alignbyte(F[j], F[j ? j - 1u : 0u], 4u - s) : F[j];
+            // j = 0 with s > 0: the dword holding the previous frame's tail (its writer's)
+            if (j <= jend && (j > 0 || s == 0)) tw[j] = v;
+        }
+    }
+    NEXG_BUILD_STAMP(1);
+    __syncthreads();
+    NEXG_BUILD_STAMP(2);
+    NEXG_BUILD_STAMP(3);
+    build_copy_out(s_tile, a.out + first * P, nf * P);
+#if NEXG_PROBE_TIMING
+    NEXG_BUILD_STAMP(4);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    NEXG_BUILD_STAMP(5);
+    NEXG_BUILD_STAMP(7);
+#endif
+}
+
 // ---- host: probe templates (the bytes the per-lane builders write, with the
 // destination, checksums and payload zero) and their base sums
 namespace {
@@ -1061,6 +1171,44 @@ hipError_t launch_probe(ProbeArgs& a, const uint8_t* tmpl, uint32_t dw, hipStrea
 #undef NEXG_PROBE_LAUNCH
     return hipGetLastError();
 }
+
+// k_build_lane: tmpl = one period P <= kLaneMaxP; the kernel's template is the
+// period followed by its first 8 bytes (the next frame's head)
+constexpr uint32_t kLaneMaxP = 96;
+bool lane_launch_ok(uint32_t flen, uint32_t period, uint32_t pay_len, const uint8_t* out) {
+    return period <= kLaneMaxP && flen <= period && pay_len <= kSmallPay && (reinterpret_cast<uint64_t>(out) & 15u) == 0;
+}
+
+hipError_t launch_lane(ProbeArgs& a, const uint8_t* tmpl, int fam, int kind, hipStream_t s) {
+    if (a.count == 0) return hipSuccess;
+    const uint32_t P = a.period;
+    uint8_t d[kProbeMaxP] = {0};
+    for (uint32_t k = 0; k < P; k++) d[k] = tmpl[k];
+    for (uint32_t k = 0; k < 8u; k++) d[P + k] = tmpl[k];
+    for (uint32_t k = 0; k < kProbeMaxP / 4; k++)
+        a.tmpl[k] = (uint32_t)d[4 * k] | ((uint32_t)d[4 * k + 1] << 8) | ((uint32_t)d[4 * k + 2] << 16) |
+                    ((uint32_t)d[4 * k + 3] << 24);
+    const uint64_t ntiles = (a.count + kBuildTile - 1) / kBuildTile;
+    if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
+#ifdef NEXG_AB_KNOBS
+    if (probe_env("NEXG_PROBE_FAIL", 0u, 0u, 1u) == 1u) return hipErrorInvalidValue;
+#endif
+    // dynamic LDS: the tile (+ the last lane's tail dword), raised to set the
+    // workgroups per CU (probe_wgs_per_cu, as k_build_probe)
+    const uint32_t tile_lds = kBuildTile * P + 16u, wgs = probe_wgs_per_cu();
+    const uint32_t cap = wgs ? 160u * 1024u / wgs - 1024u : 0u;
+    const uint32_t lds = tile_lds > cap ? tile_lds : cap < 65536u ? cap : 65536u;
+    a.tile_order = build_tile_order();
+    const dim3 g((uint32_t)ntiles), b(kBuildTile);
+    if (kind == kL4Icmp) {
+        if (fam == 4) hipLaunchKernelGGL((k_build_lane<4, kL4Icmp, kLaneMaxP>), g, b, lds, s, a);
+        else hipLaunchKernelGGL((k_build_lane<6, kL4Icmp, kLaneMaxP>), g, b, lds, s, a);
+    } else {
+        if (fam == 4) hipLaunchKernelGGL((k_build_lane<4, kL4Tcp, kLaneMaxP>), g, b, lds, s, a);
+        else hipLaunchKernelGGL((k_build_lane<6, kL4Tcp, kLaneMaxP>), g, b, lds, s, a);
+    }
+    return hipGetLastError();
+}
 }  // namespace
 
 // udp_ping's IPv6 probe batch (src_shared, dst per frame): builder/udp.rs:67-95
@@ -1095,10 +1243,17 @@ static bool try_probe_l4(const L4Args& l, int kind, uint8_t* out, uint32_t out_s
     const uint32_t l4_hdr = kind == kL4Tcp ? 20u + l.opt_padded : 8u;
     const uint32_t l4_len = l4_hdr + l.payload_len;
     const uint32_t flen = 14u + l3 + l4_len;
-    // tcp_ping only: the ICMP shapes run faster per lane (0.44 / 0.57 of 8 TB/s
-    // against 0.41 / 0.37 for the template kernel, profiles/r05/probe/)
-    static const bool icmp_template = probe_env("NEXG_PROBE_ICMP", 0u, 0u, 1u) == 1u;  // measurement override
-    if ((kind != kL4Tcp && !icmp_template) || !probe_launch_ok(flen, out_stride, l.payload_len, out)) return false;
+    // icmp_ping: k_build_lane (whole-dword tile writes at any frame period);
+    // tcp_ping: k_build_probe (0.72-0.89 of 8 TB/s written, round 5).
+    // Measurement overrides (knobs build): NEXG_PROBE_ICMP = 1 the template
+    // kernel, 2 the per-lane k_build_l4; NEXG_PROBE_LANE_TCP = 1 k_build_lane
+    // for tcp_ping (no payload)
+    static const uint32_t icmp_path = probe_env("NEXG_PROBE_ICMP", 0u, 0u, 2u);
+    static const bool tcp_lane = probe_env("NEXG_PROBE_LANE_TCP", 0u, 0u, 1u) == 1u;
+    const bool lane = kind == kL4Icmp ? icmp_path == 0u && lane_launch_ok(flen, out_stride, l.payload_len, out)
+                                      : tcp_lane && l.payload_len == 0 && lane_launch_ok(flen, out_stride, 0, out);
+    if (!lane && ((kind != kL4Tcp && icmp_path != 1u) || !probe_launch_ok(flen, out_stride, l.payload_len, out)))
+        return false;
     ProbeArgs a{};
     uint8_t t[kProbeMaxP] = {0};
     const uint8_t zero[16] = {0};
@@ -1134,7 +1289,7 @@ static bool try_probe_l4(const L4Args& l, int kind, uint8_t* out, uint32_t out_s
     a.dst = ip.dst_ip; a.dst_off = v4 ? 30u : 38u;
     a.payload = l.payload; a.pay_off = 14 + l3 + l4_hdr; a.pay_len = l.payload_len;
     a.out = out; a.count = l.count; a.period = out_stride;
-    e = launch_probe(a, t, v4 ? 1u : 4u, s);
+    e = lane ? launch_lane(a, t, ip.family, kind, s) : launch_probe(a, t, v4 ? 1u : 4u, s);
     return true;
 }
 
