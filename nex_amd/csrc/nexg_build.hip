@@ -970,7 +970,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_build_probe(ProbeArgs a) {
 //    next frame's head (the Ethernet addresses: batch constants), so every
 //    tile dword has exactly one writer and no lane needs a neighbour's bytes.
 // Then one barrier and the tile leaves with 16-B non-temporal stores.
-template <int FAM, int KIND, uint32_t MAXP>
+// MINP <= P <= MAXP: the frame dwords every lane writes are known at compile
+// time (no exec mask per dword); the last one or two are per lane.
+template <int FAM, int KIND, uint32_t MAXP, uint32_t MINP = 0>
 __global__ __launch_bounds__(256) void k_build_lane(ProbeArgs a) {
     constexpr uint32_t DW = FAM == 4 ? 1u : 4u;              // destination dwords
     constexpr uint32_t SRC = FAM == 4 ? 26u : 22u;           // source address offset (= 2 mod 4)
@@ -981,6 +983,7 @@ __global__ __launch_bounds__(256) void k_build_lane(ProbeArgs a) {
     constexpr bool L4DST = !(FAM == 4 && KIND == kL4Icmp);   // ICMPv4 sums the message alone
     constexpr uint32_t NF = MAXP / 4u + 3u;                  // frame dwords + the next frame's head
     static_assert(SRC % 4u == 2u && DST % 4u == 2u && PAY % 4u == 2u, "halfword-shifted fields");
+    static_assert(KIND != kL4Icmp || MAXP >= PAY, "the period holds the ICMP header");
     extern __shared__ __attribute__((aligned(16))) uint8_t s_tile[];  // 256 x P + 16
     const uint32_t t = threadIdx.x, P = a.period;
     NEXG_BUILD_STAMP(0);
@@ -1011,15 +1014,28 @@ __global__ __launch_bounds__(256) void k_build_lane(ProbeArgs a) {
             F[SRC / 4u + k + 1u] |= sx[k] >> 16;
         }
     }
-    uint32_t psum = 0;
-    if (KIND == kL4Icmp && a.pay_len) {  // uniform
-        SmallPayload sp;
-        load_small_payload(a.payload, a.pay_len, sp, psum);  // realigned words, 0 past pay_len
+    uint64_t psum = 0;
+    if (KIND == kL4Icmp && a.pay_len) {  // uniform: scalar loads and SALU only
+        // (load_small_payload's v_alignbyte / v_perm forms put ~250 VALU
+        // instructions in every wave; 64-bit scalar shifts, and the payload's
+        // word sum as 256 x its LE halves, congruent mod 0xFFFF, stay scalar)
+        constexpr uint32_t NP = (MAXP - PAY + 3u) / 4u;  // payload dwords a period can hold
+        const uint64_t pa = reinterpret_cast<uint64_t>(a.payload);
+        const uint32_t n = a.pay_len, sh = 8u * (uint32_t)(pa & 3u), nw = ((uint32_t)(pa & 3u) + n + 3u) >> 2;
+        const uniform_u32_ptr src = uniform_u32(reinterpret_cast<const void*>(pa & ~3ull));
+        uint32_t raw[NP + 1];
 #pragma unroll
-        for (uint32_t m = 0; m < kSmallPay / 4u; m++) {
-            if (PAY / 4u + m < NF) F[PAY / 4u + m] |= sp.w[m] << 16;
-            if (PAY / 4u + m + 1u < NF) F[PAY / 4u + m + 1u] |= sp.w[m] >> 16;
+        for (uint32_t k = 0; k < NP + 1u; k++) raw[k] = k < nw ? src[k] : 0u;  // none past the payload
+        uint32_t le = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < NP; k++) {
+            const uint32_t x = (uint32_t)((((uint64_t)raw[k + 1] << 32) | raw[k]) >> sh);
+            const uint32_t w = 4u * k + 4u <= n ? x : 4u * k >= n ? 0u : x & ((1u << (8u * (n - 4u * k))) - 1u);
+            le += (w & 0xFFFFu) + (w >> 16);
+            if (PAY / 4u + k < NF) F[PAY / 4u + k] |= w << 16;
+            if (PAY / 4u + k + 1u < NF) F[PAY / 4u + k + 1u] |= w >> 16;
         }
+        psum = 256ull * le;  // the payload starts at an even offset: BE word sum (mod 0xFFFF)
     }
     const uint64_t S = ssum;
     if (!L4DST) {  // ICMPv4: one checksum for the batch
@@ -1038,15 +1054,24 @@ __global__ __launch_bounds__(256) void k_build_lane(ProbeArgs a) {
         const uint64_t D = 256ull * dsum;
         if (FAM == 4) F[6] |= bswap16(fold_complement(a.ip_sum + S + D));  // bytes 24-25
         if (L4DST) F[L4CK / 4u] |= bswap16(fold_complement(a.l4_sum + psum + S + D)) << (8u * (L4CK % 4u));
-        const uint32_t b0 = t * P, s = b0 & 3u, jend = (s + P - 1u) >> 2;
-        uint32_t* const tw = reinterpret_cast<uint32_t*>(s_tile) + (b0 >> 2);
-        // fully unrolled with a guard (a `break` here rolled the loop back up
-        // with dynamic register indexing of F)
+        // frame start s' = 1..4 bytes into tile dword qb = (t P - s') / 4 (s' = 4
+        // when t P is dword-aligned), so tile dword qb + j = frame bytes
+        // [4j - s', 4j - s' + 4) = v_alignbyte(F[j], F[j - 1], (4 - s') mod 4) for
+        // every lane alike; j = 0 is the previous frame's (its writer's), j runs
+        // to the dword holding byte P - 1: j <= (P - 1 + s') / 4, which is
+        // lane-dependent only for the last one or two j
+        const uint32_t b0 = t * P, s1 = ((b0 + 3u) & 3u) + 1u, sh = (4u - s1) & 3u;
+        const uint32_t jend = (P - 1u + s1) >> 2, jlo = P >> 2, jhi = (P + 3u) >> 2;
+        uint32_t* const tw = reinterpret_cast<uint32_t*>(s_tile) + ((b0 + 4u - s1) >> 2) - 1u;
+        // fully unrolled (a `break` here rolls the loop back up with dynamic
+        // register indexing of F): j <= MINP / 4 unconditionally, then uniform
+        // and per-lane guards
 #pragma unroll
-        for (uint32_t j = 0; j < NF; j++) {
-            const uint32_t v = s ? __builtin_amdgcn_alignbyte(F[j], F[j ? j - 1u : 0u], 4u - s) : F[j];
-            // j = 0 with s > 0: the dword holding the previous frame's tail (its writer's)
-            if (j <= jend && (j > 0 || s == 0)) tw[j] = v;
+        for (uint32_t j = 1; j < NF; j++) {
+            const uint32_t v = __builtin_amdgcn_alignbyte(F[j], F[j - 1u], sh);
+            if (j <= MINP / 4u) tw[j] = v;
+            else if (j <= jlo) tw[j] = v;
+            else if (j <= jhi && j <= jend) tw[j] = v;
         }
     }
     NEXG_BUILD_STAMP(1);
@@ -1172,6 +1197,16 @@ hipError_t launch_probe(ProbeArgs& a, const uint8_t* tmpl, uint32_t dw, hipStrea
     return hipGetLastError();
 }
 
+// Workgroups per CU of k_build_lane, set by its dynamic LDS (NEXG_LANE_WGS
+// overrides in the knobs build; 0 = the tile's LDS only): icmp_ping's 47-B
+// batch, 16M frames, in one process (profiles/r06/lane/lane_ab2.log): 0.693
+// of 8 TB/s written at 3 per CU, 0.663-0.667 at 4, 0.662 at 5, 0.654-0.661
+// at 6, against 0.58 for k_build_l4
+uint32_t lane_wgs_per_cu() {
+    static const uint32_t v = probe_env("NEXG_LANE_WGS", 3u, 0u, 64u);
+    return v;
+}
+
 // k_build_lane: tmpl = one period P <= kLaneMaxP; the kernel's template is the
 // period followed by its first 8 bytes (the next frame's head)
 constexpr uint32_t kLaneMaxP = 96;
@@ -1195,18 +1230,26 @@ hipError_t launch_lane(ProbeArgs& a, const uint8_t* tmpl, int fam, int kind, hip
 #endif
     // dynamic LDS: the tile (+ the last lane's tail dword), raised to set the
     // workgroups per CU (probe_wgs_per_cu, as k_build_probe)
-    const uint32_t tile_lds = kBuildTile * P + 16u, wgs = probe_wgs_per_cu();
+    const uint32_t tile_lds = kBuildTile * P + 16u, wgs = lane_wgs_per_cu();
     const uint32_t cap = wgs ? 160u * 1024u / wgs - 1024u : 0u;
-    const uint32_t lds = tile_lds > cap ? tile_lds : cap < 65536u ? cap : 65536u;
+    const uint32_t lds = tile_lds > cap ? tile_lds : cap < 65536u ? cap : 65536u;  // (1 per CU: 64 KiB)
     a.tile_order = build_tile_order();
     const dim3 g((uint32_t)ntiles), b(kBuildTile);
-    if (kind == kL4Icmp) {
-        if (fam == 4) hipLaunchKernelGGL((k_build_lane<4, kL4Icmp, kLaneMaxP>), g, b, lds, s, a);
-        else hipLaunchKernelGGL((k_build_lane<6, kL4Icmp, kLaneMaxP>), g, b, lds, s, a);
-    } else {
-        if (fam == 4) hipLaunchKernelGGL((k_build_lane<4, kL4Tcp, kLaneMaxP>), g, b, lds, s, a);
-        else hipLaunchKernelGGL((k_build_lane<6, kL4Tcp, kLaneMaxP>), g, b, lds, s, a);
-    }
+    // the unrolled frame-dword count follows the period: instances for
+    // 44-48 B (icmp_ping, 47 B), 64-68 B (its IPv6 form, 67 B; tcp_ping, 66 B)
+    // and any period up to 96 B
+    const bool p48 = P >= 44u && P <= 48u, p68 = P >= 64u && P <= 68u;
+#define NEXG_LANE(F, K)                                                                           \
+    do {                                                                                          \
+        if (p68) hipLaunchKernelGGL((k_build_lane<F, K, 68, 64>), g, b, lds, s, a);               \
+        else hipLaunchKernelGGL((k_build_lane<F, K, kLaneMaxP>), g, b, lds, s, a);                \
+    } while (0)
+    if (kind == kL4Icmp && fam == 4 && p48) hipLaunchKernelGGL((k_build_lane<4, kL4Icmp, 48, 44>), g, b, lds, s, a);
+    else if (kind == kL4Icmp && fam == 4) NEXG_LANE(4, kL4Icmp);
+    else if (kind == kL4Icmp) NEXG_LANE(6, kL4Icmp);
+    else if (fam == 4) NEXG_LANE(4, kL4Tcp);
+    else NEXG_LANE(6, kL4Tcp);
+#undef NEXG_LANE
     return hipGetLastError();
 }
 }  // namespace
@@ -1243,14 +1286,16 @@ static bool try_probe_l4(const L4Args& l, int kind, uint8_t* out, uint32_t out_s
     const uint32_t l4_hdr = kind == kL4Tcp ? 20u + l.opt_padded : 8u;
     const uint32_t l4_len = l4_hdr + l.payload_len;
     const uint32_t flen = 14u + l3 + l4_len;
-    // icmp_ping: k_build_lane (whole-dword tile writes at any frame period);
-    // tcp_ping: k_build_probe (0.72-0.89 of 8 TB/s written, round 5).
+    // icmp_ping IPv4: k_build_lane (whole-dword tile writes at any frame
+    // period); tcp_ping: k_build_probe (0.72-0.89 of 8 TB/s written, round 5).
     // Measurement overrides (knobs build): NEXG_PROBE_ICMP = 1 the template
     // kernel, 2 the per-lane k_build_l4; NEXG_PROBE_LANE_TCP = 1 k_build_lane
     // for tcp_ping (no payload)
     static const uint32_t icmp_path = probe_env("NEXG_PROBE_ICMP", 0u, 0u, 2u);
     static const bool tcp_lane = probe_env("NEXG_PROBE_LANE_TCP", 0u, 0u, 1u) == 1u;
-    const bool lane = kind == kL4Icmp ? icmp_path == 0u && lane_launch_ok(flen, out_stride, l.payload_len, out)
+    // (ICMPv6's 67 B ran 0.634-0.637 in k_build_lane against 0.656 per lane in
+    // k_build_l4, tcp_ping 0.69-0.70 against 0.80 in k_build_probe: both stay)
+    const bool lane = kind == kL4Icmp ? icmp_path == 0u && v4 && lane_launch_ok(flen, out_stride, l.payload_len, out)
                                       : tcp_lane && l.payload_len == 0 && lane_launch_ok(flen, out_stride, 0, out);
     if (!lane && ((kind != kL4Tcp && icmp_path != 1u) || !probe_launch_ok(flen, out_stride, l.payload_len, out)))
         return false;

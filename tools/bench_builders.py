@@ -58,7 +58,10 @@ def main():
     res = {"frames": n, "lib": args.lib or "default", "lds_pad": os.environ.get("NEXG_BUILD_LDS_PAD", "default"),
            "probe_wgs": os.environ.get("NEXG_PROBE_WGS", "default"), "probe_waves": os.environ.get("NEXG_PROBE_WAVES", "default"),
            "order": os.environ.get("NEXG_L4_ORDER", "default"),
-           "build_order": os.environ.get("NEXG_BUILD_ORDER", "default")}
+           "build_order": os.environ.get("NEXG_BUILD_ORDER", "default"),
+           "probe_icmp": os.environ.get("NEXG_PROBE_ICMP", "default"),
+           "probe_lane_tcp": os.environ.get("NEXG_PROBE_LANE_TCP", "default"),
+           "lane_wgs": os.environ.get("NEXG_LANE_WGS", "default")}
     for name, (flen, fn) in shapes.items():
         out = torch.empty(n * flen, dtype=torch.uint8, device="cuda")
         for _ in range(10):

@@ -96,6 +96,9 @@ for s in ${STEPS:-tests}; do
     # in-process A/B of library variants under abvar/ (LIBS=a,b,...): IMIX with an output check, then the mixes
     abspan) step ab_imix 600 python -u tools/bench_parse_ab.py --libs ${LIBS} --workloads imix,udp64 --out grouped --check --rounds 4
             step ab_mixes 600 python -u tools/bench_malformed.py --libs ${LIBS} --kinds ${KINDS:-clean,all,tcp_ts} --out grouped ;;
+    lanetests) step pytest_lane 600 python -u -m pytest tests/test_gpu_probe_batches.py tests/test_gpu_build_l4.py tests/test_gpu_tile_order.py tests/test_gpu_build_probe.py -q -x --timeout 300 --timeout-method thread ;;
+    laneab) step lane_ab 900 bash -c 'for r in 1 2; do for cfg in "" "NEXG_PROBE_ICMP=2" "NEXG_PROBE_ICMP=1" "NEXG_PROBE_LANE_TCP=1" "NEXG_PROBE_WGS=3" "NEXG_PROBE_WGS=4" "NEXG_PROBE_WGS=8" "NEXG_PROBE_WGS=0"; do env $cfg python tools/bench_builders.py --probe || exit 1; done; done' ;;
+    laneab2) step lane_ab2 900 bash -c 'for r in 1 2; do for cfg in "" "NEXG_PROBE_ICMP=2" "NEXG_LANE_WGS=3" "NEXG_LANE_WGS=5" "NEXG_LANE_WGS=6" "NEXG_PROBE_LANE_TCP=1" "NEXG_PROBE_LANE_TCP=1 NEXG_LANE_WGS=5"; do env $cfg python tools/bench_builders.py --probe || exit 1; done; done' ;;
     # the driver's own command under the kernel trace: a row for every object of its line (tools/line_trace.py)
     lineprof) step lineprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lineprof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed --no-real --no-large --no-ser
