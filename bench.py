@@ -69,13 +69,13 @@ def cpu_baseline(batch, workload, count, seconds, nthreads=1):
         offs, lens, stride = None, None, batch.stride
         nbytes = n * batch.stride
     elif batch.lengths is not None:  # offsets + lengths (capture-record shape)
-        offs = batch.offsets[:n].cpu().numpy().astype(np.uint64)
+        offs = batch.host_offsets()[:n].astype(np.uint64)
         lens = batch.lengths[:n].cpu().numpy().astype(np.uint32)
         data = batch.data[: int(offs[-1]) + int(lens[-1])].cpu().numpy()
         stride = 0
         nbytes = int(lens.sum())
     else:
-        offs = batch.offsets[: n + 1].cpu().numpy().astype(np.uint64)
+        offs = batch.host_offsets()[: n + 1].astype(np.uint64)
         data = batch.data[: int(offs[n])].cpu().numpy()
         lens, stride = None, 0
         nbytes = int(offs[n] - offs[0])

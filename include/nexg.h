@@ -381,6 +381,16 @@ typedef struct nexg_slice {
  * 256-frame group and fall back to per-frame reads where it fails, so a
  * wrong hint costs speed, never correctness. */
 #define NEXG_FRAMES_MONOTONE 0x1u
+/* NEXG_FRAMES_OFFSETS32: `offsets` points to uint32_t entries (4 bytes per
+ * frame instead of 8; any 4-B aligned address). offsets32[i] is offset(i)
+ * modulo 2^32. When data_bytes > 0xFFFFFFFF the table is followed, at the
+ * first 8-B aligned address past its count + 1 entries, by one uint64_t per
+ * 256 frames, base[k] = offset(256 k) in full (nexg_offsets32_bases), and
+ * offset(i) = base[i / 256] + (uint32_t)(offsets32[i] - (uint32_t)base[i / 256]):
+ * every frame (and, packed, the end of its group) lies within 4 GiB after
+ * its group's first frame, which packed and monotone batches satisfy by
+ * construction. nexg_offsets32_bytes gives the whole table's size. */
+#define NEXG_FRAMES_OFFSETS32 0x2u
 typedef struct nexg_frames {
     const uint8_t* data;
     uint64_t data_bytes;
@@ -390,6 +400,18 @@ typedef struct nexg_frames {
     uint32_t hints; /* NEXG_FRAMES_* */
     uint64_t count;
 } nexg_frames;
+
+/* NEXG_FRAMES_OFFSETS32 table of `count` frames: count + 1 uint32 entries,
+ * then (for batches over 4 GiB) ceil((count + 1) / 256) uint64 group bases
+ * at the next 8-B boundary. */
+static inline const uint64_t* nexg_offsets32_bases(const void* table, uint64_t count) {
+    const uintptr_t end = (uintptr_t)table + 4u * (uintptr_t)(count + 1u);
+    return (const uint64_t*)((end + 7u) & ~(uintptr_t)7u);
+}
+static inline uint64_t nexg_offsets32_bytes(uint64_t count, int with_bases) {
+    const uint64_t b = (4u * (count + 1u) + 7u) & ~(uint64_t)7u;
+    return with_bases ? b + 8u * ((count + 1u + 255u) / 256u) : 4u * (count + 1u);
+}
 
 /* ---- context ----------------------------------------------------------- */
 typedef struct nexg_ctx nexg_ctx;

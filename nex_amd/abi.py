@@ -53,6 +53,45 @@ OUT_GROUPED = 7  # SPARSE with uniform 64-frame groups as a head byte + 2 verdic
 
 # NEXG_FRAMES_* hints (nexg_frames.hints)
 FRAMES_MONOTONE = 0x1
+FRAMES_OFFSETS32 = 0x2  # u32 offset table (+ 64-bit group bases over 4 GiB)
+
+
+def offsets32_layout(count, with_bases):
+    """(u32 entries, byte offset of the u64 group bases, base count, total
+    bytes) of a NEXG_FRAMES_OFFSETS32 table for `count` frames whose table
+    starts 8-B aligned (include/nexg.h nexg_offsets32_bytes)."""
+    n = count + 1
+    base_off = (4 * n + 7) // 8 * 8
+    nb = (n + 255) // 256 if with_bases else 0
+    return n, base_off, nb, (base_off + 8 * nb) if with_bases else 4 * n
+
+
+def offsets32_table(offsets64, data_bytes):
+    """numpy u64 offsets (count + 1 entries) -> the NEXG_FRAMES_OFFSETS32
+    table as a uint8 array: offsets mod 2^32, then (data_bytes > 0xFFFFFFFF)
+    the full offset of every 256th frame."""
+    o = np.asarray(offsets64, dtype=np.uint64)
+    count = len(o) - 1
+    with_bases = data_bytes > 0xFFFFFFFF
+    n, base_off, nb, total = offsets32_layout(count, with_bases)
+    buf = np.zeros(total, np.uint8)
+    buf[: 4 * n].view(np.uint32)[:] = (o & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    if with_bases:
+        buf[base_off:].view(np.uint64)[:] = o[::256]
+    return buf
+
+
+def offsets32_decode(table, count, data_bytes):
+    """The full u64 offsets (count + 1) of a NEXG_FRAMES_OFFSETS32 table
+    (uint8 array), as the kernels read it."""
+    t = np.asarray(table, np.uint8)
+    with_bases = data_bytes > 0xFFFFFFFF
+    n, base_off, nb, _ = offsets32_layout(count, with_bases)
+    lo = t[: 4 * n].view(np.uint32).astype(np.uint64)
+    if not with_bases:
+        return lo
+    b = t[base_off: base_off + 8 * nb].view(np.uint64)[np.arange(n) >> 8]
+    return b + ((lo - (b & np.uint64(0xFFFFFFFF))) & np.uint64(0xFFFFFFFF))
 
 # NEXG_OUT_SPARSE code byte
 SPARSE_IP_OK = 0x10
@@ -346,7 +385,7 @@ FIXUP_DTYPE = np.dtype([("done", "u1"), ("proto", "u1"), ("ip_csum", "<u2"), ("l
 assert FIXUP_DTYPE.itemsize == 8
 
 #: static inline helpers of include/nexg.h (header-only, not exported)
-HEADER_INLINE = ("nexg_sparse_decode", "nexg_grouped_code")
+HEADER_INLINE = ("nexg_sparse_decode", "nexg_grouped_code", "nexg_offsets32_bases", "nexg_offsets32_bytes")
 
 #: every symbol include/nexg.h declares (tests check the .so exports them)
 EXPORTED_SYMBOLS = (

@@ -92,6 +92,7 @@ bool frames_valid(const nexg_frames* f) {
     if (!f->data) return false;
     if (!f->offsets && f->stride == 0) return false;
     if ((reinterpret_cast<uint64_t>(f->data) & 3u) != 0) return false;  // 4-B aligned base
+    if ((f->hints & NEXG_FRAMES_OFFSETS32) && (reinterpret_cast<uint64_t>(f->offsets) & 3u) != 0) return false;
     return true;
 }
 
@@ -104,6 +105,8 @@ nexg::ParseArgs to_args(const nexg_frames* f) {
     a.stride = f->stride;
     a.count = f->count;
     a.hints = f->hints;
+    if ((f->hints & NEXG_FRAMES_OFFSETS32) && f->offsets && f->data_bytes > 0xFFFFFFFFull)
+        a.off_bases = nexg_offsets32_bases(f->offsets, f->count);
     return a;
 }
 

@@ -25,6 +25,7 @@ struct ParseArgs {
                               // narrower than 4 B per frame; null -> the output itself
     uint64_t* stamps = nullptr;  // k_parse_span<..., TIMING>: 8 clock stamps per workgroup
     uint8_t* grouped_heads = nullptr;  // span kernel, NEXG_OUT_GROUPED run as SPARSE at the code offset: head bytes (all 0)
+    const uint64_t* off_bases = nullptr;  // NEXG_FRAMES_OFFSETS32 over 4 GiB: one full offset per 256 frames
 };
 
 // Kernel variants of the parse path.

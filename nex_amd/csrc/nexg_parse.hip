@@ -407,9 +407,9 @@ hipError_t launch_probe_latency(uint32_t* buf, uint32_t lines, uint32_t start, u
 __global__ __launch_bounds__(256) void k_checksum(ParseArgs a, uint32_t skipword, uint16_t* out) {
     const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
     if (idx >= a.count) return;
-    const uint64_t off = a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride;
+    const uint64_t off = a.offsets ? table_off(a, idx, idx) : idx * (uint64_t)a.stride;
     const uint64_t l64 = a.lengths ? (uint64_t)a.lengths[idx]
-                                   : (a.offsets ? a.offsets[idx + 1] - off : (uint64_t)a.stride);
+                                   : (a.offsets ? table_off(a, idx + 1, idx) - off : (uint64_t)a.stride);
     if (l64 == 0 || l64 > 65535u || off > a.data_bytes || l64 > a.data_bytes - off) {
         out[idx] = 0;
         return;

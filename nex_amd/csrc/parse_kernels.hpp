@@ -177,6 +177,18 @@ __device__ __forceinline__ void stage_record(uint8_t* slot, const nexg_record& r
     for (int k = 0; k < 4; k++) reinterpret_cast<uint4*>(slot)[k] = v[k];
 }
 
+// Offset i of the batch's table (include/nexg.h): u64 entries, or with
+// NEXG_FRAMES_OFFSETS32 u32 entries, completed from the 256-frame group base
+// of frame g when the batch is over 4 GiB (g = i, or for a packed frame's end
+// the frame itself: its end lies within 4 GiB of its own group's base)
+__device__ __forceinline__ uint64_t table_off(const ParseArgs& a, uint64_t i, uint64_t g) {
+    if (!(a.hints & NEXG_FRAMES_OFFSETS32)) return NEXG_GLOBAL(uint64_t, a.offsets)[i];
+    const uint32_t o = NEXG_GLOBAL(uint32_t, a.offsets)[i];
+    if (!a.off_bases) return o;
+    const uint64_t b = NEXG_GLOBAL(uint64_t, a.off_bases)[g >> 8];
+    return b + (uint32_t)(o - (uint32_t)b);
+}
+
 // MODE 0: fixed stride tile staging (STRIDE = 0 -> runtime stride).
 // MODE 1: per-lane window staging.
 template <int MODE, int OUT, int STRIDE, int WIN, bool FAST = true, bool NT = false>
@@ -235,10 +247,10 @@ __global__ __launch_bounds__(256) void k_parse(ParseArgs a) {
     } else {
         // SPARSE stores need every lane of the wave; other outputs leave early
         if (!sparse_like(OUT) && tid >= nf) return;
-        const uint64_t off = tid < nf ? (a.offsets ? a.offsets[idx] : idx * (uint64_t)a.stride) : 0u;
+        const uint64_t off = tid < nf ? (a.offsets ? table_off(a, idx, idx) : idx * (uint64_t)a.stride) : 0u;
         const uint64_t l64 = tid >= nf ? 0u
                              : a.lengths ? (uint64_t)a.lengths[idx]
-                                         : (a.offsets ? a.offsets[idx + 1] - off : (uint64_t)a.stride);
+                                         : (a.offsets ? table_off(a, idx + 1, idx) - off : (uint64_t)a.stride);
         bad = l64 > 65535u || off > a.data_bytes || l64 > a.data_bytes - off;
         if (!bad && tid < nf) {
             len = (uint32_t)l64;
@@ -340,11 +352,23 @@ __device__ __forceinline__ uint32_t* handoff_slot(const ParseArgs& a, uint64_t i
 // then offsets[idx + 1]: two dependent round trips at every workgroup's start)
 __device__ __forceinline__ bool frame_extent(const ParseArgs& a, uint64_t idx, uint64_t& off, uint32_t& len) {
     uint64_t l64;
-    if (a.offsets && !a.lengths) {  // packed: the next frame's offset ends this one
+    if (a.offsets && !a.lengths && (a.hints & NEXG_FRAMES_OFFSETS32)) {  // packed, u32 table
+        const auto* op = NEXG_GLOBAL(uint32_t, a.offsets);
+        const uint32_t o0 = op[idx], o1 = op[idx + 1];
+        uint64_t b = 0;
+        if (a.off_bases) b = NEXG_GLOBAL(uint64_t, a.off_bases)[idx >> 8];
+        off = b + (uint32_t)(o0 - (uint32_t)b);
+        l64 = (uint32_t)(o1 - o0);  // < 4 GiB by the table's contract
+    } else if (a.offsets && !a.lengths) {  // packed: the next frame's offset ends this one
         const auto* op = NEXG_GLOBAL(uint64_t, a.offsets);
         const uint64_t o0 = op[idx], o1 = op[idx + 1];
         off = o0;
         l64 = o1 - o0;
+    } else if (a.offsets && (a.hints & NEXG_FRAMES_OFFSETS32)) {
+        const uint64_t o0 = table_off(a, idx, idx);
+        const uint32_t l = NEXG_GLOBAL(uint32_t, a.lengths)[idx];
+        off = o0;
+        l64 = l;
     } else if (a.offsets) {
         const uint64_t o0 = NEXG_GLOBAL(uint64_t, a.offsets)[idx];
         const uint32_t l = NEXG_GLOBAL(uint32_t, a.lengths)[idx];

@@ -47,7 +47,9 @@ class FrameBatch:
     """A device-resident batch of raw frames (nexg_frames).
 
     data     uint8 tensor on the device
-    offsets  int64 tensor (count or count+1 entries) or None (fixed stride)
+    offsets  int64 tensor (count or count+1 entries), or a uint8 tensor
+             holding a NEXG_FRAMES_OFFSETS32 table (abi.offsets32_table;
+             hints must carry abi.FRAMES_OFFSETS32), or None (fixed stride)
     lengths  int32 tensor or None
     """
     data: "object"
@@ -65,22 +67,45 @@ class FrameBatch:
             lengths=None if self.lengths is None else self.lengths.data_ptr(),
             stride=self.stride, hints=self.hints, count=self.count)
 
+    def host_offsets(self):
+        """Host int64 array of the table's offsets (count + 1 entries for a
+        packed batch), decoding a NEXG_FRAMES_OFFSETS32 table."""
+        if self.hints & abi.FRAMES_OFFSETS32:
+            return abi.offsets32_decode(self.offsets.cpu().numpy(), self.count,
+                                        self.data.numel()).astype(np.int64)
+        return self.offsets.cpu().numpy().astype(np.int64)
+
     def frame_lengths(self):
         """Host int64 array of every frame's length (the nexg_frames rules)."""
         if self.lengths is not None:
             return self.lengths[: self.count].cpu().numpy().astype(np.int64)
         if self.offsets is not None:
-            o = self.offsets[: self.count + 1].cpu().numpy().astype(np.int64)
-            return np.diff(o)
+            return np.diff(self.host_offsets()[: self.count + 1])
         return np.full(self.count, self.stride, np.int64)
 
     @property
     def total_bytes(self):
         if self.lengths is not None:
             return int(self.lengths.sum().item())
+        if self.offsets is not None and self.hints & abi.FRAMES_OFFSETS32:
+            o = self.host_offsets()
+            return int(o[self.count] - o[0])
         if self.offsets is not None:
             return int((self.offsets[self.count] - self.offsets[0]).item())
         return self.count * self.stride
+
+    def with_offsets32(self):
+        """The same frames described by a NEXG_FRAMES_OFFSETS32 table (4 B per
+        frame instead of 8, plus one 8-B base per 256 frames over 4 GiB)."""
+        torch = _torch()
+        assert self.offsets is not None and not self.hints & abi.FRAMES_OFFSETS32
+        n = self.count + (0 if self.lengths is not None else 1)
+        o = self.offsets[:n].cpu().numpy().astype(np.uint64)
+        if self.lengths is not None:  # count entries: the table still has count + 1 slots
+            o = np.concatenate([o, o[-1:] if len(o) else np.zeros(1, np.uint64)])
+        t = torch.from_numpy(abi.offsets32_table(o, self.data.numel())).to(self.data.device)
+        return FrameBatch(data=self.data, count=self.count, stride=self.stride, offsets=t, lengths=self.lengths,
+                          hints=self.hints | abi.FRAMES_OFFSETS32)
 
     @classmethod
     def from_frames(cls, frames: Sequence[bytes], device="cuda", pad_to=4):

@@ -17,7 +17,7 @@ LIB = os.path.join(ROOT, "nex_amd", "libnexg.so")
 
 def declared_functions():
     text = open(HDR).read()
-    inline = set(re.findall(r"static inline \w+ (nexg_[a-z0-9_]+)\s*\(", text))
+    inline = set(re.findall(r"static inline [\w\s*]*?\b(nexg_[a-z0-9_]+)\s*\(", text))
     assert inline == set(abi.HEADER_INLINE)
     return sorted(set(re.findall(r"\b(nexg_[a-z0-9_]+)\s*\(", text)) - inline)
 
@@ -140,3 +140,26 @@ def test_error_contexts_match_header():
     assert len(pairs) == len(abi.ERR_CONTEXTS) - 1
     for v, ctx in pairs:
         assert abi.ERR_CONTEXTS[int(v)] == ctx
+
+
+def test_offsets32_table_roundtrip():
+    """abi.offsets32_table / offsets32_decode (include/nexg.h
+    NEXG_FRAMES_OFFSETS32): under 4 GiB the table is the low 32 bits alone;
+    over 4 GiB the u64 group bases at the next 8-B boundary restore every
+    offset, including groups that straddle a 4-GiB multiple."""
+    import numpy as np
+    from nex_amd import abi
+    rng = np.random.default_rng(3)
+    for count, start, data_bytes in ((1, 0, 100), (255, 7, 1 << 20), (256, 0, 1 << 20), (1000, 0, 1 << 20),
+                                     (70_000, (1 << 32) - 3_000_000, 9 << 30)):
+        lens = rng.integers(0, 1500, count, dtype=np.uint64)
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(start)
+        t = abi.offsets32_table(offs, data_bytes)
+        with_bases = data_bytes > 0xFFFFFFFF
+        n, base_off, nb, total = abi.offsets32_layout(count, with_bases)
+        assert len(t) == total and n == count + 1
+        assert (t[: 4 * n].view(np.uint32) == (offs & np.uint64(0xFFFFFFFF))).all()
+        if with_bases:
+            assert base_off % 8 == 0 and nb == (count + 256) // 256
+            assert int(offs[-1]) > (1 << 32) > int(offs[0])  # the case crosses 4 GiB
+        assert (abi.offsets32_decode(t, count, data_bytes) == offs).all()

@@ -162,3 +162,45 @@ def test_desc_output_at_8_mod_16(engine, mixed, layout):
     torch.cuda.synchronize()
     assert torch.equal(buf[8: 8 + n], want)
     assert bool((buf[:8] == 0xA5).all()) and bool((buf[8 + n:] == 0xA5).all())
+
+
+def test_offsets32_small_layouts(engine, mixed):
+    """NEXG_FRAMES_OFFSETS32 under 4 GiB (no group bases): packed, packed at
+    an unaligned start, offsets + lengths with and without the monotone hint
+    give the u64 table's outputs in every output kind, and the checksum batch
+    and the fix-up read the same frames."""
+    import torch
+    for b64 in (FrameBatch.from_packed(mixed, pad_to=1, shift=0), FrameBatch.from_packed(mixed, pad_to=4, shift=12),
+                FrameBatch.from_frames(mixed)):
+        for hints in ((0, abi.FRAMES_MONOTONE) if b64.lengths is not None else (0,)):
+            b64.hints = hints
+            b32 = b64.with_offsets32()
+            assert b32.hints & abi.FRAMES_OFFSETS32
+            for kind in (abi.OUT_RECORD, abi.OUT_GROUPED, abi.OUT_DESC, abi.OUT_SPARSE, abi.OUT_FLAGS):
+                n = max(engine.out_bytes(kind, b64.count), 16)
+                want, got = (torch.zeros(n, dtype=torch.uint8, device="cuda") for _ in range(2))
+                engine.parse(b64, out_kind=kind, out=want)
+                engine.parse(b32, out_kind=kind, out=got)
+                assert torch.equal(got, want), (kind, hints)
+            assert torch.equal(engine.checksum(b32, 5), engine.checksum(b64, 5))
+
+
+def test_offsets32_imix_over_4gib(engine):
+    """The 16M IMIX batch (5.95 GB, past 4 GiB: the table's group bases carry
+    the high bits) with a u32 table: the grouped output equals the u64
+    table's byte for byte, and the descriptors too."""
+    import torch
+    b64 = engine.gen_batch(abi.WL_IMIX, 16 << 20)
+    assert b64.data.numel() > 0xFFFFFFFF
+    b32 = b64.with_offsets32()
+    assert b32.offsets.numel() == abi.offsets32_layout(b64.count, True)[3]
+    assert b32.total_bytes == b64.total_bytes
+    for kind in (abi.OUT_GROUPED, abi.OUT_DESC):
+        n = engine.out_bytes(kind, b64.count)
+        want = torch.empty(n, dtype=torch.uint8, device="cuda")
+        got = torch.empty(n, dtype=torch.uint8, device="cuda")
+        engine.parse(b64, out_kind=kind, out=want)
+        engine.parse(b32, out_kind=kind, out=got)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), kind
+        del want, got

@@ -3,7 +3,8 @@
 UDP64 (and optionally IMIX) batch and output buffer, each build timed with HIP
 events, interleaved A B C A B C. Output-width experiments write different
 bytes, so outputs are compared only with --check.
-usage: python tools/bench_parse_ab.py --libs A.so,B.so [--workloads udp64,imix,mix,real] [--out sparse]"""
+usage: python tools/bench_parse_ab.py --libs A.so,B.so [--workloads udp64,imix,mix,real] [--out sparse]
+       [--tables 64,32]   (each build with the u64 and the NEXG_FRAMES_OFFSETS32 offset table)"""
 import argparse
 import json
 import os
@@ -22,6 +23,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--tables", default="64", help="offset-table forms of packed batches: 64, 32 or 64,32")
     args = ap.parse_args()
     import torch
     from nex_amd import _lib, abi
@@ -44,25 +46,29 @@ def main():
         else:
             b = engines[0].gen_batch(abi.WL_UDP64 if wl == "udp64" else abi.WL_IMIX, 16 << 20)
         out = torch.empty(Engine.out_bytes(ok, b.count), dtype=torch.uint8, device="cuda")
+        forms = {"64": b}
+        if "32" in args.tables.split(",") and b.offsets is not None:
+            forms["32"] = b.with_offsets32()
+        variants = [(f"{l}:{t}" if len(forms) > 1 else l, e, forms[t]) for l, e in zip(libs, engines)
+                    for t in args.tables.split(",") if t in forms]
         if args.check:
             ref = None
-            for l, e in zip(libs, engines):
+            for l, e, bb in variants:
                 out.zero_()
-                e.parse(b, out_kind=ok, out=out, stream=s)
+                e.parse(bb, out_kind=ok, out=out, stream=s)
                 torch.cuda.synchronize()
                 ref = out.clone() if ref is None else ref
                 assert torch.equal(out, ref), f"{l}: output differs"
-        times = {l: [] for l in libs}
+        times = {l: [] for l, _, _ in variants}
         for rnd in range(args.rounds):
-            pairs = list(zip(libs, engines))
-            for l, e in (pairs[::-1] if rnd % 2 else pairs):  # alternate the order (first-measured bias)
+            for l, e, bb in (variants[::-1] if rnd % 2 else variants):  # alternate the order (first-measured bias)
                 for _ in range(args.warmup):
-                    e.parse(b, out_kind=ok, out=out, stream=s)
+                    e.parse(bb, out_kind=ok, out=out, stream=s)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
                 e0.record(s)
                 for _ in range(args.steps):
-                    e.parse(b, out_kind=ok, out=out, stream=s)
+                    e.parse(bb, out_kind=ok, out=out, stream=s)
                 e1.record(s)
                 torch.cuda.synchronize()
                 times[l].append(round(e0.elapsed_time(e1) / args.steps, 4))
@@ -70,7 +76,7 @@ def main():
                           "kernel_ms": times,
                           "frac_best": {l: round(b.total_bytes / (min(t) * 1e-3) / 8e12, 4) for l, t in times.items()}}),
               flush=True)
-        del b, out
+        del b, out, forms, variants
         torch.cuda.empty_cache()
 
 
