@@ -340,7 +340,7 @@ def stream_ceilings(eng, batch, args, stream, device):
     out = torch.empty(max(batch.data.numel() // 8, need + 16), dtype=torch.uint8, device=device)
     nbytes = batch.data.numel() // 16384 * 16384
     r = {}
-    for key, w8 in (("read_only_gbs", False), ("read64_write8_gbs", True)):
+    for key, w8 in (("read_only_gbs", False), ("read64_write8_gbs", True), ("read64_write8_6cu_gbs", 9)):
         _, ks = timed(lambda: eng.probe_stream(batch.data, w8, out=out, stream=stream),
                       args.steps, args.warmup, stream, device)
         r[key] = round(nbytes / ks / 1e9, 1)

@@ -521,6 +521,8 @@ int nexg_decode_options(nexg_ctx* ctx, const nexg_frames* frames, const nexg_rec
  * 256-lane workgroup). out_per_64 = 8: for every 64 B read, 8 B written
  * (the nexg_desc stream shape): out[i] = {x, i} with x the XOR of the four
  * 16-B chunks lane i % 256 of tile i / 256 loaded (chunks i%256 + 256k).
+ * out_per_64 = 9: the same stream capped at the fixed-stride parse kernel's
+ * occupancy (6 workgroups per CU, by dynamic LDS; 8 runs 8 per CU).
  * out_per_64 = 0: read only; out[tile] = XOR of the tile's dwords (4 B per
  * 16 KiB). bench.py reports the headline kernel against both.
  * out_per_64 = 64: write only (the builders' copy-out shape: 16-B

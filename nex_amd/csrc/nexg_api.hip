@@ -258,7 +258,7 @@ int nexg_probe_stream(nexg_ctx* ctx, const void* data, uint64_t bytes, uint32_t 
     if (!ctx) return NEXG_EINVAL;
     const bool wo = out_per_64 == 64;  // write-only: data unused
     if (bytes % 16384u != 0 || (bytes && ((!wo && !data) || !out)) ||
-        (out_per_64 != 0 && out_per_64 != 8 && !wo) || (reinterpret_cast<uint64_t>(data) & 15u) != 0 ||
+        (out_per_64 != 0 && out_per_64 != 8 && out_per_64 != 9 && !wo) || (reinterpret_cast<uint64_t>(data) & 15u) != 0 ||
         (reinterpret_cast<uint64_t>(out) & (wo ? 15u : 7u)) != 0)
         return fail(ctx, NEXG_EINVAL, "probe: bytes must be a multiple of 16384, buffers aligned%s", nullptr);
     if (bytes / 16384u > 0x7FFFFFFFull) return fail(ctx, NEXG_ERANGE, "probe: too many tiles%s", nullptr);

@@ -301,7 +301,9 @@ hipError_t launch_decode_options(const ParseArgs& a, const nexg_record* recs, ne
 template <bool W8>
 __global__ __launch_bounds__(256) void k_probe_stream(const uint8_t* data, void* out, uint32_t order) {
     __shared__ uint32_t s_x[4];
+    extern __shared__ uint32_t s_occ[];  // dynamic LDS: caps workgroups per CU only (out_per_64 = 9)
     const uint32_t t = threadIdx.x;
+    if (order == 0xFFFFFFFFu) s_occ[t] = 0u;
     const uint64_t tile = tile_index(order);
     const uint8_t* T = data + tile * 16384u;
     uint4 v[4];
@@ -347,6 +349,9 @@ hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, uint32_t mod
         hipLaunchKernelGGL(k_probe_write, dim3((uint32_t)tiles), dim3(kTile), 16400u + build_lds_pad(), s,
                            static_cast<uint8_t*>(out), wo);
     else if (mode == 8) hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out, ro);
+    else if (mode == 9)  // 6 workgroups per CU: the fixed-stride parse kernel's occupancy
+        hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 160u * 1024u / 6u - 1024u, s, data,
+                           out, ro);
     else hipLaunchKernelGGL(k_probe_stream<false>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out, ro);
     return hipGetLastError();
 }

@@ -652,6 +652,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 #ifndef NEXG_SPAN_NT
 #define NEXG_SPAN_NT true  // sub-tile fetch cache policy (A/B builds override)
 #endif
+#ifndef NEXG_SPAN_DEPTH
+#define NEXG_SPAN_DEPTH 1  // sub-tiles in flight beside the one being scanned (A/B builds: 2)
+#endif
 template <int OUT, int NB = 1, uint32_t SUB = 16384, int WPE = 1, bool TIMING = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_parse_span(ParseArgs a) {
     // each stage buffer: [96-B apron | SUB bytes | 96-B pad]; the apron holds
@@ -695,6 +698,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // range of the batch, so every load stays inside its 16-B blocks
     constexpr int CPT = SUB / 4096u;  // 16-B chunks per thread per sub-tile
     uint4 cur[CPT];
+#if NEXG_SPAN_DEPTH == 2
+    uint4 nxt[CPT];
+#endif
     auto fetch = [&](uint32_t S, uint4 (&v)[CPT]) {
 #pragma unroll
         for (int i = 0; i < CPT; i++) {
@@ -703,7 +709,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
     };
     const bool plausible = hi >= lo && hi <= a.data_bytes && hi - lo <= (1ull << 30);
-    if (plausible) fetch(0, cur);
+    if (plausible) {
+        fetch(0, cur);
+#if NEXG_SPAN_DEPTH == 2
+        fetch(SUB, nxt);  // (chunks past the span load nothing)
+#endif
+    }
     // packed contract: every frame of the group lies inside [lo, hi], and the
     // span is small enough for 32-bit span-relative arithmetic
     const bool inside = !have || (ok && off >= lo && off + len <= hi);
@@ -739,7 +750,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     for (int j = 0; j < 21; j++) u[j] = 0;
 
     uint32_t buf = 0;
-    for (uint32_t S = 0; S < span; S += SUB, buf = NB == 2 ? buf ^ 1u : 0u) {
+    // one sub-tile: stage v (this sub-tile's chunks) into LDS, refill v with the
+    // sub-tile NEXG_SPAN_DEPTH ahead, scan, gather
+    auto sub_tile = [&](const uint32_t S, uint4 (&v)[CPT]) {
         uint8_t* sb = s_bytes[buf] + kApron;
         uint32_t* sp = s_pfx[buf];
         // (1) stage bytes + chunk sums, put the next sub-tile in flight. The
@@ -753,11 +766,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int i = 0; i < CPT; i++) {
             const uint32_t c = t + 256u * i;
-            *reinterpret_cast<uint4*>(sb + 16u * c) = cur[i];
-            sp[c] = chunk_le_sum(cur[i]);
+            *reinterpret_cast<uint4*>(sb + 16u * c) = v[i];
+            sp[c] = chunk_le_sum(v[i]);
         }
         const uint32_t E = S + SUB;
-        if (E < span) fetch(E, cur);
+        if (S + NEXG_SPAN_DEPTH * SUB < span) fetch(S + NEXG_SPAN_DEPTH * SUB, v);
         __syncthreads();
         // (2) block exclusive scan of the 1024 chunk sums (4 consecutive per thread)
         uint32_t cs[CPT];
@@ -803,7 +816,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (have && (db < SUB || (last && db == SUB))) qb = q_at(db);
         run += total;
         if (NB == 1) __syncthreads();
+    };
+#if NEXG_SPAN_DEPTH == 2
+    // two sub-tiles in flight: the loop unrolled by two over two register sets
+    // (a copy between them would wait for the loads in flight)
+    static_assert(NB == 1, "depth 2 runs on one stage buffer");
+    for (uint32_t S = 0; S < span; S += 2u * SUB) {
+        sub_tile(S, cur);
+        if (S + SUB < span) sub_tile(S + SUB, nxt);
     }
+#else
+    for (uint32_t S = 0; S < span; S += SUB, buf = NB == 2 ? buf ^ 1u : 0u) sub_tile(S, cur);
+#endif
     if (NB == 2) __syncthreads();  // the stage buffers become per-lane slots below
     NEXG_SPAN_STAMP(2);
     uint8_t* const slots = &s_bytes[0][0];  // 80 B per lane from here on

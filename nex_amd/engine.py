@@ -275,16 +275,17 @@ class Engine:
                                                  self._stream(stream)))
         return out
 
-    def probe_stream(self, data, write8: bool, out=None, stream=None):
+    def probe_stream(self, data, write8, out=None, stream=None):
         """Calibration stream over a uint8 device tensor (nexg_probe_stream):
         the parse kernels' load shape, read-only or with the 8-B-per-64-B
-        descriptor store stream. Not a reference entry point."""
+        descriptor store stream (write8 = 9: that stream at the fixed-stride
+        parse kernel's 6 workgroups per CU). Not a reference entry point."""
         torch = _torch()
         nbytes = data.numel() // 16384 * 16384
         if out is None:
             n = nbytes // 64 * 8 if write8 else nbytes // 16384 * 4
             out = torch.empty(max(n, 8), dtype=torch.uint8, device=self.torch_device)
-        self._check(self.lib.nexg_probe_stream(self.ctx, _ptr(data), nbytes, 8 if write8 else 0,
+        self._check(self.lib.nexg_probe_stream(self.ctx, _ptr(data), nbytes, 9 if write8 == 9 else 8 if write8 else 0,
                                                _ptr(out), self._stream(stream)))
         return out
 

@@ -5,6 +5,7 @@
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 out=$(realpath -m "$1"); shift
+mkdir -p "$(dirname "$out")"
 tmp=$(mktemp -d)
 mkdir -p "$tmp/a/b" && cp -r "$ROOT/nex_amd/csrc" "$tmp/a/b/csrc" && cp -r "$ROOT/include" "$tmp/a/include"
 rm -rf "$tmp/a/b/csrc/build"

@@ -101,6 +101,9 @@ for s in ${STEPS:-tests}; do
     laneab2) step lane_ab2 900 bash -c 'for r in 1 2; do for cfg in "" "NEXG_PROBE_ICMP=2" "NEXG_LANE_WGS=3" "NEXG_LANE_WGS=5" "NEXG_LANE_WGS=6" "NEXG_PROBE_LANE_TCP=1" "NEXG_PROBE_LANE_TCP=1 NEXG_LANE_WGS=5"; do env $cfg python tools/bench_builders.py --probe || exit 1; done; done' ;;
     o32tests) step pytest_o32 600 python -u -m pytest tests/test_gpu_span.py tests/test_gpu_grouped.py tests/test_gpu_sparse.py tests/test_gpu_fixup.py -q -x --timeout 300 --timeout-method thread ;;
     o32ab) step o32_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so --tables 64,32 --workloads imix,mix,real --out grouped --check --rounds 4 ;;
+    depthab) step depth_ab 1100 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_d2w4.so,abx/libnexg_d2w4s16.so,abx/libnexg_d2w4s20.so,abx/libnexg_d1w4.so --workloads imix,mix,real --out grouped --check --rounds 3 ;;
+    mixkinds) step mix_kinds 900 python -u tools/bench_malformed.py --libs nex_amd/libnexg.so,abx/libnexg_d1w4.so --kinds clean,truncate,pad,ip_length,ver_ihl,l4_length,ipv6_hbh,vlan,proto200,random --out grouped
+              step mix_phases 600 python -u tools/span_phases_ab.py --libs nex_amd/libnexg.so,abx/libnexg_d1w4.so --workloads imix,mix ;;
     # the driver's own command under the kernel trace: a row for every object of its line (tools/line_trace.py)
     lineprof) step lineprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lineprof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed --no-real --no-large --no-ser

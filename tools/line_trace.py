@@ -35,6 +35,8 @@ def expected(line):
     if "read_only_gbs" in sc:
         ex.append(("stream.read_only", "k_probe_stream", line["steps"], nb // 16384 * 16384, None))
         ex.append(("stream.read64_write8", "k_probe_stream", line["steps"], nb // 16384 * 16384, None))
+        if "read64_write8_6cu_gbs" in sc:
+            ex.append(("stream.read64_write8_6cu", "k_probe_stream", line["steps"], nb // 16384 * 16384, None))
         for k in ("desc_output", "flags_output", "verdict_output", "sparse_output", "grouped_output"):
             if k in sc:
                 ex.append((f"stream.{k}", "k_parse", line["steps"], nb, sc[k]["kernel_ms"]))
@@ -68,14 +70,16 @@ def runs(trace_csv):
             k = r["Kernel_Name"]
             if "nexg::" not in k or any(s in k for s in SKIP):
                 continue
-            rows.append((int(r["Start_Timestamp"]), k, int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+            # (kernel, LDS size): the occupancy-capped stream (dynamic LDS) is its own run
+            key = (k, r.get("LDS_Block_Size", ""))
+            rows.append((int(r["Start_Timestamp"]), key, int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     rows.sort()
     out = []
-    for _, k, d in rows:
-        if out and out[-1][0] == k:
+    for _, key, d in rows:
+        if out and out[-1][2] == key:
             out[-1][1].append(d)
         else:
-            out.append((k, [d]))
+            out.append((key[0], [d], key))
     return out
 
 
@@ -99,7 +103,7 @@ def main():
         if i == len(rs):
             rows[name] = {"error": f"no run of {kern} with >= {k + 1} launches left"}
             continue
-        kn, ds = rs[i]
+        kn, ds, _ = rs[i]
         i += 1
         last = ds[-k:]
         avg_ms = sum(last) / len(last) / 1e6
