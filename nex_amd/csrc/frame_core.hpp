@@ -243,8 +243,12 @@ NEXG_HD uint32_t span_tail_end(uint32_t b12, uint32_t b16, uint32_t len, uint32_
 #ifndef NEXG_SPAN_PROBE
 #define NEXG_SPAN_PROBE(k, c)
 #endif
+#ifndef NEXG_SPAN_SLOT
+#define NEXG_SPAN_SLOT 80  // bytes of a declined frame's head in its LDS slot (A/B builds: 128)
+#endif
 struct SpanFrame {
-    static constexpr uint32_t kSlot = 80;
+    static constexpr uint32_t kSlot = NEXG_SPAN_SLOT;
+    static_assert(kSlot >= 80 && kSlot % 16 == 0, "the slot holds the 80-B fast-path window");
     static constexpr uint32_t kDefer = 64;
     const uint8_t* slot;
     const uint8_t* g;
@@ -267,7 +271,11 @@ struct SpanFrame {
     }
     NEXG_HD uint64_t le_sum(uint32_t a, uint32_t b) const {
         uint64_t acc = 0;
-        const uint32_t lb = b < kSlot ? b : kSlot;
+        // a range to tail_end from at most byte 80: [a, 80) from the slot and
+        // the scanned tail sum of [80, tail_end); any other range: the slot's
+        // part, then HBM past the slot
+        const bool to_end = b == tail_end && tail_end > 80u && a <= 80u;
+        const uint32_t lb = to_end ? 80u : b < kSlot ? b : kSlot;
         if (a < lb) {  // frame-relative LE sum, x256 for an odd frame (congruent, 0 iff 0)
             const uint32_t* w = reinterpret_cast<const uint32_t*>(slot);
             uint32_t s = 0;
@@ -275,16 +283,14 @@ struct SpanFrame {
             acc = parity ? (uint64_t)s * 256u : (uint64_t)s;
         }
         const uint32_t ga = a > kSlot ? a : kSlot;
-        const bool to_end = b == tail_end && tail_end > 80u && ga <= 80u;
-        const uint32_t gb = to_end ? 80u : b;
-        if (ga < gb) {
+        if (!to_end && ga < b) {
             const uint64_t base = reinterpret_cast<uint64_t>(g);
-            if (gb - ga > kDefer && d.rng == 0) {
-                d.rng = ga | (gb - ga) << 16;
+            if (b - ga > kDefer && d.rng == 0) {
+                d.rng = ga | (b - ga) << 16;
                 pend = true;
             } else {
                 NEXG_SPAN_PROBE(1, true);
-                acc += global_le_sum(base + ga, base + gb);
+                acc += global_le_sum(base + ga, base + b);
             }
         }
         if (to_end) acc += tail;

@@ -65,6 +65,17 @@ ParseVariant choose_parse_variant(const ParseArgs& a);
 // order, so the map is a bijection on [0, nb) for every grid size.
 __host__ __device__ __forceinline__ uint64_t tile_of(uint32_t b, uint32_t nb, uint32_t order) {
     if (!order) return b;
+    if (order & 0x80000000u) {  // CU-affine runs (measurement order "cuR", round 6): XCD-local runs of
+        // 32 R tiles in which the XCD's c-th workgroup of a dispatch round (CU c of 32 at launch)
+        // takes R consecutive tiles: tile c R + j for the run's (32 j + c)-th workgroup
+        const uint32_t R = order & 0x7FFFFFFFu;
+        if (R == 0 || R > (nb >> 8)) return b;  // no whole run of 8 x 32 R
+        const uint32_t K = 32u * R;
+        const uint32_t whole = nb / (8u * K) * (8u * K);
+        if (b >= whole) return b;
+        const uint32_t i = b >> 3, x = b & 7u, l = i % K;
+        return ((uint64_t)(i / K) * 8u + x) * K + (uint64_t)(l % 32u) * R + l / 32u;
+    }
     if (order == 1u) {
         const uint32_t q = nb >> 3;
         return b >= (q << 3) ? b : (uint64_t)(b & 7u) * q + (b >> 3);

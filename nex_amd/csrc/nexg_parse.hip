@@ -24,11 +24,12 @@ namespace nexg {
 // tools and tests/test_gpu_tile_order.py load; the product library has none):
 // linear = 0, xcd = 1 (contiguous eighths), xcdK = XCD-local runs of K tiles;
 // -1 when unset or unrecognised.
-static int order_from_env(const char* name) {
+static int64_t order_from_env(const char* name) {
 #ifdef NEXG_AB_KNOBS
     const char* e = getenv(name);
     if (!e) return -1;
     if (strncmp(e, "xcd", 3) == 0 && e[3]) return atoi(e + 3);
+    if (strncmp(e, "cu", 2) == 0 && e[2]) return (int64_t)(0x80000000u | (uint32_t)atoi(e + 2));  // CU-affine runs
     return strcmp(e, "xcd") == 0 ? 1 : (strcmp(e, "linear") == 0 ? 0 : -1);
 #else
     (void)name;
@@ -36,15 +37,19 @@ static int order_from_env(const char* name) {
 #endif
 }
 
-// Tile order of the parse kernels; NEXG_TILE_ORDER overrides. Fixed-stride
-// tiles (16 KiB at 64 B) take XCD-local runs of 16 tiles at every size
-// (profiles/r04/tile_order/: 0.921-0.924 of 8 TB/s at 1 and 3.25 GiB, grid
+// Tile order of the parse kernels; NEXG_TILE_ORDER overrides (knobs build).
+// Fixed-stride tiles (16 KiB at 64 B) take XCD-local runs of 16 tiles at every
+// size (profiles/r04/tile_order/: 0.921-0.924 of 8 TB/s at 1 and 3.25 GiB, grid
 // order 0.86-0.88, contiguous eighths 0.887-0.894, runs of 4 0.82-0.83). The
-// span kernel (packed batches, ~90 KB per IMIX tile) keeps grid order.
+// span kernel's 256-frame groups (~90 KB of IMIX each) take XCD-local runs of
+// 64 groups (~5.8 MB per run): in one process (profiles/r06/order/) IMIX
+// 0.853 -> 0.870 of 8 TB/s, the App. C mix 0.782 -> 0.790, real traffic
+// 0.784 -> 0.799 against grid order; runs of 16 / 32 / 128 gained less on one
+// of them, runs of 2 and 8 nothing (round 5)
 uint32_t tile_order_for(const ParseArgs& a) {
-    static const int forced = order_from_env("NEXG_TILE_ORDER");
+    static const int64_t forced = order_from_env("NEXG_TILE_ORDER");
     if (forced >= 0) return (uint32_t)forced;
-    return a.offsets ? 0u : 16u;
+    return a.offsets ? 64u : 16u;
 }
 
 // Tile order of the udp_ping builder (k_build_udp4) and the write-only stream
@@ -53,7 +58,7 @@ uint32_t tile_order_for(const ParseArgs& a) {
 // against 0.697-0.701 in grid order, full tuples 0.680 against 0.663; runs of
 // 16-64 tiles fall between.
 uint32_t build_tile_order() {
-    static const int forced = order_from_env("NEXG_BUILD_ORDER");
+    static const int64_t forced = order_from_env("NEXG_BUILD_ORDER");
     return forced >= 0 ? (uint32_t)forced : 1u;
 }
 
@@ -62,7 +67,7 @@ uint32_t build_tile_order() {
 // eighths made tcp SYN 0.199 -> 0.230-0.240 ms and tcp_ping 0.247 -> 0.30 at
 // 16M frames, icmp4 echo 0.133 -> 0.129 (profiles/r04/builders/order_ab.log).
 uint32_t l4_build_tile_order() {
-    static const int forced = order_from_env("NEXG_L4_ORDER");
+    static const int64_t forced = order_from_env("NEXG_L4_ORDER");
     return forced >= 0 ? (uint32_t)forced : 0u;
 }
 

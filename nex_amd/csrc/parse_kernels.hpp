@@ -20,7 +20,9 @@ constexpr uint32_t kTile = 256;
 #ifndef NEXG_DESC_MODE
 #define NEXG_DESC_MODE 2
 #endif
-constexpr uint32_t kApron = 96;  // k_parse_span: bytes of the previous sub-tile kept in front
+// k_parse_span: bytes of the previous sub-tile kept in front (and of pad
+// behind): at least the slot, so a head window that starts there is whole
+constexpr uint32_t kApron = NEXG_SPAN_SLOT > 96 ? NEXG_SPAN_SLOT : 96;
 
 // Frame read entirely from HBM (checksum utility path).
 struct GlobalFrame {
@@ -745,9 +747,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const uint32_t sh = (uint32_t)((base + off) & 3u);
     uint32_t qa = 0, qb = 0, run = 0;
     uint32_t qend = len;  // frame-relative position of the second prefix value
-    uint32_t u[21];
+    constexpr uint32_t NW = SpanFrame::kSlot / 4u + 1u;  // head window dwords (one of alignment slack)
+    uint32_t u[NW];
 #pragma unroll
-    for (int j = 0; j < 21; j++) u[j] = 0;
+    for (int j = 0; j < (int)NW; j++) u[j] = 0;
 
     uint32_t buf = 0;
     // one sub-tile: stage v (this sub-tile's chunks) into LDS, refill v with the
@@ -801,9 +804,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // in the first sub-tile that holds all of it (apron included: dh >= -80),
         // or in the last one (bytes past the span end are masked by len)
         const int dh = (int)((hr & ~3u) - S);
-        if (have && dh >= -(int)kLaneWin && (dh <= (int)(SUB - kLaneWin - 4u) || (last && dh < (int)SUB))) {
+        constexpr int kWin = (int)SpanFrame::kSlot;
+        if (have && dh >= -kWin && (dh <= (int)SUB - kWin - 4 || (last && dh < (int)SUB))) {
 #pragma unroll
-            for (int j = 0; j < 21; j++) u[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4 * j);
+            for (int j = 0; j < (int)NW; j++) u[j] = *reinterpret_cast<const uint32_t*>(sb + dh + 4 * j);
             // A padded frame's L4 range ends at the IP end, not the frame end:
             // take the second prefix value there instead (at or past the window
             // end, so in this sub-tile or a later one), so SpanFrame sums that
@@ -849,13 +853,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             if (OUT == NEXG_OUT_RECORD) stage_record(slots + SpanFrame::kSlot * t, r);
         } else {  // declined: the window goes to this lane's slot for pass (B), zero past len
             gen = true;
+            constexpr int NS = (int)SpanFrame::kSlot / 4;
+            uint32_t x[NS];
 #pragma unroll
-            for (int k = 0; k < 20; k++) w[k] = 4u * k < len ? (w[k] & range_mask(4u * k, 0, len)) : 0u;
-            key = span_bucket(w[3], w[5], a.opt_flags);
+            for (int k = 0; k < NS; k++) {
+                const uint32_t v = k < 20 ? w[k] : __builtin_amdgcn_alignbyte(u[k + 1], u[k], sh);
+                x[k] = 4u * k < len ? (v & range_mask(4u * k, 0, len)) : 0u;
+            }
+            key = span_bucket(x[3], x[5], a.opt_flags);
 #pragma unroll
-            for (int k = 0; k < 5; k++)
+            for (int k = 0; k < NS / 4; k++)
                 reinterpret_cast<uint4*>(slots + SpanFrame::kSlot * t)[k] =
-                    make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+                    make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
         }
     }
     // (B) the declined frames of the workgroup, bucketed by (family, L4
@@ -968,7 +977,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         copy_out_descs<SpanFrame::kSlot>(slots, a.out, f0, nf);
     } else if (OUT != NEXG_OUT_RECORD) store_out<OUT>(a, idx, have, r);
     if (OUT == NEXG_OUT_RECORD) {  // 256 x 64 B records through the slots (pitch 80 B)
-        static_assert(kStage >= kTile * SpanFrame::kSlot, "record staging needs 20 KiB");
+        static_assert(kStage >= kTile * SpanFrame::kSlot, "record staging needs kTile slots");
         __syncthreads();
         copy_out_records<SpanFrame::kSlot>(slots, a.out, f0, nf);
     }

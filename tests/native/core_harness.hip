@@ -86,8 +86,8 @@ extern "C" int harness_parse(const uint8_t* data, uint64_t data_bytes, const uin
                     // the span kernel stores canonical80_code for these: it must be the encoder's code
                     if (nexg::canonical80_code(r) != nexg::sparse_encode(r, flags, ip_offset)) return -2;
                 } else {
-                    alignas(16) uint8_t s64[80];
-                    memcpy(s64, w80, 80);
+                    alignas(16) uint8_t s64[nexg::SpanFrame::kSlot] = {0};  // the slot: head bytes, 0 past len
+                    memcpy(s64, g, len < sizeof(s64) ? len : sizeof(s64));
                     nexg::SpanFrame f{s64, g, te, par, tail};
                     nexg::parse_frame(f, par, (uint32_t)len, flags, ip_offset, r);
                     if (f.d.which()) {
@@ -206,8 +206,8 @@ extern "C" int harness_span_groups(const uint8_t* data, uint64_t data_bytes, con
             len[t] = (uint32_t)l;
             hr[t] = (uint32_t)(base + off - A0);
             const uint8_t* g = data + off;
-            uint32_t w[20] = {0};
-            memcpy(w, g, l < W ? l : W);
+            uint32_t w[S / 4] = {0};  // the slot's bytes (the first W: the fast path's window)
+            memcpy(w, g, l < S ? l : S);
             uint32_t wf[20];  // as the kernel: the window unmasked past len (the batch's next bytes)
             memset(wf, 0x5A, sizeof(wf));
             memcpy(wf, g, (uint64_t)W <= (uint64_t)(data + data_bytes - g) ? W : (size_t)(data + data_bytes - g));

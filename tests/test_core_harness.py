@@ -283,7 +283,7 @@ def test_tcp_option_walk_span_groups(oracle):
             assert q13.sum() > 20
 
 
-@pytest.mark.parametrize("order", [0, 1, 2, 3, 8, 16, 64, 1 << 20, 0xFFFFFFFF])
+@pytest.mark.parametrize("order", [0, 1, 2, 3, 8, 16, 64, 1 << 20, 0xFFFFFFFF, 0x80000001, 0x80000004, 0x80000000])
 def test_tile_map_is_a_permutation(order):
     """tile_of (nexg_internal.hpp), the workgroup -> tile map every tile
     kernel uses: a permutation of [0, nb) for every grid size, ragged tails
@@ -292,6 +292,11 @@ def test_tile_map_is_a_permutation(order):
     for nb in list(range(0, 300)) + [1023, 1024, 1025, 4096 + 127, 65536, 212993]:
         m = harness.tile_map(nb, order)
         assert np.array_equal(np.sort(m), np.arange(nb, dtype=np.uint64)), (nb, order)
+    if order == 0x80000004:  # CU-affine runs of 32 x 4: the c-th workgroup of XCD x's round takes 4 tiles
+        m = harness.tile_map(65536, order).reshape(-1, 8)
+        for x in range(8):
+            for c in range(32):
+                assert np.array_equal(m[c::32, x][:4], x * 128 + c * 4 + np.arange(4))
     if order == 16:
         m = harness.tile_map(65536, 16).reshape(-1, 8)  # row i: the i-th workgroup of each XCD
         for x in range(8):

@@ -197,8 +197,9 @@ def test_offsets32_imix_over_4gib(engine):
     assert b32.total_bytes == b64.total_bytes
     for kind in (abi.OUT_GROUPED, abi.OUT_DESC):
         n = engine.out_bytes(kind, b64.count)
-        want = torch.empty(n, dtype=torch.uint8, device="cuda")
-        got = torch.empty(n, dtype=torch.uint8, device="cuda")
+        # (zeroed: the grouped layout writes exception slots only where frames have one)
+        want = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        got = torch.zeros(n, dtype=torch.uint8, device="cuda")
         engine.parse(b64, out_kind=kind, out=want)
         engine.parse(b32, out_kind=kind, out=got)
         torch.cuda.synchronize()
