@@ -654,6 +654,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 #ifndef NEXG_SPAN_NT
 #define NEXG_SPAN_NT true  // sub-tile fetch cache policy (A/B builds override)
 #endif
+#ifndef NEXG_SPAN_PF
+#define NEXG_SPAN_PF 0  // offset-table prefetch distance in same-XCD dispatches (A/B builds)
+#endif
 #ifndef NEXG_SPAN_DEPTH
 #define NEXG_SPAN_DEPTH 1  // sub-tiles in flight beside the one being scanned (A/B builds: 2)
 #endif
@@ -688,6 +691,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // profiles/r05/grouped_as_sparse/)
     if (OUT == NEXG_OUT_SPARSE && a.grouped_heads && lane == 0 && have) a.grouped_heads[idx >> 6] = 0;
     if (OUT == NEXG_OUT_GROUPED && lane == 0 && have) reinterpret_cast<uint8_t*>(a.out)[idx >> 6] = 0;
+#if NEXG_SPAN_PF
+    // warm this XCD's L2 with the offset table of the group its workgroup
+    // NEXG_SPAN_PF dispatches later will take (same XCD: block + 8 k): one
+    // u64 per 64-B line of that group's 2 KiB, read now, used after the loop
+    uint64_t pfv = 0;
+    const uint64_t pfb = (uint64_t)blockIdx.x + 8ull * NEXG_SPAN_PF;
+    if (a.offsets && !a.lengths && !(a.hints & NEXG_FRAMES_OFFSETS32) && pfb < gridDim.x && t < 33u) {
+        const uint64_t pg = tile_of((uint32_t)pfb, gridDim.x, a.tile_order) * kTile + 8u * t;
+        if (pg <= a.count) pfv = NEXG_GLOBAL(uint64_t, a.offsets)[pg];
+    }
+#endif
     const bool ok = have && frame_extent(a, idx, off, len);
     if (t == 0) s_span[0] = off;
     if (t == nf - 1) s_span[1] = off + len;
@@ -833,6 +847,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     for (uint32_t S = 0; S < span; S += SUB, buf = NB == 2 ? buf ^ 1u : 0u) sub_tile(S, cur);
 #endif
     if (NB == 2) __syncthreads();  // the stage buffers become per-lane slots below
+#if NEXG_SPAN_PF
+    if (pfv == ~0ull) s_hist[0] = 1u;  // consumes the prefetch (long returned); s_hist is rewritten below
+#endif
     NEXG_SPAN_STAMP(2);
     uint8_t* const slots = &s_bytes[0][0];  // 80 B per lane from here on
     // (A) every lane: the canonical fast path on its head window
