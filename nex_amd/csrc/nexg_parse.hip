@@ -303,7 +303,9 @@ hipError_t launch_decode_options(const ParseArgs& a, const nexg_record* recs, ne
 // calibration stream (include/nexg.h nexg_probe_stream): the parse kernels'
 // load shape with either the 8-B-per-64-B descriptor store stream or none
 // (tiles in the parse kernels' fixed-stride tile order)
-template <bool W8>
+// OCC6: the out_per_64 = 9 instance (its own symbol, so a kernel trace tells
+// the occupancy-capped run from the 8-per-CU one)
+template <bool W8, bool OCC6 = false>
 __global__ __launch_bounds__(256) void k_probe_stream(const uint8_t* data, void* out, uint32_t order) {
     __shared__ uint32_t s_x[4];
     extern __shared__ uint32_t s_occ[];  // dynamic LDS: caps workgroups per CU only (out_per_64 = 9)
@@ -355,8 +357,8 @@ hipError_t launch_probe_stream(const uint8_t* data, uint64_t tiles, uint32_t mod
                            static_cast<uint8_t*>(out), wo);
     else if (mode == 8) hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out, ro);
     else if (mode == 9)  // 6 workgroups per CU: the fixed-stride parse kernel's occupancy
-        hipLaunchKernelGGL(k_probe_stream<true>, dim3((uint32_t)tiles), dim3(kTile), 160u * 1024u / 6u - 1024u, s, data,
-                           out, ro);
+        hipLaunchKernelGGL((k_probe_stream<true, true>), dim3((uint32_t)tiles), dim3(kTile), 160u * 1024u / 6u - 1024u, s,
+                           data, out, ro);
     else hipLaunchKernelGGL(k_probe_stream<false>, dim3((uint32_t)tiles), dim3(kTile), 0, s, data, out, ro);
     return hipGetLastError();
 }

@@ -33,10 +33,11 @@ def expected(line):
     sc = rl.get("stream_ceilings") or {}
     nb = rl["algorithmic_bytes_per_launch"]
     if "read_only_gbs" in sc:
-        ex.append(("stream.read_only", "k_probe_stream", line["steps"], nb // 16384 * 16384, None))
-        ex.append(("stream.read64_write8", "k_probe_stream", line["steps"], nb // 16384 * 16384, None))
+        ex.append(("stream.read_only", "k_probe_stream<false, false>", line["steps"], nb // 16384 * 16384, None))
+        ex.append(("stream.read64_write8", "k_probe_stream<true, false>", line["steps"], nb // 16384 * 16384, None))
         if "read64_write8_6cu_gbs" in sc:
-            ex.append(("stream.read64_write8_6cu", "k_probe_stream", line["steps"], nb // 16384 * 16384, None))
+            ex.append(("stream.read64_write8_6cu", "k_probe_stream<true, true>", line["steps"], nb // 16384 * 16384,
+                       None))
         for k in ("desc_output", "flags_output", "verdict_output", "sparse_output", "grouped_output"):
             if k in sc:
                 ex.append((f"stream.{k}", "k_parse", line["steps"], nb, sc[k]["kernel_ms"]))
