@@ -1177,7 +1177,7 @@ hipError_t launch_probe(ProbeArgs& a, const uint8_t* tmpl, uint32_t dw, hipStrea
     const uint32_t tile_lds = kch * 16u * kT + 2u * kProbeMaxP + 32u, wgs = probe_wgs_per_cu();
     const uint32_t cap = wgs ? 160u * 1024u / wgs - 1024u : 0u;
     const uint32_t lds = tile_lds > cap ? tile_lds : cap < 65536u ? cap : 65536u;  // a workgroup's LDS limit
-    a.tile_order = build_tile_order();
+    a.tile_order = probe_tile_order();
     const dim3 g((uint32_t)ntiles), b(kT);
 #define NEXG_PROBE_LAUNCH(DW, K)                                                     \
     do {                                                                             \

@@ -49,6 +49,7 @@ inline bool parse_needs_tail(ParseVariant v, int out_kind) {
 uint32_t tile_order_for(const ParseArgs& a);
 uint32_t build_tile_order();
 uint32_t l4_build_tile_order();
+uint32_t probe_tile_order();
 uint32_t build_lds_pad();  // dynamic LDS of the udp_ping builds (workgroups per CU)
 ParseVariant choose_parse_variant(const ParseArgs& a);
 

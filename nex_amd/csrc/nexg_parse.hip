@@ -62,6 +62,18 @@ uint32_t build_tile_order() {
     return forced >= 0 ? (uint32_t)forced : 1u;
 }
 
+// Tile order of the probe-batch template kernel (k_build_probe: tcp_ping and
+// udp_ping's IPv6 branch); NEXG_PROBE_ORDER overrides. XCD-local runs of 64
+// tiles: 16M frames in one process (profiles/r06/order/build_order2.log)
+// tcp_ping 0.740 -> 0.807 of 8 TB/s written, udp6 0.666 -> 0.684 against
+// contiguous eighths; runs of 16 lost (0.711). udp_ping's IPv4 probe batch
+// (0.889 against 0.846 in runs of 64) and icmp_ping's k_build_lane (0.675
+// against 0.639) keep contiguous eighths.
+uint32_t probe_tile_order() {
+    static const int64_t forced = order_from_env("NEXG_PROBE_ORDER");
+    return forced >= 0 ? (uint32_t)forced : 64u;
+}
+
 // Tile order of the builders with several per-frame parameter arrays
 // (k_build_udp6, k_build_l4); NEXG_L4_ORDER overrides. Grid order: contiguous
 // eighths made tcp SYN 0.199 -> 0.230-0.240 ms and tcp_ping 0.247 -> 0.30 at

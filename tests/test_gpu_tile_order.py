@@ -71,12 +71,15 @@ put("build.tcp4_opts", e.build_tcp(4, a4s, a4d, sp, dp, seq, None, flags=0x02, w
 put("build.tcp6", e.build_tcp(6, a6s, a6d, sp, dp, seq, None, flags=0x12, window=1024))
 put("build.icmp4", e.build_icmp_echo(4, a4s, a4d, sp, dp))
 put("build.icmp6", e.build_icmp_echo(6, a6s, a6d, sp, dp))
+from nex_amd import probes  # the probe batches: k_build_probe (tcp_ping, udp6) and k_build_lane (icmp_ping)
+for shape in ("tcp_ping", "udp6", "icmp_ping"):
+    put("probe." + shape, probes.build(e, shape, a6d if probes.dst_bytes(shape) == 16 else a4d))
 print(json.dumps(h))
 '''
 
 
 def run_child(order):
-    env = dict(os.environ, NEXG_TILE_ORDER=order, NEXG_BUILD_ORDER=order, NEXG_L4_ORDER=order)
+    env = dict(os.environ, NEXG_TILE_ORDER=order, NEXG_BUILD_ORDER=order, NEXG_L4_ORDER=order, NEXG_PROBE_ORDER=order)
     r = subprocess.run([sys.executable, "-c", CHILD, str(N_FIXED), str(N_IMIX), KNOBS_LIB], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -85,7 +88,7 @@ def run_child(order):
 
 def test_every_tile_order_gives_the_same_bytes():
     want = run_child("linear")
-    for order in ("xcd", "xcd3", "xcd8", "xcd16", "xcd64"):
+    for order in ("xcd", "xcd3", "xcd8", "xcd16", "xcd64", "cu1", "cu4"):
         got = run_child(order)
         diff = sorted(k for k in want if got[k] != want[k])
         assert not diff, (order, diff)
