@@ -55,12 +55,18 @@ def main():
             d = rb(n, probes.dst_bytes(name))
             shapes[f"probe_{name}_{probes.frame_len(name)}B"] = (
                 probes.frame_len(name), lambda out, name=name, d=d: probes.build(eng, name, d, out=out))
+        # udp_ping's IPv4 probe batch (bench.py's ser object): a BE u32 destination value per frame
+        d4 = r32()
+        shapes["probe_udp_ping_42B"] = (42, lambda out: eng.build_udp4(
+            None, d4, def_src_ip=0xC0A80164, def_src_port=53443, def_dst_port=33435, src_mac=b"\x02\0\0\0\0\1",
+            dst_mac=b"\x02\0\0\0\0\2", ip_flags=2, out=out))
     res = {"frames": n, "lib": args.lib or "default", "lds_pad": os.environ.get("NEXG_BUILD_LDS_PAD", "default"),
            "probe_wgs": os.environ.get("NEXG_PROBE_WGS", "default"), "probe_waves": os.environ.get("NEXG_PROBE_WAVES", "default"),
            "order": os.environ.get("NEXG_L4_ORDER", "default"),
            "build_order": os.environ.get("NEXG_BUILD_ORDER", "default"),
            "probe_icmp": os.environ.get("NEXG_PROBE_ICMP", "default"),
            "probe_lane_tcp": os.environ.get("NEXG_PROBE_LANE_TCP", "default"),
+           "probe_udp4": os.environ.get("NEXG_PROBE_UDP4", "default"),
            "lane_wgs": os.environ.get("NEXG_LANE_WGS", "default")}
     for name, (flen, fn) in shapes.items():
         out = torch.empty(n * flen, dtype=torch.uint8, device="cuda")

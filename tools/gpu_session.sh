@@ -114,6 +114,9 @@ for s in ${STEPS:-tests}; do
     buildorder2) step build_order2 1100 bash -c 'for o in xcd xcd16 xcd64 cu1; do echo "order $o"; NEXG_BUILD_ORDER=$o python -u tools/bench_ser_ab.py --libs nex_amd/libnexg.so,nex_amd/libnexg_knobs.so --shape probe --rounds 3 || exit 1; NEXG_BUILD_ORDER=$o NEXG_L4_ORDER=$o python -u tools/bench_builders.py --probe || exit 1; done; python -u tools/bench_builders.py --probe --lib nex_amd/libnexg.so' ;;
     shortab) step short_ab 1100 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_noshort.so --workloads imix,mix,real --out grouped --check --rounds 4
              step short_kinds 900 python -u tools/bench_malformed.py --libs nex_amd/libnexg.so,abx/libnexg_noshort.so --kinds clean,ver_ihl,l4_length,ipv6_hbh --out grouped ;;
+    w6ab) step w6_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_s20w6.so,abx/libnexg_s16w6.so --workloads imix,mix,real --out grouped --check --rounds 3 ;;
+    udptests) step pytest_udp 600 python -u -m pytest tests/test_gpu_probe_batches.py tests/test_gpu_parity.py tests/test_gpu_fixup.py tests/test_gpu_tile_order.py -q -x --timeout 300 --timeout-method thread ;;
+    udpab) step udp_ab 900 bash -c 'for r in 1 2; do for cfg in "" "NEXG_LANE_WGS=4" "NEXG_LANE_WGS=5" "NEXG_LANE_WGS=2"; do env $cfg python tools/bench_builders.py --probe || exit 1; done; done' ;;
     # the driver's own command under the kernel trace: a row for every object of its line (tools/line_trace.py)
     lineprof) step lineprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lineprof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed --no-real --no-large --no-ser
