@@ -29,7 +29,8 @@ def main():
     ap.add_argument("--libs", default="")
     ap.add_argument("--share", type=float, default=0.5, help="share of frames mutated (kinds other than clean)")
     ap.add_argument("--unwrap-vlan", action="store_true", help="parse with NEXG_PARSE_VLAN (ParseOption.unwrap_vlan)")
-    ap.add_argument("--out", default="sparse", choices=["sparse", "grouped"], help="output kind")
+    ap.add_argument("--out", default="sparse", choices=["sparse", "grouped", "verdict", "flags", "desc"],
+                    help="output kind (verdict / flags / desc: fixed-size, no exception slots)")
     args = ap.parse_args()
     import torch
     from nex_amd import _lib, abi, workloads
@@ -42,7 +43,8 @@ def main():
         engines.append(Engine(0))
     eng = engines[0]
     stream = torch.cuda.current_stream()
-    ok = abi.OUT_GROUPED if args.out == "grouped" else abi.OUT_SPARSE
+    ok = {"grouped": abi.OUT_GROUPED, "sparse": abi.OUT_SPARSE, "verdict": abi.OUT_VERDICT, "flags": abi.OUT_FLAGS,
+          "desc": abi.OUT_DESC}[args.out]
     kinds = args.kinds.split(",") if args.kinds else ["clean"] + list(workloads.MUTATIONS) + ["all"]
     for k in kinds:
         share = 0.0 if k == "clean" else args.share
@@ -81,8 +83,11 @@ def main():
                         same.append(bool(torch.equal(out, ref)))
             times.append(row)
         s = min(t[0] for t in times)
-        codes = out[: b.count].cpu().numpy() if ok == abi.OUT_SPARSE else abi.grouped_codes(out.cpu().numpy(), b.count)
-        exc = float((codes == 0).mean())
+        if ok in (abi.OUT_SPARSE, abi.OUT_GROUPED):
+            codes = out[: b.count].cpu().numpy() if ok == abi.OUT_SPARSE else abi.grouped_codes(out.cpu().numpy(), b.count)
+            exc = float((codes == 0).mean())
+        else:
+            exc = float("nan")
         line = {"kind": k, "frames": b.count, "bytes": b.total_bytes, "kernel_ms": round(s * 1e3, 4),
                 "mpkt_s": round(b.count / s / 1e6, 1), "frac": round(b.total_bytes / s / 8e12, 4),
                 "exception_share": round(exc, 4), "mutated": counts.get(k, None)}

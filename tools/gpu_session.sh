@@ -117,6 +117,15 @@ for s in ${STEPS:-tests}; do
     w6ab) step w6_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_s20w6.so,abx/libnexg_s16w6.so --workloads imix,mix,real --out grouped --check --rounds 3 ;;
     udptests) step pytest_udp 600 python -u -m pytest tests/test_gpu_probe_batches.py tests/test_gpu_parity.py tests/test_gpu_fixup.py tests/test_gpu_tile_order.py -q -x --timeout 300 --timeout-method thread ;;
     udpab) step udp_ab 900 bash -c 'for r in 1 2; do for cfg in "" "NEXG_LANE_WGS=4" "NEXG_LANE_WGS=5" "NEXG_LANE_WGS=2"; do env $cfg python tools/bench_builders.py --probe || exit 1; done; done' ;;
+    realkinds) step real_kinds 900 python -u tools/bench_malformed.py --libs nex_amd/libnexg.so --kinds clean,tcp_ts,tcp_sack,tcp_mss --share 0.7 --out grouped ;;
+    pmc32) mkdir -p gpurun_out/pmc32 && export TMPDIR=/tmp && for c in FETCH_SIZE WRITE_SIZE; do for t in 64 32; do
+        step pmc32_${t}_$c 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc32/t${t}_$c -o run -- python3 tools/bench_parse_ab.py --libs nex_amd/libnexg.so --tables $t --workloads imix --out grouped --rounds 1 --steps 5 --warmup 1 || exit 1; done; done ;;
+    realout) for o in grouped verdict desc; do step real_out_$o 600 python -u tools/bench_malformed.py --kinds clean,tcp_ts,clean,tcp_ts --share 0.7 --out $o; done ;;
+    padab) step pad_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_pad1.so,abx/libnexg_pad2.so --workloads real,mix,imix --out grouped --rounds 3 &&
+        step pad_kinds 900 python -u tools/bench_malformed.py --libs nex_amd/libnexg.so,abx/libnexg_pad1.so,abx/libnexg_pad2.so --kinds clean,tcp_ts,truncate,pad,ver_ihl --out grouped ;;
+    excab) step exc_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_skip.so,abx/libnexg_e9.so --workloads real,mix,imix --out grouped --rounds 3 && step exc_kinds 900 python -u tools/bench_malformed.py --libs nex_amd/libnexg.so,abx/libnexg_skip.so,abx/libnexg_e9.so --kinds clean,tcp_ts --share 0.7 --out grouped ;;
+    codeab) step code_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_p7.so,abx/libnexg_p1.so,abx/libnexg_p2.so,abx/libnexg_p3.so,abx/libnexg_p4.so,abx/libnexg_p5.so,abx/libnexg_p6.so --workloads imix,real --out grouped --rounds 3 ;;
+    tpwab) step tpw_ab 900 python -u tools/bench_parse_ab.py --libs abx/libnexg_head.so,abx/libnexg_t1.so,abx/libnexg_t2.so,abx/libnexg_t4.so --workloads imix,real,mix --out grouped --check --rounds 3 ;;
     # the driver's own command under the kernel trace: a row for every object of its line (tools/line_trace.py)
     lineprof) step lineprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lineprof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof) step prof_udp64 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_udp64 -o run -- python3 bench.py --steps 60 --warmup 25 --no-cpu-baseline --no-imix --no-malformed --no-real --no-large --no-ser
