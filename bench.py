@@ -477,7 +477,16 @@ def parse_object(eng, args, batch, out_kind, stream, device, rank, world, worklo
     return r
 
 
-IMIX_DESC = "(64/576/1500 at 7:4:1, {IPv4,IPv6}x{TCP,UDP,ICMP}), packed with an offset table; "
+IMIX_DESC = ("(64/576/1500 at 7:4:1, {IPv4,IPv6}x{TCP,UDP,ICMP}), packed with a u32 offset table "
+             "(NEXG_FRAMES_OFFSETS32 + a u64 base per 256 frames: the batch is over 4 GiB); ")
+
+
+def imix_batch(eng, F, first):
+    """configs[2]'s batch: F IMIX frames packed back to back, described by
+    the u32 offset table (half the u64 table's bytes: HBM traffic 1.023x the
+    frame bytes against 1.033x, profiles/r06/pmc/imix_offsets32_pmc.json)."""
+    from nex_amd import abi
+    return eng.gen_batch(abi.WL_IMIX, F, first_index=first).with_offsets32()
 
 
 def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world):
@@ -487,8 +496,7 @@ def imix_line(eng, args, F, first, out_kind, width, stream, device, rank, world)
     back-to-back load) run 5-25 % slow before the chip settles
     (profiles/r01_staging/imix_ramp.txt, profiles/r03_final/imix_ramp.txt),
     so the IMIX objects warm up for IMIX_WARMUP untimed launches."""
-    from nex_amd import abi
-    batch = eng.gen_batch(abi.WL_IMIX, F, first_index=first)
+    batch = imix_batch(eng, F, first)
     return parse_object(eng, args, batch, out_kind, stream, device, rank, world, f"configs[2] IMIX {args.out}",
                         "imix", max(IMIX_WARMUP, args.warmup), max(1, args.steps // 2), cpu_label="imix",
                         desc=f"configs[2]: {F} IMIX frames per GPU " + IMIX_DESC + OUT_NOTE[args.out])
@@ -620,6 +628,8 @@ def main():
         elif args.workload == "real_traffic":  # the real_traffic object's batch (PMC / rocprof)
             batch, rdesc = real_traffic_batch(eng, F, first)
             F = batch.count
+        elif args.workload == "imix" and not args.e2e:
+            batch = imix_batch(eng, F, first)
         else:
             batch = eng.gen_batch(wl, F, first_index=first, record_gap=16 if args.workload == "imix_pcap" else 0)
         torch.cuda.synchronize(device)
