@@ -125,7 +125,7 @@ for s in ${STEPS:-tests}; do
         step pad_kinds 900 python -u tools/bench_malformed.py --libs nex_amd/libnexg.so,abx/libnexg_pad1.so,abx/libnexg_pad2.so --kinds clean,tcp_ts,truncate,pad,ver_ihl --out grouped ;;
     excab) step exc_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_skip.so,abx/libnexg_e9.so --workloads real,mix,imix --out grouped --rounds 3 && step exc_kinds 900 python -u tools/bench_malformed.py --libs nex_amd/libnexg.so,abx/libnexg_skip.so,abx/libnexg_e9.so --kinds clean,tcp_ts --share 0.7 --out grouped ;;
     codeab) step code_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_p7.so,abx/libnexg_p1.so,abx/libnexg_p2.so,abx/libnexg_p3.so,abx/libnexg_p4.so,abx/libnexg_p5.so,abx/libnexg_p6.so --workloads imix,real --out grouped --rounds 3 ;;
-    tpwab) step tpw_ab 900 python -u tools/bench_parse_ab.py --libs abx/libnexg_head.so,abx/libnexg_t1.so,abx/libnexg_t2.so,abx/libnexg_t4.so --workloads imix,real,mix --out grouped --check --rounds 3 ;;
+    tpwab) step tpw_ab 900 python -u tools/bench_parse_ab.py --libs abx/libnexg_t1.so,abx/libnexg_t2.so,abx/libnexg_t1s.so,abx/libnexg_t2s.so --workloads imix,real --out grouped --rounds 3 ;;
     codeat) step code_at 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_at1.so,abx/libnexg_at2.so,abx/libnexg_at3.so --workloads imix,real --out grouped --rounds 3 ;;
     # the driver's own command under the kernel trace: a row for every object of its line (tools/line_trace.py)
     lineprof) step lineprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lineprof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
