@@ -298,8 +298,12 @@ static inline int nexg_sparse_decode(uint8_t code, uint32_t len, uint32_t parse_
  * verdict bits is "uniform": heads[g] = that code with bits 4..5 clear, and
  * its verdicts are two 64-bit masks (bit i % 64 = NEXG_SPARSE_IP_OK /
  * NEXG_SPARSE_L4_OK of frame i); nothing else of the group is written
- * (17 B per 64 frames on single-shape traffic). Any other group has heads[g]
- * = 0 and stores its 1-B codes and exceptions as NEXG_OUT_SPARSE does. Every
+ * (17 B per 64 frames on single-shape traffic). Any other group is mixed and
+ * stores its 1-B codes and exceptions as NEXG_OUT_SPARSE does, with heads[g]
+ * = 0; or heads[g] = NEXG_GROUPED_TILE_RUN (the packed-batch kernel's form):
+ * then the exceptions of its 256-frame tile T = i / 256 sit in one run, frame
+ * i's at exc[256 T + k], k = the code-0 frames of [256 T, i) (one write burst
+ * per tile instead of one per group: DESIGN.md §6 round 6). Every
  * area is written densely (a head byte per group, 16 B of masks per group):
  * interleaving them with the codes costs partial-line writes.
  * `out` (16-B aligned) holds
@@ -308,27 +312,40 @@ static inline int nexg_sparse_decode(uint8_t code, uint32_t len, uint32_t parse_
  *   codes : uint8_t[count]                 at out + NEXG_GROUPED_CODE_OFFSET(count)
  *   exc   : nexg_desc[count] (capacity)    at out + NEXG_GROUPED_EXC_OFFSET(count)
  * nexg_grouped_code gives frame i's NEXG_OUT_SPARSE code (then
- * nexg_sparse_decode, exceptions at exc[64 * g + k]); nexg_grouped_expand
- * restores nexg_desc[count] on the device. */
+ * nexg_sparse_decode), nexg_grouped_exc_slot the exc index of a code-0
+ * frame; nexg_grouped_expand restores nexg_desc[count] on the device. */
 #define NEXG_OUT_GROUPED 7
 #define NEXG_GROUPED_GROUPS(count) ((((uint64_t)(count)) + 63u) >> 6)
 #define NEXG_GROUPED_MASK_OFFSET(count) ((NEXG_GROUPED_GROUPS(count) + 15u) & ~(uint64_t)15u)
 #define NEXG_GROUPED_CODE_OFFSET(count) (NEXG_GROUPED_MASK_OFFSET(count) + 16u * NEXG_GROUPED_GROUPS(count))
 #define NEXG_GROUPED_EXC_OFFSET(count) ((NEXG_GROUPED_CODE_OFFSET(count) + (uint64_t)(count) + 15u) & ~(uint64_t)15u)
 #define NEXG_GROUPED_BYTES(count) (NEXG_GROUPED_EXC_OFFSET(count) + 8u * (uint64_t)(count))
+/* head of a mixed group whose exceptions are kept per 256-frame tile (its
+ * shape bits are 0, so it is never a uniform group's head) */
+#define NEXG_GROUPED_TILE_RUN 0x80u
 
 /* frame i's NEXG_OUT_SPARSE code from a NEXG_OUT_GROUPED output (host side) */
 static inline uint8_t nexg_grouped_code(const void* out, uint64_t count, uint64_t i) {
     const uint8_t* o = (const uint8_t*)out;
     const uint64_t g = i >> 6;
     const uint8_t head = o[g];
-    if (!head) return o[NEXG_GROUPED_CODE_OFFSET(count) + i];
+    if (!head || head == NEXG_GROUPED_TILE_RUN) return o[NEXG_GROUPED_CODE_OFFSET(count) + i];
     const uint8_t* m = o + NEXG_GROUPED_MASK_OFFSET(count) + 16u * g;
     /* the masks are little-endian words: bit b of a 64-bit mask is bit b % 8
      * of its byte b / 8 */
     const uint32_t b = (uint32_t)(i & 63u), byte = b >> 3, sh = b & 7u;
     const uint32_t ip = (m[byte] >> sh) & 1u, l4 = (m[8u + byte] >> sh) & 1u;
     return (uint8_t)(head | (ip ? NEXG_SPARSE_IP_OK : 0u) | (l4 ? NEXG_SPARSE_L4_OK : 0u));
+}
+
+/* index in the exc area of frame i's descriptor when its code is 0 (host
+ * side): its group's run (heads[g] = 0) or its tile's (NEXG_GROUPED_TILE_RUN) */
+static inline uint64_t nexg_grouped_exc_slot(const void* out, uint64_t count, uint64_t i) {
+    const uint8_t* o = (const uint8_t*)out;
+    const uint64_t first = o[i >> 6] == NEXG_GROUPED_TILE_RUN ? (i & ~(uint64_t)255u) : (i & ~(uint64_t)63u);
+    uint64_t k = 0;
+    for (uint64_t j = first; j < i; j++) k += nexg_grouped_code(out, count, j) == 0u;
+    return first + k;
 }
 
 /* FrameSlice::try_from_buf (frame.rs:84-287) per frame, out_kind

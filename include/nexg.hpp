@@ -923,12 +923,18 @@ class Engine {  // one nexg context on one gfx950 device, one stream
         check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
         const nexg_desc* exc = reinterpret_cast<const nexg_desc*>(g.data() + NEXG_GROUPED_EXC_OFFSET(n));
         const uint32_t fl = option.flags(mode);
-        for (uint64_t g0 = 0; g0 < n; g0 += 64) {
-            uint32_t k = 0;  // the group's exceptions, in frame order
-            for (uint64_t i = g0; i < n && i < g0 + 64; i++)
-                if (!nexg_sparse_decode(nexg_grouped_code(g.data(), n, i), (uint32_t)frames[i].size(), fl,
-                                        (uint32_t)option.offset, &out[i]))
-                    out[i] = exc[g0 + k++];
+        uint64_t kg = 0, kt = 0;  // exceptions so far in the frame's group / tile
+        for (uint64_t i = 0; i < n; i++) {
+            if ((i & 63u) == 0) kg = 0;
+            if ((i & 255u) == 0) kt = 0;
+            if (!nexg_sparse_decode(nexg_grouped_code(g.data(), n, i), (uint32_t)frames[i].size(), fl,
+                                    (uint32_t)option.offset, &out[i])) {
+                // (nexg_grouped_exc_slot, without its rescan of the run)
+                const bool run = g[i >> 6] == NEXG_GROUPED_TILE_RUN;
+                out[i] = exc[run ? (i & ~(uint64_t)255u) + kt : (i & ~(uint64_t)63u) + kg];
+                kg++;
+                kt++;
+            }
         }
         return out;
     }

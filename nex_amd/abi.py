@@ -50,6 +50,7 @@ OUT_FLAGS = 4  # nexg_desc.flags only (include/nexg.h)
 OUT_VERDICT = 5  # lossless 2-B form of the flags word (include/nexg.h)
 OUT_SPARSE = 6  # 1-B shape codes + per-64-frame exception slots (include/nexg.h)
 OUT_GROUPED = 7  # SPARSE with uniform 64-frame groups as a head byte + 2 verdict masks
+GROUPED_TILE_RUN = 0x80  # NEXG_GROUPED_TILE_RUN: a mixed group whose exceptions run per 256-frame tile
 
 # NEXG_FRAMES_* hints (nexg_frames.hints)
 FRAMES_MONOTONE = 0x1
@@ -143,15 +144,18 @@ def grouped_codes(buf, count):
     ip = (m[g, 0] >> b) & np.uint64(1)
     l4 = (m[g, 1] >> b) & np.uint64(1)
     uni = head | np.where(ip != 0, SPARSE_IP_OK, 0) | np.where(l4 != 0, SPARSE_L4_OK, 0)
-    return np.where(head != 0, uni, buf[code:code + count].astype(np.int64))
+    mixed = (head == 0) | (head == GROUPED_TILE_RUN)
+    return np.where(mixed, buf[code:code + count].astype(np.int64), uni)
 
 
 def grouped_to_desc(buf, count, lengths, parse_flags=0, ip_offset=0):
     """nexg_desc[count] from a NEXG_OUT_GROUPED output (uint8 host array)."""
     buf = np.asarray(buf, np.uint8)
     _, _, exc, _ = grouped_offsets(count)
+    G = (count + 63) >> 6
+    run = buf[:G][np.arange(count) >> 6] == GROUPED_TILE_RUN
     return codes_to_desc(grouped_codes(buf, count), buf[exc:exc + 8 * count].view(DESC_DTYPE), count, lengths,
-                         parse_flags, ip_offset)
+                         parse_flags, ip_offset, tile_run=run)
 
 
 def sparse_to_desc(buf, count, lengths, parse_flags=0, ip_offset=0):
@@ -164,9 +168,11 @@ def sparse_to_desc(buf, count, lengths, parse_flags=0, ip_offset=0):
                          count, lengths, parse_flags, ip_offset)
 
 
-def codes_to_desc(codes, exc, count, lengths, parse_flags=0, ip_offset=0):
+def codes_to_desc(codes, exc, count, lengths, parse_flags=0, ip_offset=0, tile_run=None):
     """nexg_sparse_decode over every code; code-0 frames take the k-th
-    exception of their 64-frame group (exc = the exception slots)."""
+    exception of their 64-frame group (exc = the exception slots), or of
+    their 256-frame tile where `tile_run` (per frame) is set
+    (NEXG_GROUPED_TILE_RUN groups)."""
     lengths = np.asarray(lengths, np.int64)[:count]
     shape, tags = codes & 0xF, (codes >> SPARSE_TAG_SHIFT) & 3
     out = np.zeros(count, DESC_DTYPE)
@@ -183,10 +189,11 @@ def codes_to_desc(codes, exc, count, lengths, parse_flags=0, ip_offset=0):
     out["payload_off"] = np.where(pay & (lengths > h), h, 0).astype(np.uint16)
     ex = np.nonzero(shape == SHAPE_EXCEPTION)[0]
     if len(ex):
-        grp = ex // 64
-        first = np.searchsorted(ex, grp * 64)  # index in ex of the group's first exception
+        unit = np.full(len(ex), 64, np.int64) if tile_run is None else np.where(tile_run[ex], 256, 64)
+        start = ex // unit * unit  # the first frame of the exception's group or tile
+        first = np.searchsorted(ex, start)  # index in ex of that run's first exception
         rank = np.arange(len(ex)) - first
-        out[ex] = exc[grp * 64 + rank]
+        out[ex] = exc[start + rank]
     return out
 
 # FrameSlice presence bits (nexg_slice.flags)
@@ -385,7 +392,8 @@ FIXUP_DTYPE = np.dtype([("done", "u1"), ("proto", "u1"), ("ip_csum", "<u2"), ("l
 assert FIXUP_DTYPE.itemsize == 8
 
 #: static inline helpers of include/nexg.h (header-only, not exported)
-HEADER_INLINE = ("nexg_sparse_decode", "nexg_grouped_code", "nexg_offsets32_bases", "nexg_offsets32_bytes")
+HEADER_INLINE = ("nexg_sparse_decode", "nexg_grouped_code", "nexg_grouped_exc_slot", "nexg_offsets32_bases",
+                 "nexg_offsets32_bytes")
 
 #: every symbol include/nexg.h declares (tests check the .so exports them)
 EXPORTED_SYMBOLS = (

@@ -24,7 +24,8 @@ struct ParseArgs {
     uint32_t* tail = nullptr; // TwoPass tail-sum hand-off (count entries) for outputs
                               // narrower than 4 B per frame; null -> the output itself
     uint64_t* stamps = nullptr;  // k_parse_span<..., TIMING>: 8 clock stamps per workgroup
-    uint8_t* grouped_heads = nullptr;  // span kernel, NEXG_OUT_GROUPED run as SPARSE at the code offset: head bytes (all 0)
+    uint8_t* grouped_heads = nullptr;  // span kernel, NEXG_OUT_GROUPED run as SPARSE at the code offset: head bytes
+                                       // (all NEXG_GROUPED_TILE_RUN: exceptions in one run per 256-frame tile)
     const uint64_t* off_bases = nullptr;  // NEXG_FRAMES_OFFSETS32 over 4 GiB: one full offset per 256 frames
 };
 

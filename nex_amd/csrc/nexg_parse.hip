@@ -103,9 +103,10 @@ ParseVariant choose_parse_variant(const ParseArgs& a) {
 #define NEXG_SPAN_WPE 5  // span kernel waves per SIMD (its VGPR cap)
 #endif
 
-// The span kernel's NEXG_OUT_GROUPED output: every group mixed (head 0), so
-// from NEXG_GROUPED_CODE_OFFSET on it is NEXG_OUT_SPARSE's layout (codes, then
-// the exceptions at the next 16-B boundary): the SPARSE instance writes it there
+// The span kernel's NEXG_OUT_GROUPED output: every group mixed (head
+// NEXG_GROUPED_TILE_RUN), so from NEXG_GROUPED_CODE_OFFSET on it is
+// NEXG_OUT_SPARSE's layout (codes, then the exceptions at the next 16-B
+// boundary, one run per 256-frame tile): the SPARSE instance writes it there
 // and stores the heads.
 static ParseArgs grouped_as_sparse(const ParseArgs& a) {
     ParseArgs b = a;
@@ -197,9 +198,10 @@ hipError_t launch_parse(ParseVariant v, const ParseArgs& a, int out_kind, hipStr
 // them, past the heads and masks.
 template <bool GROUPED>
 __global__ __launch_bounds__(256) void k_sparse_expand(ParseArgs a, const uint8_t* sparse, nexg_desc* out) {
+    __shared__ uint32_t s_wexc[4];  // GROUPED: each wave's exceptions (a NEXG_GROUPED_TILE_RUN tile's run)
     const uint64_t idx = (uint64_t)blockIdx.x * kTile + threadIdx.x;
     const bool valid = idx < a.count;
-    uint32_t code = 0xFFu;
+    uint32_t code = 0xFFu, head = 0;
     const uint8_t* codes = sparse;
     const nexg_desc* exc = reinterpret_cast<const nexg_desc*>(sparse + NEXG_SPARSE_EXC_OFFSET(a.count));
     if (GROUPED) {
@@ -207,8 +209,8 @@ __global__ __launch_bounds__(256) void k_sparse_expand(ParseArgs a, const uint8_
         exc = reinterpret_cast<const nexg_desc*>(sparse + NEXG_GROUPED_EXC_OFFSET(a.count));
     }
     if (valid) {
-        const uint32_t head = GROUPED ? sparse[idx >> 6] : 0u;
-        if (head) {
+        head = GROUPED ? sparse[idx >> 6] : 0u;
+        if (head && head != NEXG_GROUPED_TILE_RUN) {
             const uint4 m = reinterpret_cast<const uint4*>(sparse + NEXG_GROUPED_MASK_OFFSET(a.count))[idx >> 6];
             const uint32_t b = (uint32_t)idx & 63u;
             const uint32_t ip = b < 32u ? m.x : m.y, l4 = b < 32u ? m.z : m.w;
@@ -219,12 +221,20 @@ __global__ __launch_bounds__(256) void k_sparse_expand(ParseArgs a, const uint8_
         }
     }
     const uint64_t m = __ballot(code == 0u);
+    uint32_t below = 0;  // a tile run: the exceptions of the tile's lower waves
+    if (GROUPED) {
+        if ((threadIdx.x & 63u) == 0u) s_wexc[threadIdx.x >> 6] = (uint32_t)__builtin_popcountll(m);
+        __syncthreads();
+        for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) below += s_wexc[w];
+    }
     if (!valid) return;
     uint64_t off;
     uint32_t len = 0;
     frame_extent(a, idx, off, len);
     nexg_desc d;
-    if (!sparse_decode(code, len, a.opt_flags, a.ip_offset, d)) d = exc[(idx & ~63ull) + lanes_below(m)];
+    if (!sparse_decode(code, len, a.opt_flags, a.ip_offset, d))
+        d = exc[GROUPED && head == NEXG_GROUPED_TILE_RUN ? (idx & ~255ull) + below + lanes_below(m)
+                                                         : (idx & ~63ull) + lanes_below(m)];
     out[idx] = d;
 }
 

@@ -112,7 +112,20 @@ __device__ __forceinline__ void store_sparse_coded(const ParseArgs& a, uint64_t 
     }
     const bool exc = valid && code == 0u;
     const uint64_t m = __ballot(exc);
-    if (exc) x[(idx & ~63ull) + lanes_below(m)] = make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
+    uint64_t slot = (idx & ~63ull) + lanes_below(m);
+    if (OUT == NEXG_OUT_SPARSE && a.grouped_heads) {
+        // the span kernel's grouped output (heads NEXG_GROUPED_TILE_RUN): the
+        // 256-frame tile's exceptions as one run. Every thread of the
+        // workgroup calls this together; each group's exceptions written apart
+        // cost 1.5-3 % on the real-traffic / App. C batches
+        __shared__ uint32_t s_wexc[4];
+        if ((threadIdx.x & 63u) == 0u) s_wexc[threadIdx.x >> 6] = (uint32_t)__builtin_popcountll(m);
+        __syncthreads();
+        uint32_t below = 0;
+        for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) below += s_wexc[w];
+        slot = (idx & ~255ull) + below + lanes_below(m);
+    }
+    if (exc) x[slot] = make_uint2(r.flags, (uint32_t)r.payload_off | ((uint32_t)r.payload_len << 16));
     const uint32_t c1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x55, 0xF, 0xF, false);  // quad_perm 1111
     const uint32_t c2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xAA, 0xF, 0xF, false);  // quad_perm 2222
     const uint32_t c3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xFF, 0xF, 0xF, false);  // quad_perm 3333
@@ -685,11 +698,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const bool have = t < nf;
     // NEXG_OUT_GROUPED runs as the SPARSE instance on the grouped output's
     // code / exception area (the same layout from NEXG_GROUPED_CODE_OFFSET on)
-    // with every group stored mixed: head 0. A GROUPED instance of this kernel
+    // with every group stored mixed: head NEXG_GROUPED_TILE_RUN (the tile's
+    // exceptions in one run, store_sparse_coded). A GROUPED instance of this kernel
     // ran the App. C mix 7 % slower than SPARSE on the same batch (register
     // allocation of the generic section: a spill inside its loop,
     // profiles/r05/grouped_as_sparse/)
-    if (OUT == NEXG_OUT_SPARSE && a.grouped_heads && lane == 0 && have) a.grouped_heads[idx >> 6] = 0;
+    if (OUT == NEXG_OUT_SPARSE && a.grouped_heads && lane == 0 && have) a.grouped_heads[idx >> 6] = NEXG_GROUPED_TILE_RUN;
     if (OUT == NEXG_OUT_GROUPED && lane == 0 && have) reinterpret_cast<uint8_t*>(a.out)[idx >> 6] = 0;
 #if NEXG_SPAN_PF
     // warm this XCD's L2 with the offset table of the group its workgroup
@@ -981,7 +995,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
     }
     // (the span kernel's batches mix shapes: its grouped output stores every
-    // group as a mixed one — head 0, stored at the start — which keeps the
+    // group as a mixed one — head NEXG_GROUPED_TILE_RUN, stored at the start — which keeps the
     // uniformity test and the head store out of the generic section's register
     // budget: with them the App. C mix ran 10 % slower, profiles/r03/grouped)
     NEXG_SPAN_STAMP(4);

@@ -57,8 +57,10 @@ def layouts(frames):
 
 
 def marks(out, n):
-    """per group: stored as a single-shape group (nonzero head byte)"""
-    return out.cpu().numpy()[: (n + 63) >> 6] != 0
+    """per group: stored as a single-shape group (a head byte other than 0
+    and NEXG_GROUPED_TILE_RUN, the two mixed forms)"""
+    h = out.cpu().numpy()[: (n + 63) >> 6]
+    return (h != 0) & (h != abi.GROUPED_TILE_RUN)
 
 
 @pytest.mark.parametrize("opt,mode", MODES, ids=lambda x: str(x))
@@ -78,6 +80,8 @@ def test_grouped_matches_oracle_every_layout(engine, oracle, corpus, opt, mode):
         assert (~h).sum() >= 100
         if name == "lengths":  # the lane kernel stores single-shape groups as such (the span kernel: all mixed)
             assert h.sum() >= 40
+        else:  # the span kernel: every group mixed, exceptions in one run per 256-frame tile
+            assert (raw.cpu().numpy()[: (len(corpus) + 63) >> 6] == abi.GROUPED_TILE_RUN).all()
 
 
 @pytest.mark.parametrize("stride", [64, 128])

@@ -88,15 +88,24 @@ def test_synthetic_workloads_need_no_exceptions(oracle, workload):
         assert set(np.unique(codes & 0xF)) == {1}  # NEXG_SHAPE_V4_UDP
 
 
-def host_grouped_buffer(codes, recs):
+def host_grouped_buffer(codes, recs, tile_run=False):
     """The NEXG_OUT_GROUPED byte layout a kernel writes for these codes
     (include/nexg.h): uniform 64-frame groups as head + verdict masks, the
-    rest as NEXG_OUT_SPARSE codes and exceptions past them."""
+    rest as NEXG_OUT_SPARSE codes and exceptions past them. tile_run: the
+    packed-batch kernel's form, every group mixed with head
+    NEXG_GROUPED_TILE_RUN and each 256-frame tile's exceptions in one run."""
     n = len(codes)
     mask, code, exc_off, total = abi.grouped_offsets(n)
     buf = np.zeros(total, np.uint8)
     exc = buf[exc_off:].view(abi.DESC_DTYPE)
     d = desc_of(recs)
+    if tile_run:
+        buf[:(n + 63) // 64] = abi.GROUPED_TILE_RUN
+        buf[code:code + n] = np.asarray(codes, np.uint8)
+        for t in range(0, n, 256):
+            for k, i in enumerate([i for i in range(t, min(t + 256, n)) if codes[i] == 0]):
+                exc[t + k] = d[i]
+        return buf
     for g in range(0, n, 64):
         c = np.asarray(codes[g:g + 64], np.int64)
         base = c & ~(abi.SPARSE_IP_OK | abi.SPARSE_L4_OK)
@@ -146,3 +155,35 @@ def test_grouped_roundtrip_both_decoders(oracle, corpus, tmp_path):
     buf.tofile(tmp_path / "b.bin")
     out = subprocess.check_output([str(tmp_path / "g"), str(tmp_path / "b.bin"), str(len(frames))]).split()
     assert [int(x) for x in out] == [int(x) for x in codes]
+
+
+def test_grouped_tile_run_both_decoders(oracle, corpus, tmp_path):
+    """The packed-batch kernel's grouped form (heads NEXG_GROUPED_TILE_RUN,
+    each 256-frame tile's exceptions in one run) over the mixed corpus with a
+    partial last tile: the numpy decoder restores every descriptor, and the
+    header's nexg_grouped_exc_slot names each exception's slot."""
+    import os
+    import subprocess
+    frames = corpus[:1000] + corpus[:77]
+    recs = oracle.parse_frames(frames)
+    codes, _, _ = harness.sparse(recs, 0, 0)
+    assert 50 < int((np.asarray(codes) == 0).sum()) < len(frames)  # exceptions in most tiles
+    buf = host_grouped_buffer(codes, recs, tile_run=True)
+    lens = np.array([len(f) for f in frames])
+    helpers.records_equal(abi.grouped_to_desc(buf, len(frames), lens), desc_of(recs), frames, "grouped tile run")
+    assert (abi.grouped_codes(buf, len(frames)) == codes).all()
+    src = tmp_path / "s.c"
+    src.write_text('#include <stdio.h>\n#include <stdlib.h>\n#include "%s"\n'
+                   'int main(int c, char** v) { FILE* f = fopen(v[1], "rb"); static unsigned char b[1 << 22];'
+                   ' if (!f || fread(b, 1, sizeof b, f) == 0) return 2; unsigned long long n = strtoull(v[2], 0, 10);'
+                   ' for (unsigned long long i = 0; i < n; i++) if (nexg_grouped_code(b, n, i) == 0)'
+                   ' printf("%%llu %%llu\\n", i, (unsigned long long)nexg_grouped_exc_slot(b, n, i));'
+                   ' return 0; }\n' % os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                    "include", "nexg.h"))
+    subprocess.check_call(["gcc", "-O1", "-std=c99", "-Wall", "-Werror", "-o", str(tmp_path / "s"), str(src)])
+    buf.tofile(tmp_path / "b.bin")
+    out = subprocess.check_output([str(tmp_path / "s"), str(tmp_path / "b.bin"), str(len(frames))]).split()
+    pairs = [(int(out[k]), int(out[k + 1])) for k in range(0, len(out), 2)]
+    ex = [i for i in range(len(frames)) if codes[i] == 0]
+    want = [(i, i // 256 * 256 + sum(1 for j in ex if i // 256 * 256 <= j < i)) for i in ex]
+    assert pairs == want
