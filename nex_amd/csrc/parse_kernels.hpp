@@ -86,6 +86,9 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // valid lanes share one non-exception code up to the verdict bits stores that
 // code as its head byte and its verdicts as two 64-bit ballots (16 B); any
 // other group stores head 0, then what SPARSE stores, past the heads and masks.
+// The span kernel's grouped output runs as SPARSE with a.grouped_heads set
+// (heads NEXG_GROUPED_TILE_RUN, stored by the caller): its exceptions go in one
+// run per 256-frame tile, and the whole workgroup must call this together.
 template <int OUT, bool GROUP_CHECK = true>
 __device__ __forceinline__ void store_sparse_coded(const ParseArgs& a, uint64_t idx, bool valid,
                                                    const nexg_record& r, uint32_t code) {
