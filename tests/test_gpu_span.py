@@ -88,6 +88,12 @@ def test_packed_bad_extent_group(engine, oracle, mixed):
     assert abi.status_of(np.array([want["flags"][k]]))[0] == abi.ERR_BAD_EXTENT
     got = engine.parse_to_numpy(b2, out_kind=abi.OUT_RECORD)
     helpers.records_equal(got, want, None, "bad extent group")
+    # the fallback group's grouped / sparse stores (a tile run of exceptions in
+    # the grouped form, the per-group run in the sparse one), host-decoded
+    for kind in (abi.OUT_GROUPED, abi.OUT_SPARSE):
+        got_d = engine.parse_to_numpy(b2, out_kind=kind)
+        for n in abi.DESC_DTYPE.names:
+            assert (got_d[n] == want[n]).all(), (kind, n)
 
 
 @pytest.mark.parametrize("stride", [144, 200, 1518])
