@@ -127,7 +127,6 @@ for s in ${STEPS:-tests}; do
     codeab) step code_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_p7.so,abx/libnexg_p1.so,abx/libnexg_p2.so,abx/libnexg_p3.so,abx/libnexg_p4.so,abx/libnexg_p5.so,abx/libnexg_p6.so --workloads imix,real --out grouped --rounds 3 ;;
     tpwab) step tpw_ab 900 python -u tools/bench_parse_ab.py --libs abx/libnexg_t1.so,abx/libnexg_t2.so,abx/libnexg_t1s.so,abx/libnexg_t2s.so --workloads imix,real --out grouped --rounds 3 ;;
     codeat) step code_at 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_at1.so,abx/libnexg_at2.so,abx/libnexg_at3.so --workloads imix,real --out grouped --rounds 3 ;;
-    spantests) step pytest_span 600 python -u -m pytest tests/test_gpu_span.py -q -x --timeout 300 --timeout-method thread ;;
     runtests) step pytest_run 900 python -u -m pytest tests/test_gpu_grouped.py tests/test_gpu_malformed.py tests/test_gpu_span.py tests/test_gpu_tcp_options.py tests/test_gpu_clocks.py tests/test_gpu_tile_order.py tests/test_gpu_parity.py tests/test_cpp_api.py -q -x --timeout 300 --timeout-method thread ;;
     # the driver's own command under the kernel trace: a row for every object of its line (tools/line_trace.py)
     lineprof) step lineprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lineprof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
