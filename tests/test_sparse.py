@@ -148,13 +148,18 @@ def test_grouped_roundtrip_both_decoders(oracle, corpus, tmp_path):
     src.write_text('#include <stdio.h>\n#include <stdlib.h>\n#include "%s"\n'
                    'int main(int c, char** v) { FILE* f = fopen(v[1], "rb"); static unsigned char b[1 << 22];'
                    ' if (!f || fread(b, 1, sizeof b, f) == 0) return 2; unsigned long long n = strtoull(v[2], 0, 10);'
-                   ' for (unsigned long long i = 0; i < n; i++) printf("%%u\\n", nexg_grouped_code(b, n, i));'
+                   ' for (unsigned long long i = 0; i < n; i++) printf("%%u %%llu\\n", nexg_grouped_code(b, n, i),'
+                   ' (unsigned long long)nexg_grouped_exc_slot(b, n, i));'
                    ' return 0; }\n' % os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                    "include", "nexg.h"))
     subprocess.check_call(["gcc", "-O1", "-std=c99", "-Wall", "-Werror", "-o", str(tmp_path / "g"), str(src)])
     buf.tofile(tmp_path / "b.bin")
     out = subprocess.check_output([str(tmp_path / "g"), str(tmp_path / "b.bin"), str(len(frames))]).split()
-    assert [int(x) for x in out] == [int(x) for x in codes]
+    assert [int(x) for x in out[0::2]] == [int(x) for x in codes]
+    # per-group exception slots (heads 0): the group's base + the rank among its code-0 frames
+    ex = [i for i in range(len(frames)) if codes[i] == 0]
+    want = {i: i // 64 * 64 + sum(1 for j in ex if i // 64 * 64 <= j < i) for i in ex}
+    assert all(int(out[2 * i + 1]) == want[i] for i in ex)
 
 
 def test_grouped_tile_run_both_decoders(oracle, corpus, tmp_path):
