@@ -128,8 +128,8 @@ for s in ${STEPS:-tests}; do
     tpwab) step tpw_ab 900 python -u tools/bench_parse_ab.py --libs abx/libnexg_t1.so,abx/libnexg_t2.so,abx/libnexg_t1s.so,abx/libnexg_t2s.so --workloads imix,real --out grouped --rounds 3 ;;
     codeat) step code_at 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_at1.so,abx/libnexg_at2.so,abx/libnexg_at3.so --workloads imix,real --out grouped --rounds 3 ;;
     runtests) step pytest_run 900 python -u -m pytest tests/test_gpu_grouped.py tests/test_gpu_malformed.py tests/test_gpu_span.py tests/test_gpu_tcp_options.py tests/test_gpu_clocks.py tests/test_gpu_tile_order.py tests/test_gpu_parity.py tests/test_cpp_api.py -q -x --timeout 300 --timeout-method thread ;;
-    offnt) step offnt_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_ont.so --tables 32 --workloads imix,imix --out grouped --check --rounds 4 &&
-        step offnt_ab2 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_ont.so --workloads real,mix --out grouped --check --rounds 4 ;;
+    offnt) step offnt_ab 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_vote.so --tables 32 --workloads imix,imix --out grouped --check --rounds 4 &&
+        step offnt_ab2 900 python -u tools/bench_parse_ab.py --libs nex_amd/libnexg.so,abx/libnexg_vote.so --workloads real,mix --out grouped --check --rounds 4 ;;
     driverbench2) step bench_driver_2 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 && step bench_driver_3 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     # the driver's own command under the kernel trace: a row for every object of its line (tools/line_trace.py)
     lineprof) step lineprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lineprof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
